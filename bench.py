@@ -1,0 +1,233 @@
+"""bench.py — GCNConv forward on MI355X: aggregated edges/s + achieved HBM GB/s.
+
+Metric (BASELINE.json): "aggregated edges/sec + achieved HBM GB/s, GCNConv fwd,
+1/2/4/8 MI355X".  A step is one full GCNConv forward (node-level X·W GEMM +
+the fused kgx aggregation with bias epilogue) over a device-resident synthetic
+R-MAT graph.  The graph's CSR/schedule is built once (graph preparation,
+reported separately as graph_build_ms) and reused across steps, as a GNN
+training loop over a fixed graph does.
+
+N = 1 : north-star workload — R-MAT 10M nodes / 100M edges (+10M self loops),
+        F 128 -> 128, fp32.
+N > 1 : one process per GPU (torchrun), weak scaling — every rank owns a
+        contiguous destination range of 10M nodes and ~100M edges of one global
+        R-MAT graph of N x 10M nodes / N x 100M edges; source rows owned by other
+        ranks arrive by a halo all-to-all over RCCL (xGMI) every layer.
+
+Prints ONE JSON line on rank 0.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+for _p in (ROOT, ROOT / "keras-geometric_amd"):
+    if str(_p) not in sys.path:
+        sys.path.insert(0, str(_p))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "aggregated edges/sec + achieved HBM GB/s, GCNConv fwd, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+CONFIGS = {
+    # name: (nodes per GPU, edges per GPU, F_in, F_out)
+    "ns": (10_000_000, 100_000_000, 128, 128),
+    "c2": (1_000_000, 10_000_000, 128, 128),
+    "tiny": (100_000, 1_000_000, 128, 128),
+}
+
+
+def b_alg_spmm(n: int, e_agg: int, f: int, weighted: bool) -> int:
+    """4(N+1) + E_agg (4 col + 4 w + 4F src row) + 4 N F out."""
+    return 4 * (n + 1) + e_agg * (4 + (4 if weighted else 0) + 4 * f) + 4 * n * f
+
+
+def log(msg: str) -> None:
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def cpu_baseline(device: torch.device, seconds_hint: str) -> dict:
+    """Time the oracle's op-for-op Keras-torch CPU GCNConv forward (the reference's
+    CPU path) on a bounded sample: the C2-shaped 1M-node / 10M-edge R-MAT graph."""
+    from keras_geometric_amd import synthetic
+    from oracle import reference as R
+
+    n, e, f = 1_000_000, 10_000_000, 128
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    ei = synthetic.rmat_edge_index(n, e, seed=0, device=device).cpu()
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(n, f, generator=g)
+    w = (torch.rand(f, f, generator=g) * 2 - 1) * (6.0 / (2 * f)) ** 0.5
+    b = torch.zeros(f)
+    t0 = time.perf_counter()
+    y = R.gcn_forward(x, ei, w, b)
+    dt = time.perf_counter() - t0
+    del y
+    return {
+        "value": (e + n) / dt,
+        "unit": "edges/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"oracle GCNConv fwd (Keras-torch CPU lowering, op for op) on R-MAT N={n} E={e} "
+                  f"(+{n} self loops) F {f}->{f}, 1 timed forward = {dt:.2f} s, torch threads={threads}"
+                  f"{seconds_hint}",
+    }
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="ns", choices=sorted(CONFIGS))
+    ap.add_argument("--exact", action="store_true", help="EXACT mode (no hub split)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--seed", type=int, default=0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}; launch N>1 with torch.distributed.run")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import keras_geometric_amd as kgx
+    from keras_geometric_amd import ops as kops
+    from keras_geometric_amd import synthetic
+
+    n_local, e_local, f_in, f_out = CONFIGS[args.config]
+    torch.manual_seed(args.seed + 17 * rank)
+
+    if world == 1:
+        log(f"generating R-MAT N={n_local} E={e_local}")
+        ei = synthetic.rmat_edge_index(n_local, e_local, seed=args.seed, device=dev)
+        x = torch.randn(n_local, f_in, device=dev)
+        layer = kgx.GCNConv(f_out, exact=args.exact)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        layer([x, ei])  # build: weights + CSR + schedule (cached)
+        torch.cuda.synchronize()
+        graph_build_ms = (time.perf_counter() - t0) * 1e3
+        g = next(iter(kgx.graph._CACHE.values()))[1]
+        e_agg, n_rows, max_deg = g.kept, g.n_dst, g.max_degree
+        step = lambda: layer([x, ei])  # noqa: E731
+        shard_info = {}
+    else:
+        from keras_geometric_amd import distributed as kd
+
+        log(f"world={world}: generating shards of R-MAT N={n_local * world} E={e_local * world}")
+        t0 = time.perf_counter()
+        sg = kd.ShardedGraph.rmat(n_local * world, e_local * world, seed=args.seed, device=dev,
+                                  self_loops=True, gcn_norm=True, exact=args.exact)
+        x = torch.randn(sg.n_local, f_in, device=dev)
+        layer = kd.ShardedGCNConv(f_out, sg)
+        layer(x)
+        torch.cuda.synchronize()
+        graph_build_ms = (time.perf_counter() - t0) * 1e3
+        e_agg, n_rows, max_deg = sg.graph.kept, sg.n_local, sg.graph.max_degree
+        step = lambda: layer(x)  # noqa: E731
+        shard_info = {"halo_rows_per_rank": sg.n_halo, "halo_MB_per_layer": sg.n_halo * f_out * 4 / 1e6}
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+    kops.EVENT_SINK = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    events = kops.EVENT_SINK
+    kops.EVENT_SINK = None
+    kern_ms = sum(s.elapsed_time(e) for s, e in events) / max(1, len(events))
+
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+        tot = torch.tensor([e_agg], device=dev, dtype=torch.float64)
+        dist.all_reduce(tot)
+        e_total = float(tot[0])
+    else:
+        e_total = float(e_agg)
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = e_total * args.steps / elapsed
+    balg = b_alg_spmm(n_rows, e_agg, f_out, weighted=True)
+    achieved = balg / (kern_ms * 1e-3) / 1e9
+    result = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "edges/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": f"synthetic R-MAT (a,b,c=.57,.19,.19, seed {args.seed}), x~N(0,1), glorot weights",
+        "config": {
+            "workload": f"GCNConv fwd (X.W GEMM + fused CSR gather-sum, bias), R-MAT "
+                        f"{n_local * world} nodes / {e_local * world} edges (+self loops), "
+                        f"F {f_in}->{f_out}" + (", dst-range shards, RCCL halo all-to-all" if world > 1 else ""),
+            "nodes_per_gpu": n_local,
+            "edges_per_gpu": e_local,
+            "e_agg_per_gpu": e_agg,
+            "max_in_degree": max_deg,
+            "features": [f_in, f_out],
+            "mode": "exact" if args.exact else "split-hub",
+            "parallelism": f"dst-shard{world}" if world > 1 else "single",
+        },
+        "edges_per_s_aggregation_kernel": e_agg * world / (kern_ms * 1e-3),
+        "aggregation_ms": kern_ms,
+        "graph_build_ms": graph_build_ms,
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+            "algorithmic_bytes_per_launch": balg,
+        },
+        **shard_info,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "ns":
+        log("timing the CPU baseline (oracle, C2-sized sample)")
+        del x, layer, ei
+        kgx.clear_cache()
+        torch.cuda.empty_cache()
+        result["cpu_baseline"] = cpu_baseline(dev, "")
+    elif rank == 0:
+        result["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

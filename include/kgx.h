@@ -1,0 +1,198 @@
+/*
+ * kgx.h — C-ABI of the MI355X-native message-passing aggregation engine.
+ *
+ * This is the drop-in boundary for keras-geometric's MessagePassing.propagate()
+ * hot path (edge-index gather -> message -> segment-{sum,mean,max,min,std}
+ * scatter).  Every entry point takes plain device pointers, sizes and a HIP
+ * stream (passed as an opaque pointer so callers need no HIP headers), returns
+ * an int status (KGX_OK == 0) and never allocates or frees memory: buffers are
+ * owned by the caller (the torch caching allocator in the Python host layer).
+ * On failure kgx_last_error() returns a thread-local message.
+ *
+ * Reference citations are relative to the keras-geometric snapshot the survey
+ * studied (src/keras_geometric/...).  The reference itself is pure Python on
+ * Keras-3 ops; each function below names the reference code it replaces.
+ *
+ * Conventions
+ *   - node features are fp32, row-major, leading dimension `ld_*` in elements;
+ *   - edge ids / node ids are int32 (the reference casts edge_index to int32:
+ *     layers/message_passing.py:265, layers/gcn_conv.py:307);
+ *   - E (edges) must be < 2^31 - n_dst; feature offsets are computed in int64.
+ */
+#ifndef KGX_H_
+#define KGX_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* kgx_stream_t; /* a hipStream_t; NULL = the null stream */
+
+enum kgx_status {
+  KGX_OK = 0,
+  KGX_ERR_ARG = 1,         /* bad sizes / null pointers / misalignment      */
+  KGX_ERR_HIP = 2,         /* HIP runtime error (launch, memcpy, ...)        */
+  KGX_ERR_INDEX = 3,       /* an edge index lies outside the node range      */
+  KGX_ERR_UNSUPPORTED = 4  /* shape the kernels do not implement             */
+};
+
+/* Segment reductions: layers/aggregators.py Sum(:119-141) Mean(:48-89)
+ * Max(:92-116) Min(:144-171) Std(:174-232).                                  */
+enum kgx_reduce { KGX_SUM = 0, KGX_MEAN = 1, KGX_MAX = 2, KGX_MIN = 3, KGX_STD = 4 };
+
+/* Fused epilogues applied after the reduction of a destination row.
+ *   BIAS: out = aggr + bias[f]              (GCNConv.update, gcn_conv.py:266-272)
+ *   GIN : out = gin_scale * x[row,f] + aggr (GINConv.update, gin_conv.py:216-222) */
+enum kgx_epilogue { KGX_EPI_NONE = 0, KGX_EPI_BIAS = 1, KGX_EPI_GIN = 2 };
+
+/* Graph-preparation flags. */
+enum kgx_csr_flags {
+  KGX_CSR_SELF_LOOPS = 1, /* append (i,i) after the E input edges: utils/main.py:8-16    */
+  KGX_CSR_SEGMENT_ONLY = 2, /* segment semantics only (Aggregator.aggregate called directly,
+                               aggregators.py:24-39): ids outside [0,n_dst) are dropped,
+                               src is not validated                                       */
+  KGX_CSR_GCN_NORM = 4    /* also produce dinv[n_dst] and per-CSR-edge weight w:
+                               utils/main.py:20-33                                        */
+};
+
+int kgx_version(void);
+const char* kgx_last_error(void);
+
+/* ---------------------------------------------------------------------------
+ * Graph preparation: COO int32 [2,E] (generation order, unsorted) -> CSR by
+ * destination, STABLE (edges of one destination keep their input order, the
+ * self-loop is last), which is the order the reference's segment_sum
+ * (Keras-torch scatter_add) accumulates in.
+ *
+ * Replaces: MessagePassing.call edge_index cast/cache (message_passing.py:256-268),
+ *           add_self_loops (utils/main.py:8-16), the degree segment_sum of
+ *           compute_gcn_normalization (utils/main.py:23-24) and of
+ *           MeanAggregator (aggregators.py:66-69).
+ *
+ * Index semantics (Keras-3 torch lowering of take/segment_sum):
+ *   src in [-n_src, n_src): negative ids wrap (+n_src), else KGX_ERR_INDEX;
+ *   dst in [-n_dst, n_dst): negative ids are dropped from every segment
+ *   reduction (and from degrees), else KGX_ERR_INDEX.
+ *   With KGX_CSR_SEGMENT_ONLY every dst outside [0,n_dst) is dropped.
+ * Outputs (caller-allocated, capacity E + n_dst when SELF_LOOPS else E):
+ *   rowptr[n_dst+1], col[cap] (source id per CSR slot), eid[cap] (input edge
+ *   id per CSR slot; self loop i has id E+i), deg[n_dst] (int32 in-degree),
+ *   optional dinv[n_dst] and w[cap] (KGX_CSR_GCN_NORM).
+ * info[4] (host) receives: kept edges, max in-degree, #bad indices, 0.
+ * This call synchronises `stream` once (to return info).
+ * ------------------------------------------------------------------------- */
+int kgx_csr_workspace_bytes(int64_t E, int64_t n_dst, int flags, size_t* bytes);
+int kgx_csr_build(const int32_t* src, const int32_t* dst, int64_t E,
+                  int64_t n_src, int64_t n_dst, int flags,
+                  int32_t* rowptr, int32_t* col, int32_t* eid, int32_t* deg,
+                  float* dinv, float* w,
+                  void* workspace, size_t workspace_bytes,
+                  int64_t* info, kgx_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Row schedule (no reference counterpart: the reference has one device and no
+ * scheduling).  Orders destination rows by descending degree (log2 buckets,
+ * stable) so hub rows start first, and cuts rows with deg >= split_len into
+ * split_len-edge chunks whose partials are combined in chunk order.
+ *   rows[n_dst]              row ids in schedule order (EXACT mode iterates these)
+ *   items[4*cap_items]       {row, edge_begin, edge_end, partial_slot|-1}
+ *   split[4*n_dst]           {row, first_slot, n_chunks, degree} for split rows
+ * cap_items must be >= n_dst + E_kept / split_len + 1.  split_len <= 0 means
+ * never split.  info[4] (host): n_items, n_split_rows, n_slots, 0.  Syncs once.
+ * ------------------------------------------------------------------------- */
+int kgx_schedule_workspace_bytes(int64_t n_dst, size_t* bytes);
+int kgx_schedule_build(const int32_t* rowptr, int64_t n_dst, int32_t split_len,
+                       int32_t* rows, int32_t* items, int64_t cap_items,
+                       int32_t* split, void* workspace, size_t workspace_bytes,
+                       int64_t* info, kgx_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Fused gather -> (weight) -> segment reduction -> epilogue, one launch.
+ *   out[row, f] = EPI( REDUCE_{e in CSR row} table[idx[e], f] * (w ? w[e] : 1) )
+ *
+ * Replaces: MessagePassing.propagate's take(x_j, src) (message_passing.py:195),
+ *   the default/GCN/GIN/SAGE message (message_passing.py:73-77, gcn_conv.py:233-248,
+ *   gin_conv.py:193, sage_conv.py:294-298), MessagePassing.aggregate ->
+ *   Aggregator.aggregate (message_passing.py:79-102, aggregators.py:48-232) and
+ *   the GCN/GIN update epilogues.
+ * With idx = col and table = node features it is the node-gather SpMM; with
+ *   idx = eid and table = a per-edge message tensor [E,F] it is the reference's
+ *   Aggregator.aggregate(messages, target_idx, dim_size) on arbitrary messages.
+ * Work list: if items != NULL the (possibly split) item list of
+ *   kgx_schedule_build is used and split rows are finished by an in-call fix-up
+ *   (partials: n_slots*F floats); otherwise every row of `rows` is reduced
+ *   sequentially in CSR order (EXACT: bit-identical to the reference's
+ *   sequential scatter_add / scatter_reduce for identical messages).
+ * KGX_STD ignores items (always EXACT, two sequential passes per row).
+ * ------------------------------------------------------------------------- */
+int kgx_spmm(int reduce, int epilogue,
+             const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
+             const int32_t* items, int64_t n_items,
+             const int32_t* split, int64_t n_split,
+             const int32_t* idx, const float* w,
+             const float* table, int64_t ld_table, int64_t F,
+             float* out, int64_t ld_out,
+             const float* bias, const float* xroot, int64_t ld_x, float gin_scale,
+             float* partials, kgx_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Fused GATv2 attention aggregation (single pass, online segment softmax).
+ *   s[e,h]  = sum_c att[h,c] * leaky_relu(h_dst[i,h,c] + h_src[j,h,c], slope)
+ *   alpha   = exp(s - max_i) / (sum_i exp(s - max_i) + 1e-10)
+ *   out[i,h,c] = sum_e alpha[e,h] * h_src[j,h,c]  (+ bias[h*C+c] if bias)
+ * Replaces GATv2Conv._gatv2_propagate's gathers, _compute_attention,
+ *   _softmax_by_target, alpha*h_j, _aggregate_messages and the concat-mode
+ *   _final_update (gatv2_conv.py:241-266, 268-311, 313-335, 337-352).
+ * h_src/h_dst: [n, heads*channels] row-major with leading dimension ld_h.
+ * partials: n_slots * (heads*channels + 2*heads) floats when items are split.
+ * ------------------------------------------------------------------------- */
+int kgx_gatv2(const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
+              const int32_t* items, int64_t n_items,
+              const int32_t* split, int64_t n_split,
+              const int32_t* col, const float* h_src, const float* h_dst, int64_t ld_h,
+              const float* att, int heads, int channels, float negative_slope,
+              float* out, int64_t ld_out, const float* bias,
+              float* partials, kgx_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Row gather out[i,:] = table[rows[i], :] — packs halo rows for the multi-GPU
+ * exchange (no reference counterpart; the reference is single-device) and
+ * scatters per-edge values back to input edge order.
+ * ------------------------------------------------------------------------- */
+int kgx_gather_rows(const float* table, int64_t ld_table, const int32_t* rows,
+                    int64_t n, int64_t F, float* out, int64_t ld_out,
+                    kgx_stream_t stream);
+/* out[perm[i]] = in[i] for i < n (int32 perm) — CSR-order -> input-order. */
+int kgx_scatter_f32(const float* in, const int32_t* perm, int64_t n, float* out,
+                    kgx_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Synthetic R-MAT edge generator (bench/test input; the reference has no
+ * generator — its perf tests use numpy.random, tests/performance/
+ * test_large_graphs.py:86-110).  Counter-based and bit-reproducible: edge k of
+ * (seed, scale, a, b, c) is the same on every device and in the numpy
+ * restatement (oracle/rmat.py).  Probabilities are 24-bit fixed point
+ * (p * 2^24).  Raw ids (mod n_nodes) are relabelled by a keyed Feistel
+ * permutation.  Writes edges [e_begin, e_begin + e_count).
+ * ------------------------------------------------------------------------- */
+int kgx_rmat_edges(uint64_t seed, int scale, int64_t n_nodes,
+                   uint32_t a24, uint32_t b24, uint32_t c24,
+                   int64_t e_begin, int64_t e_count,
+                   int32_t* src, int32_t* dst, kgx_stream_t stream);
+
+/* Keep edges whose dst lies in [lo, hi): stream compaction used to carve one
+ * rank's destination-range shard out of a generated batch.  n_out (host)
+ * receives the count; out arrays need capacity n.  Syncs once.               */
+int kgx_select_dst_range(const int32_t* src, const int32_t* dst, int64_t n,
+                         int64_t lo, int64_t hi, int32_t* src_out, int32_t* dst_out,
+                         void* workspace, size_t workspace_bytes, int64_t* n_out,
+                         kgx_stream_t stream);
+int kgx_select_workspace_bytes(int64_t n, size_t* bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KGX_H_ */

@@ -1,0 +1,614 @@
+// Graph preparation for the kgx aggregation engine (gfx950).
+//
+//   COO [2,E] -> stable CSR by destination  (kgx_csr_build)
+//   degree-ordered row schedule + hub split (kgx_schedule_build)
+//   R-MAT synthetic edges                    (kgx_rmat_edges)
+//   dst-range shard selection, row gather, scatter utilities
+//
+// The CSR order is the order the reference accumulates in: Keras-3's torch
+// segment_sum is `scatter_add` over edges in input order (probed: bit-identical
+// to sequential accumulation), so a STABLE sort by destination reproduces the
+// per-destination message sequence, and add_self_loops (utils/main.py:8-16)
+// appends loop i after all input edges, i.e. last in row i.
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+#include "kgx_internal.h"
+
+namespace kgx {
+namespace {
+
+// --------------------------------------------------------------------------
+// CSR build kernels
+// --------------------------------------------------------------------------
+struct CsrStatus {
+  unsigned long long bad;      // out-of-range indices
+  unsigned long long max_deg;  // max in-degree
+  unsigned long long kept;     // rowptr[n_dst]
+  unsigned long long pad;
+};
+
+__global__ void csr_prep_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
+                                int64_t E, int64_t n_src, int64_t n_dst, int flags,
+                                uint32_t* __restrict__ keys, int32_t* __restrict__ vals,
+                                int32_t* __restrict__ srcn, CsrStatus* __restrict__ st) {
+  const bool segment_only = flags & KGX_CSR_SEGMENT_ONLY;
+  const bool loops = flags & KGX_CSR_SELF_LOOPS;
+  const int64_t total = E + (loops ? n_dst : 0);
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  unsigned long long bad = 0;
+  for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < total; e += stride) {
+    if (e < E) {
+      int64_t s = src[e];
+      int64_t d = dst[e];
+      bool keep;
+      if (segment_only) {
+        // segment_sum semantics: ids < 0 or >= num_segments go to a dropped bucket
+        keep = (d >= 0) && (d < n_dst);
+      } else {
+        // take(x, idx): negative ids wrap, ids outside [-n, n) raise
+        const bool bad_e = (s < -n_src) || (s >= n_src) || (d < -n_dst) || (d >= n_dst);
+        bad += bad_e;
+        keep = !bad_e && d >= 0;
+        if (s < 0) s += n_src;
+      }
+      keys[e] = keep ? uint32_t(d) : uint32_t(n_dst);
+      vals[e] = int32_t(e);
+      srcn[e] = int32_t(s);
+    } else {
+      const int64_t i = e - E;
+      keys[e] = uint32_t(i);
+      vals[e] = int32_t(e);
+      srcn[e] = int32_t(i);
+    }
+  }
+  if (bad) atomicAdd(&st->bad, bad);
+}
+
+// rowptr[r] = lower_bound(keys_sorted, r) for r in [0, n_dst]
+__global__ void csr_rowptr_kernel(const uint32_t* __restrict__ keys, int64_t total, int64_t n_dst,
+                                  int32_t* __restrict__ rowptr, CsrStatus* __restrict__ st) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  for (int64_t r = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; r <= n_dst; r += stride) {
+    int64_t lo = 0, hi = total;
+    const uint32_t key = uint32_t(r);
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (keys[mid] < key) lo = mid + 1; else hi = mid;
+    }
+    rowptr[r] = int32_t(lo);
+    if (r == n_dst) st->kept = (unsigned long long)lo;
+  }
+}
+
+__global__ void csr_col_kernel(const int32_t* __restrict__ eid, const int32_t* __restrict__ srcn,
+                               const int32_t* __restrict__ rowptr, int64_t n_dst,
+                               int32_t* __restrict__ col) {
+  const int64_t kept = rowptr[n_dst];
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < kept; e += stride)
+    col[e] = srcn[eid[e]];
+}
+
+// Integer in-degree; fp32 degree as the reference computes it: a sequential
+// fp32 sum of ones (utils/main.py:23-24, aggregators.py:66-69) saturates at 2^24.
+__device__ __forceinline__ float ref_degree_f32(int32_t deg) {
+  return float(deg < (1 << 24) ? deg : (1 << 24));
+}
+
+__global__ void csr_deg_kernel(const int32_t* __restrict__ rowptr, int64_t n_dst, int flags,
+                               int32_t* __restrict__ deg, float* __restrict__ dinv,
+                               CsrStatus* __restrict__ st) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  unsigned long long mx = 0;
+  for (int64_t r = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; r < n_dst; r += stride) {
+    const int32_t d = rowptr[r + 1] - rowptr[r];
+    deg[r] = d;
+    mx = d > (int64_t)mx ? (unsigned long long)d : mx;
+    if (flags & KGX_CSR_GCN_NORM) {
+      // pow(deg + 1e-12, -0.5), correctly rounded (= 1/sqrt in IEEE RN); deg 0 -> 1e6.
+      // (torch's tensor-exponent powf may differ by 1 ulp: DESIGN.md "GCN norm".)
+      const float x = __fadd_rn(ref_degree_f32(d), 1e-12f);
+      dinv[r] = __fdiv_rn(1.0f, __fsqrt_rn(x));
+    }
+  }
+  // wave max then one atomic per wave
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned long long other = __shfl_xor(mx, o, 64);
+    mx = other > mx ? other : mx;
+  }
+  if ((threadIdx.x & 63) == 0 && mx) atomicMax(&st->max_deg, mx);
+}
+
+// norm_e = dinv[dst] * dinv[src]  (utils/main.py:29-32; take(dinv,target)*take(dinv,source))
+__global__ void csr_norm_kernel(const uint32_t* __restrict__ keys_sorted, const int32_t* __restrict__ col,
+                                const int32_t* __restrict__ rowptr, int64_t n_dst,
+                                const float* __restrict__ dinv, float* __restrict__ w) {
+  const int64_t kept = rowptr[n_dst];
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < kept; e += stride)
+    w[e] = __fmul_rn(dinv[keys_sorted[e]], dinv[col[e]]);
+}
+
+size_t sort_temp_bytes(int64_t n, int end_bit) {
+  size_t bytes = 0;
+  uint32_t* k = nullptr;
+  int32_t* v = nullptr;
+  (void)rocprim::radix_sort_pairs(nullptr, bytes, k, k, v, v, (unsigned)n, 0, end_bit, 0, false);
+  return bytes;
+}
+
+struct CsrLayout {
+  uint32_t* keys;
+  uint32_t* keys_sorted;
+  int32_t* vals;
+  int32_t* srcn;
+  CsrStatus* st;
+  void* sort_tmp;
+  size_t sort_bytes;
+  size_t total;
+};
+
+CsrLayout csr_layout(void* ws, int64_t total, int64_t n_dst) {
+  Carve c(ws, ~size_t(0));
+  CsrLayout L;
+  L.keys = c.take<uint32_t>(total);
+  L.keys_sorted = c.take<uint32_t>(total);
+  L.vals = c.take<int32_t>(total);
+  L.srcn = c.take<int32_t>(total);
+  L.st = c.take<CsrStatus>(1);
+  const int end_bit = ceil_log2_u64(uint64_t(n_dst) + 1);
+  L.sort_bytes = sort_temp_bytes(total, end_bit > 0 ? end_bit : 1);
+  L.sort_tmp = c.take<char>(L.sort_bytes);
+  L.total = c.used();
+  return L;
+}
+
+// --------------------------------------------------------------------------
+// Schedule kernels
+// --------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t degree_bucket_key(int32_t d) {
+  // bucket b = floor(log2 d) + 1 (0 for d == 0); key 32 - b sorts descending.
+  const uint32_t b = d > 0 ? 32u - __clz(uint32_t(d)) : 0u;
+  return 32u - b;
+}
+
+__global__ void sched_keys_kernel(const int32_t* __restrict__ rowptr, int64_t n_dst,
+                                  uint32_t* __restrict__ keys, int32_t* __restrict__ iota) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  for (int64_t r = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; r < n_dst; r += stride) {
+    keys[r] = degree_bucket_key(rowptr[r + 1] - rowptr[r]);
+    iota[r] = int32_t(r);
+  }
+}
+
+__global__ void sched_count_kernel(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ rows,
+                                   int64_t n_dst, int32_t split_len, int32_t* __restrict__ nchunks,
+                                   int32_t* __restrict__ nslots) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n_dst; i += stride) {
+    const int32_t r = rows[i];
+    const int32_t d = rowptr[r + 1] - rowptr[r];
+    const bool split = split_len > 0 && d >= split_len;
+    const int32_t nc = split ? (d + split_len - 1) / split_len : 1;
+    nchunks[i] = nc;
+    nslots[i] = split ? nc : 0;
+  }
+}
+
+struct SchedStatus {
+  unsigned long long n_items;
+  unsigned long long n_split;
+  unsigned long long n_slots;
+  unsigned long long overflow;
+};
+
+__global__ void sched_emit_kernel(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ rows,
+                                  int64_t n_dst, int32_t split_len,
+                                  const int32_t* __restrict__ nchunks, const int32_t* __restrict__ item_off,
+                                  const int32_t* __restrict__ nslots, const int32_t* __restrict__ slot_off,
+                                  int4* __restrict__ items, int64_t cap_items, int4* __restrict__ split,
+                                  SchedStatus* __restrict__ st) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  unsigned long long nsplit = 0;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n_dst; i += stride) {
+    const int32_t r = rows[i];
+    const int32_t beg = rowptr[r];
+    const int32_t end = rowptr[r + 1];
+    const int32_t nc = nchunks[i];
+    const int32_t off = item_off[i];
+    if (int64_t(off) + nc > cap_items) {
+      atomicAdd(&st->overflow, 1ull);
+      continue;
+    }
+    if (nslots[i] > 0) {
+      const int32_t s0 = slot_off[i];
+      for (int32_t c = 0; c < nc; ++c) {
+        const int32_t b = beg + c * split_len;
+        const int32_t e = min(end, b + split_len);
+        items[off + c] = make_int4(r, b, e, s0 + c);
+      }
+      split[i] = make_int4(r, s0, nc, end - beg);  // split rows are a schedule prefix
+      ++nsplit;
+    } else {
+      items[off] = make_int4(r, beg, end, -1);
+    }
+    if (i == n_dst - 1) {
+      st->n_items = (unsigned long long)(off + nc);
+      st->n_slots = (unsigned long long)(slot_off[i] + nslots[i]);
+    }
+  }
+  if (nsplit) atomicAdd(&st->n_split, nsplit);
+}
+
+struct SchedLayout {
+  uint32_t* keys;
+  uint32_t* keys_sorted;
+  int32_t* iota;
+  int32_t* nchunks;
+  int32_t* item_off;
+  int32_t* nslots;
+  int32_t* slot_off;
+  SchedStatus* st;
+  void* tmp;
+  size_t tmp_bytes;
+  size_t total;
+};
+
+SchedLayout sched_layout(void* ws, int64_t n) {
+  Carve c(ws, ~size_t(0));
+  SchedLayout L;
+  L.keys = c.take<uint32_t>(n);
+  L.keys_sorted = c.take<uint32_t>(n);
+  L.iota = c.take<int32_t>(n);
+  L.nchunks = c.take<int32_t>(n);
+  L.item_off = c.take<int32_t>(n);
+  L.nslots = c.take<int32_t>(n);
+  L.slot_off = c.take<int32_t>(n);
+  L.st = c.take<SchedStatus>(1);
+  size_t sb = sort_temp_bytes(n, 6);
+  size_t scb = 0;
+  const int32_t* si = nullptr;
+  int32_t* so = nullptr;
+  (void)rocprim::exclusive_scan(nullptr, scb, si, so, 0, (size_t)n, rocprim::plus<int32_t>(), 0, false);
+  L.tmp_bytes = sb > scb ? sb : scb;
+  L.tmp = c.take<char>(L.tmp_bytes);
+  L.total = c.used();
+  return L;
+}
+
+// --------------------------------------------------------------------------
+// R-MAT generator (counter-based; restated bit-for-bit in oracle/rmat.py)
+// --------------------------------------------------------------------------
+__device__ __host__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+struct Feistel {
+  uint64_t keys[4];
+  int hb;          // half width in bits
+  uint64_t mask;   // (1 << hb) - 1
+};
+
+__device__ __forceinline__ uint64_t feistel_once(const Feistel& f, uint64_t x) {
+  uint64_t L = x >> f.hb, R = x & f.mask;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint64_t nl = R;
+    R = L ^ (splitmix64(f.keys[i] ^ R) & f.mask);
+    L = nl;
+  }
+  return (L << f.hb) | R;
+}
+
+__device__ __forceinline__ uint64_t relabel(const Feistel& f, uint64_t x, uint64_t n) {
+  uint64_t y = feistel_once(f, x);
+  while (y >= n) y = feistel_once(f, y);  // cycle walking: terminates (bijection on a superset)
+  return y;
+}
+
+__global__ void rmat_kernel(uint64_t base, Feistel fs, int scale, uint64_t n,
+                            uint32_t ta, uint32_t tab, uint32_t tabc,
+                            int64_t e_begin, int64_t e_count,
+                            int32_t* __restrict__ src, int32_t* __restrict__ dst) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < e_count; i += stride) {
+    const uint64_t k = uint64_t(e_begin + i);
+    uint64_t s = 0, d = 0;
+    for (int l = 0; l < scale; ++l) {
+      const uint32_t r = uint32_t(splitmix64(base + k * 64ull + uint64_t(l)) >> 40);
+      const uint32_t sb = r >= tab;                       // quadrants c, d
+      const uint32_t db = (r >= ta && r < tab) || r >= tabc;  // quadrants b, d
+      s = (s << 1) | sb;
+      d = (d << 1) | db;
+    }
+    src[i] = int32_t(relabel(fs, s % n, n));
+    dst[i] = int32_t(relabel(fs, d % n, n));
+  }
+}
+
+// --------------------------------------------------------------------------
+// small utilities
+// --------------------------------------------------------------------------
+__global__ void range_flags_kernel(const int32_t* __restrict__ dst, int64_t n, int64_t lo, int64_t hi,
+                                   int32_t* __restrict__ flags) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t d = dst[i];
+    flags[i] = (d >= lo && d < hi) ? 1 : 0;
+  }
+}
+
+__global__ void range_scatter_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
+                                     const int32_t* __restrict__ flags, const int32_t* __restrict__ pos,
+                                     int64_t n, int32_t* __restrict__ so, int32_t* __restrict__ dout,
+                                     unsigned long long* __restrict__ count) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    if (flags[i]) {
+      so[pos[i]] = src[i];
+      dout[pos[i]] = dst[i];
+    }
+    if (i == n - 1) *count = (unsigned long long)(pos[i] + flags[i]);
+  }
+}
+
+template <int VEC>
+__global__ void gather_rows_kernel(const float* __restrict__ table, int64_t ld_t,
+                                   const int32_t* __restrict__ rows, int64_t n, int64_t F,
+                                   float* __restrict__ out, int64_t ld_o) {
+  using V = typename std::conditional<VEC == 4, float4, float>::type;
+  const int64_t nv = F / VEC;
+  const int64_t total = n * nv;
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  for (int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; t < total; t += stride) {
+    const int64_t i = t / nv, j = t - i * nv;
+    const V v = *reinterpret_cast<const V*>(table + int64_t(rows[i]) * ld_t + j * VEC);
+    *reinterpret_cast<V*>(out + i * ld_o + j * VEC) = v;
+  }
+}
+
+__global__ void scatter_f32_kernel(const float* __restrict__ in, const int32_t* __restrict__ perm, int64_t n,
+                                   float* __restrict__ out) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
+    out[perm[i]] = in[i];
+}
+
+}  // namespace
+}  // namespace kgx
+
+using namespace kgx;
+
+extern "C" int kgx_csr_workspace_bytes(int64_t E, int64_t n_dst, int flags, size_t* bytes) {
+  KGX_REQUIRE(bytes && E >= 0 && n_dst >= 0, KGX_ERR_ARG, "kgx_csr_workspace_bytes: bad arguments");
+  const int64_t total = E + ((flags & KGX_CSR_SELF_LOOPS) ? n_dst : 0);
+  *bytes = csr_layout(nullptr, total, n_dst).total;
+  return KGX_OK;
+}
+
+extern "C" int kgx_csr_build(const int32_t* src, const int32_t* dst, int64_t E, int64_t n_src,
+                             int64_t n_dst, int flags, int32_t* rowptr, int32_t* col, int32_t* eid,
+                             int32_t* deg, float* dinv, float* w, void* workspace,
+                             size_t workspace_bytes, int64_t* info, kgx_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  const bool loops = flags & KGX_CSR_SELF_LOOPS;
+  const bool norm = flags & KGX_CSR_GCN_NORM;
+  KGX_REQUIRE(E >= 0 && n_dst >= 0 && n_src >= 0, KGX_ERR_ARG, "kgx_csr_build: negative sizes");
+  KGX_REQUIRE(!loops || n_src == n_dst, KGX_ERR_ARG,
+              "kgx_csr_build: self loops need n_src == n_dst (got %lld, %lld)", (long long)n_src,
+              (long long)n_dst);
+  const int64_t total = E + (loops ? n_dst : 0);
+  KGX_REQUIRE(total < (int64_t(1) << 31) - 1 && n_dst < (int64_t(1) << 31) - 1, KGX_ERR_ARG,
+              "kgx_csr_build: graph too large for int32 CSR (E'=%lld)", (long long)total);
+  KGX_REQUIRE(rowptr && deg && (total == 0 || (col && eid)), KGX_ERR_ARG, "kgx_csr_build: null output");
+  KGX_REQUIRE(E == 0 || (src && dst), KGX_ERR_ARG, "kgx_csr_build: null input");
+  KGX_REQUIRE(!norm || (dinv && (total == 0 || w)), KGX_ERR_ARG, "kgx_csr_build: GCN_NORM needs dinv and w");
+  CsrLayout L = csr_layout(workspace, total, n_dst);
+  KGX_REQUIRE(workspace && workspace_bytes >= L.total, KGX_ERR_ARG,
+              "kgx_csr_build: workspace %zu < %zu bytes", workspace_bytes, L.total);
+
+  KGX_CHECK_HIP(hipMemsetAsync(L.st, 0, sizeof(CsrStatus), stream));
+  if (total > 0) {
+    hipLaunchKernelGGL(csr_prep_kernel, dim3(grid_for(total, 8192)), dim3(kBlock), 0, stream, src, dst, E,
+                       n_src, n_dst, flags, L.keys, L.vals, L.srcn, L.st);
+    KGX_CHECK_LAUNCH();
+    const int end_bit = ceil_log2_u64(uint64_t(n_dst) + 1);
+    size_t sb = L.sort_bytes;
+    KGX_CHECK_HIP(rocprim::radix_sort_pairs(L.sort_tmp, sb, L.keys, L.keys_sorted, L.vals, eid,
+                                            (unsigned)total, 0, end_bit > 0 ? end_bit : 1, stream,
+                                            false));
+  }
+  hipLaunchKernelGGL(csr_rowptr_kernel, dim3(grid_for(n_dst + 1, 8192)), dim3(kBlock), 0, stream,
+                     L.keys_sorted, total, n_dst, rowptr, L.st);
+  KGX_CHECK_LAUNCH();
+  if (total > 0) {
+    hipLaunchKernelGGL(csr_col_kernel, dim3(grid_for(total, 8192)), dim3(kBlock), 0, stream, eid, L.srcn,
+                       rowptr, n_dst, col);
+    KGX_CHECK_LAUNCH();
+  }
+  if (n_dst > 0) {
+    hipLaunchKernelGGL(csr_deg_kernel, dim3(grid_for(n_dst, 8192)), dim3(kBlock), 0, stream, rowptr, n_dst,
+                       flags, deg, dinv, L.st);
+    KGX_CHECK_LAUNCH();
+  }
+  if (norm && total > 0) {
+    hipLaunchKernelGGL(csr_norm_kernel, dim3(grid_for(total, 8192)), dim3(kBlock), 0, stream,
+                       L.keys_sorted, col, rowptr, n_dst, dinv, w);
+    KGX_CHECK_LAUNCH();
+  }
+  CsrStatus hs;
+  KGX_CHECK_HIP(hipMemcpyAsync(&hs, L.st, sizeof(CsrStatus), hipMemcpyDeviceToHost, stream));
+  KGX_CHECK_HIP(hipStreamSynchronize(stream));
+  if (info) {
+    info[0] = int64_t(hs.kept);
+    info[1] = int64_t(hs.max_deg);
+    info[2] = int64_t(hs.bad);
+    info[3] = 0;
+  }
+  KGX_REQUIRE(hs.bad == 0, KGX_ERR_INDEX,
+              "index out of range in edge_index: %llu edge(s) reference a node outside "
+              "[-n, n) (n_src=%lld, n_dst=%lld)",
+              hs.bad, (long long)n_src, (long long)n_dst);
+  return KGX_OK;
+}
+
+extern "C" int kgx_schedule_workspace_bytes(int64_t n_dst, size_t* bytes) {
+  KGX_REQUIRE(bytes && n_dst >= 0, KGX_ERR_ARG, "kgx_schedule_workspace_bytes: bad arguments");
+  *bytes = sched_layout(nullptr, n_dst).total;
+  return KGX_OK;
+}
+
+extern "C" int kgx_schedule_build(const int32_t* rowptr, int64_t n_dst, int32_t split_len, int32_t* rows,
+                                  int32_t* items, int64_t cap_items, int32_t* split, void* workspace,
+                                  size_t workspace_bytes, int64_t* info, kgx_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  KGX_REQUIRE(rowptr && n_dst >= 0, KGX_ERR_ARG, "kgx_schedule_build: bad arguments");
+  KGX_REQUIRE(split_len <= 0 || (split_len & (split_len - 1)) == 0, KGX_ERR_ARG,
+              "kgx_schedule_build: split_len must be a power of two (got %d)", split_len);
+  if (n_dst == 0) {
+    if (info) info[0] = info[1] = info[2] = info[3] = 0;
+    return KGX_OK;
+  }
+  KGX_REQUIRE(rows && items && split, KGX_ERR_ARG, "kgx_schedule_build: null output");
+  SchedLayout L = sched_layout(workspace, n_dst);
+  KGX_REQUIRE(workspace && workspace_bytes >= L.total, KGX_ERR_ARG,
+              "kgx_schedule_build: workspace %zu < %zu bytes", workspace_bytes, L.total);
+  KGX_CHECK_HIP(hipMemsetAsync(L.st, 0, sizeof(SchedStatus), stream));
+  const unsigned g = grid_for(n_dst, 8192);
+  hipLaunchKernelGGL(sched_keys_kernel, dim3(g), dim3(kBlock), 0, stream, rowptr, n_dst, L.keys, L.iota);
+  KGX_CHECK_LAUNCH();
+  size_t tb = L.tmp_bytes;
+  KGX_CHECK_HIP(rocprim::radix_sort_pairs(L.tmp, tb, L.keys, L.keys_sorted, L.iota, rows, (unsigned)n_dst, 0,
+                                          6, stream, false));
+  hipLaunchKernelGGL(sched_count_kernel, dim3(g), dim3(kBlock), 0, stream, rowptr, rows, n_dst, split_len,
+                     L.nchunks, L.nslots);
+  KGX_CHECK_LAUNCH();
+  tb = L.tmp_bytes;
+  KGX_CHECK_HIP(rocprim::exclusive_scan(L.tmp, tb, (const int32_t*)L.nchunks, L.item_off, 0, (size_t)n_dst,
+                                        rocprim::plus<int32_t>(), stream, false));
+  tb = L.tmp_bytes;
+  KGX_CHECK_HIP(rocprim::exclusive_scan(L.tmp, tb, (const int32_t*)L.nslots, L.slot_off, 0, (size_t)n_dst,
+                                        rocprim::plus<int32_t>(), stream, false));
+  hipLaunchKernelGGL(sched_emit_kernel, dim3(g), dim3(kBlock), 0, stream, rowptr, rows, n_dst, split_len,
+                     L.nchunks, L.item_off, L.nslots, L.slot_off, reinterpret_cast<int4*>(items), cap_items,
+                     reinterpret_cast<int4*>(split), L.st);
+  KGX_CHECK_LAUNCH();
+  SchedStatus hs;
+  KGX_CHECK_HIP(hipMemcpyAsync(&hs, L.st, sizeof(SchedStatus), hipMemcpyDeviceToHost, stream));
+  KGX_CHECK_HIP(hipStreamSynchronize(stream));
+  KGX_REQUIRE(hs.overflow == 0, KGX_ERR_ARG, "kgx_schedule_build: cap_items %lld too small",
+              (long long)cap_items);
+  if (info) {
+    info[0] = int64_t(hs.n_items);
+    info[1] = int64_t(hs.n_split);
+    info[2] = int64_t(hs.n_slots);
+    info[3] = 0;
+  }
+  return KGX_OK;
+}
+
+extern "C" int kgx_rmat_edges(uint64_t seed, int scale, int64_t n_nodes, uint32_t a24, uint32_t b24,
+                              uint32_t c24, int64_t e_begin, int64_t e_count, int32_t* src, int32_t* dst,
+                              kgx_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  KGX_REQUIRE(scale > 0 && scale <= 62 && n_nodes > 0 && n_nodes <= (int64_t(1) << scale) &&
+                  n_nodes < (int64_t(1) << 31),
+              KGX_ERR_ARG, "kgx_rmat_edges: need 0 < n_nodes <= 2^scale < 2^31 (scale=%d, n=%lld)", scale,
+              (long long)n_nodes);
+  KGX_REQUIRE(uint64_t(a24) + b24 + c24 <= (1u << 24), KGX_ERR_ARG, "kgx_rmat_edges: a+b+c > 1");
+  KGX_REQUIRE(e_count >= 0 && e_begin >= 0 && (e_count == 0 || (src && dst)), KGX_ERR_ARG,
+              "kgx_rmat_edges: bad edge range");
+  if (e_count == 0) return KGX_OK;
+  Feistel fs;
+  fs.hb = (scale + 1) / 2;
+  fs.mask = (uint64_t(1) << fs.hb) - 1;
+  for (int i = 0; i < 4; ++i) fs.keys[i] = splitmix64(seed ^ (0xA5A5A5A5A5A5A5A5ull + uint64_t(i)));
+  const uint64_t base = splitmix64(seed);
+  hipLaunchKernelGGL(rmat_kernel, dim3(grid_for(e_count, 16384)), dim3(kBlock), 0, stream, base, fs, scale,
+                     uint64_t(n_nodes), a24, a24 + b24, a24 + b24 + c24, e_begin, e_count, src, dst);
+  KGX_CHECK_LAUNCH();
+  return KGX_OK;
+}
+
+extern "C" int kgx_select_workspace_bytes(int64_t n, size_t* bytes) {
+  KGX_REQUIRE(bytes && n >= 0, KGX_ERR_ARG, "kgx_select_workspace_bytes: bad arguments");
+  size_t scb = 0;
+  const int32_t* si = nullptr;
+  int32_t* so = nullptr;
+  (void)rocprim::exclusive_scan(nullptr, scb, si, so, 0, (size_t)(n > 0 ? n : 1), rocprim::plus<int32_t>(), 0,
+                          false);
+  Carve c(nullptr, ~size_t(0));
+  c.take<int32_t>(n);
+  c.take<int32_t>(n);
+  c.take<unsigned long long>(1);
+  c.take<char>(scb);
+  *bytes = c.used();
+  return KGX_OK;
+}
+
+extern "C" int kgx_select_dst_range(const int32_t* src, const int32_t* dst, int64_t n, int64_t lo, int64_t hi,
+                                    int32_t* src_out, int32_t* dst_out, void* workspace, size_t workspace_bytes,
+                                    int64_t* n_out, kgx_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  KGX_REQUIRE(n >= 0 && n < (int64_t(1) << 31) && n_out, KGX_ERR_ARG, "kgx_select_dst_range: bad arguments");
+  if (n == 0) {
+    *n_out = 0;
+    return KGX_OK;
+  }
+  size_t need = 0;
+  kgx_select_workspace_bytes(n, &need);
+  KGX_REQUIRE(workspace && workspace_bytes >= need, KGX_ERR_ARG, "kgx_select_dst_range: workspace too small");
+  Carve c(workspace, workspace_bytes);
+  int32_t* flags = c.take<int32_t>(n);
+  int32_t* pos = c.take<int32_t>(n);
+  unsigned long long* cnt = c.take<unsigned long long>(1);
+  size_t scb = workspace_bytes - c.used();
+  void* tmp = c.take<char>(0);
+  const unsigned g = grid_for(n, 8192);
+  hipLaunchKernelGGL(range_flags_kernel, dim3(g), dim3(kBlock), 0, stream, dst, n, lo, hi, flags);
+  KGX_CHECK_LAUNCH();
+  KGX_CHECK_HIP(rocprim::exclusive_scan(tmp, scb, (const int32_t*)flags, pos, 0, (size_t)n,
+                                        rocprim::plus<int32_t>(), stream, false));
+  hipLaunchKernelGGL(range_scatter_kernel, dim3(g), dim3(kBlock), 0, stream, src, dst, flags, pos, n, src_out,
+                     dst_out, cnt);
+  KGX_CHECK_LAUNCH();
+  unsigned long long h = 0;
+  KGX_CHECK_HIP(hipMemcpyAsync(&h, cnt, sizeof(h), hipMemcpyDeviceToHost, stream));
+  KGX_CHECK_HIP(hipStreamSynchronize(stream));
+  *n_out = int64_t(h);
+  return KGX_OK;
+}
+
+extern "C" int kgx_gather_rows(const float* table, int64_t ld_table, const int32_t* rows, int64_t n, int64_t F,
+                               float* out, int64_t ld_out, kgx_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  KGX_REQUIRE(n >= 0 && F >= 0, KGX_ERR_ARG, "kgx_gather_rows: bad sizes");
+  if (n == 0 || F == 0) return KGX_OK;
+  KGX_REQUIRE(table && rows && out, KGX_ERR_ARG, "kgx_gather_rows: null pointer");
+  const bool v4 = (F % 4 == 0) && (ld_table % 4 == 0) && (ld_out % 4 == 0) &&
+                  (reinterpret_cast<uintptr_t>(table) % 16 == 0) && (reinterpret_cast<uintptr_t>(out) % 16 == 0);
+  if (v4) {
+    hipLaunchKernelGGL(gather_rows_kernel<4>, dim3(grid_for(n * (F / 4))), dim3(kBlock), 0, stream, table,
+                       ld_table, rows, n, F, out, ld_out);
+  } else {
+    hipLaunchKernelGGL(gather_rows_kernel<1>, dim3(grid_for(n * F)), dim3(kBlock), 0, stream, table, ld_table,
+                       rows, n, F, out, ld_out);
+  }
+  KGX_CHECK_LAUNCH();
+  return KGX_OK;
+}
+
+extern "C" int kgx_scatter_f32(const float* in, const int32_t* perm, int64_t n, float* out,
+                               kgx_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  KGX_REQUIRE(n >= 0, KGX_ERR_ARG, "kgx_scatter_f32: bad size");
+  if (n == 0) return KGX_OK;
+  KGX_REQUIRE(in && perm && out, KGX_ERR_ARG, "kgx_scatter_f32: null pointer");
+  hipLaunchKernelGGL(scatter_f32_kernel, dim3(grid_for(n)), dim3(kBlock), 0, stream, in, perm, n, out);
+  KGX_CHECK_LAUNCH();
+  return KGX_OK;
+}

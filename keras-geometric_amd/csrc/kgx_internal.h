@@ -1,0 +1,104 @@
+// Internal helpers shared by the kgx HIP translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+
+#include "kgx.h"
+
+namespace kgx {
+
+void set_error(const char* fmt, ...);
+
+inline hipStream_t as_stream(kgx_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int ceil_log2_u64(uint64_t v) {
+  int b = 0;
+  while ((uint64_t(1) << b) < v) ++b;
+  return b;
+}
+
+inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// Bump allocator over a caller-provided workspace.
+struct Carve {
+  char* base;
+  size_t cap;
+  size_t off = 0;
+  Carve(void* b, size_t c) : base(static_cast<char*>(b)), cap(c) {}
+  template <typename T>
+  T* take(size_t count) {
+    off = align_up(off, 256);
+    T* p = reinterpret_cast<T*>(base ? base + off : nullptr);
+    off += count * sizeof(T);
+    return p;
+  }
+  size_t used() const { return align_up(off, 256); }
+};
+
+constexpr int kBlock = 256;  // 4 waves of 64 lanes
+
+// Grid for a grid-stride launch: enough blocks to fill 256 CUs x 8 blocks, never
+// more than the work needs.
+inline unsigned grid_for(int64_t work_threads, int64_t cap_blocks = 2048) {
+  int64_t b = (work_threads + kBlock - 1) / kBlock;
+  if (b < 1) b = 1;
+  if (b > cap_blocks) b = cap_blocks;
+  return static_cast<unsigned>(b);
+}
+
+// Grid for a persistent grid-stride launch: as many blocks as are resident at
+// once (occupancy x CUs), never more than the work needs.
+template <typename Kern>
+unsigned resident_grid(Kern kernel, int64_t groups_needed, int G) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0) != hipSuccess || per_cu <= 0)
+    per_cu = 4;
+  const int64_t cap = int64_t(per_cu) * cus;
+  const int64_t need = (groups_needed * G + kBlock - 1) / kBlock;
+  const int64_t g = need < cap ? need : cap;
+  return unsigned(g < 1 ? 1 : g);
+}
+
+inline int next_pow2(int v) {
+  int p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+inline int log2i(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return l;
+}
+
+}  // namespace kgx
+
+#define KGX_CHECK_HIP(expr)                                                      \
+  do {                                                                           \
+    hipError_t kgx_e_ = (expr);                                                  \
+    if (kgx_e_ != hipSuccess) {                                                  \
+      kgx::set_error("%s:%d: %s failed: %s", __FILE__, __LINE__, #expr,          \
+                     hipGetErrorString(kgx_e_));                                 \
+      return KGX_ERR_HIP;                                                        \
+    }                                                                            \
+  } while (0)
+
+#define KGX_CHECK_LAUNCH() KGX_CHECK_HIP(hipGetLastError())
+
+#define KGX_REQUIRE(cond, code, ...)                                             \
+  do {                                                                           \
+    if (!(cond)) {                                                               \
+      kgx::set_error(__VA_ARGS__);                                               \
+      return (code);                                                             \
+    }                                                                            \
+  } while (0)

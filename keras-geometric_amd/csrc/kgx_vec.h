@@ -1,0 +1,59 @@
+// Vector load/store helpers and reference-exact scalar semantics shared by the
+// aggregation kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace kgx {
+
+// Load/store VEC consecutive floats (VEC in {1,2,4,8,16}; >=4 uses float4 pieces).
+template <int VEC>
+__device__ __forceinline__ void vload(float (&d)[VEC], const float* __restrict__ p) {
+  if constexpr (VEC >= 4) {
+#pragma unroll
+    for (int i = 0; i < VEC / 4; ++i) {
+      const float4 v = reinterpret_cast<const float4*>(p)[i];
+      d[4 * i + 0] = v.x;
+      d[4 * i + 1] = v.y;
+      d[4 * i + 2] = v.z;
+      d[4 * i + 3] = v.w;
+    }
+  } else if constexpr (VEC == 2) {
+    const float2 v = *reinterpret_cast<const float2*>(p);
+    d[0] = v.x;
+    d[1] = v.y;
+  } else {
+    d[0] = *p;
+  }
+}
+
+template <int VEC>
+__device__ __forceinline__ void vstore(float* __restrict__ p, const float (&d)[VEC]) {
+  if constexpr (VEC >= 4) {
+#pragma unroll
+    for (int i = 0; i < VEC / 4; ++i)
+      reinterpret_cast<float4*>(p)[i] = make_float4(d[4 * i], d[4 * i + 1], d[4 * i + 2], d[4 * i + 3]);
+  } else if constexpr (VEC == 2) {
+    *reinterpret_cast<float2*>(p) = make_float2(d[0], d[1]);
+  } else {
+    *p = d[0];
+  }
+}
+
+// fp32 degree as the reference computes it: segment_sum of fp32 ones, which a
+// sequential fp32 accumulation saturates at 2^24 (aggregators.py:66-69,194-196).
+__device__ __forceinline__ float ref_count_f32(int32_t n) {
+  return float(n < (1 << 24) ? n : (1 << 24));
+}
+
+// torch scatter_reduce "amax" update: self = isnan(src) ? src : max(self, src),
+// std::max keeps `self` on ties (so -0 vs +0 keeps the first seen).
+__device__ __forceinline__ float amax_update(float acc, float v) {
+  return (v > acc || v != v) ? v : acc;
+}
+
+__device__ __forceinline__ bool is_inf(float v) { return __builtin_isinf(v); }
+
+}  // namespace kgx

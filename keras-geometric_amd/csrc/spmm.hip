@@ -1,0 +1,425 @@
+// Fused gather -> message -> segment reduction -> epilogue for the kgx engine
+// (gfx950, wave64).
+//
+// One "group" of G lanes (G = pow2 >= F/VEC, <= 64) owns one destination row
+// (or one chunk of a split hub row); lane l holds features
+// (t*G + l)*VEC .. +VEC for t < NT.  The group walks its CSR edges IN ORDER,
+// U edges at a time: the U neighbour indices are loaded, the U neighbour rows
+// are gathered with VEC-wide loads (all U in flight), then folded into the
+// accumulator strictly sequentially with round-to-nearest adds and no FMA
+// contraction — the same per-(row, feature) operation sequence as the
+// reference's sequential scatter_add, hence bit-identical results for
+// identical messages.  Rows come in descending-degree order (schedule) and
+// every group walks the work list grid-stride, so hub rows start first.
+//
+// Reference semantics restated here (src/keras_geometric/...):
+//   sum  : layers/aggregators.py:126-137 (segment_sum, zeros init)
+//   mean : layers/aggregators.py:56-85   (sum / max(count_f32, 1e-8))
+//   max  : layers/aggregators.py:99-112  (segment_max, -inf init; isinf -> 0)
+//   min  : layers/aggregators.py:151-167 (-segment_max(-m); isinf -> 0)
+//   std  : layers/aggregators.py:182-228 (two-pass, N divisor, count<=1 -> 0)
+//   GCN message x_j W * norm (gcn_conv.py:233-248) with W pre-applied per node,
+//   GCN update + bias (gcn_conv.py:266-272), GIN (1+eps)*x + aggr (gin_conv.py:216-222).
+#include "kgx_internal.h"
+#include "kgx_vec.h"
+
+namespace kgx {
+namespace {
+
+struct SpmmArgs {
+  const int32_t* rowptr;
+  const int32_t* rows;
+  int64_t n_rows;
+  const int4* items;
+  int64_t n_items;
+  const int4* split;
+  int64_t n_split;
+  const int32_t* idx;
+  const float* w;
+  const float* table;
+  int64_t ld_t;
+  int F;  // columns handled by this launch
+  float* out;
+  int64_t ld_o;
+  const float* bias;
+  const float* xroot;
+  int64_t ld_x;
+  float gin_scale;
+  float* partials;
+  int64_t ld_p;
+  int epi;
+  int G;
+  int lgG;
+};
+
+template <int RED>
+struct Reducer {
+  static __device__ __forceinline__ float init() {
+    if constexpr (RED == KGX_MAX || RED == KGX_MIN) return -__builtin_inff();
+    return 0.0f;
+  }
+  // message value as it enters the reduction
+  static __device__ __forceinline__ float msg(float v) {
+    if constexpr (RED == KGX_MIN) return -v;  // min = -segment_max(-m)
+    return v;
+  }
+  static __device__ __forceinline__ float combine(float acc, float v) {
+    if constexpr (RED == KGX_MAX || RED == KGX_MIN) return amax_update(acc, v);
+    return __fadd_rn(acc, v);
+  }
+  static __device__ __forceinline__ float finish(float acc, int32_t deg) {
+    if constexpr (RED == KGX_MEAN) return __fdiv_rn(acc, fmaxf(ref_count_f32(deg), 1e-8f));
+    if constexpr (RED == KGX_MAX) return is_inf(acc) ? 0.0f : acc;
+    if constexpr (RED == KGX_MIN) {
+      const float r = -acc;
+      return is_inf(r) ? 0.0f : r;
+    }
+    return acc;
+  }
+};
+
+template <int VEC>
+__device__ __forceinline__ void epilogue(const SpmmArgs& a, int32_t row, int f, float (&v)[VEC]) {
+  if (a.epi == KGX_EPI_BIAS) {
+    float b[VEC];
+    vload<VEC>(b, a.bias + f);
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) v[k] = __fadd_rn(v[k], b[k]);
+  } else if (a.epi == KGX_EPI_GIN) {
+    float x[VEC];
+    vload<VEC>(x, a.xroot + int64_t(row) * a.ld_x + f);
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) v[k] = __fadd_rn(__fmul_rn(a.gin_scale, x[k]), v[k]);
+  }
+}
+
+template <int VEC, int NT, int RED, bool WEIGHTED>
+__global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
+  using R = Reducer<RED>;
+  constexpr int U = NT >= 4 ? 2 : (NT == 2 ? 4 : 8);
+  const int G = a.G;
+  const int lane = threadIdx.x & (G - 1);
+  const int64_t ngroups = (int64_t(gridDim.x) * kBlock) >> a.lgG;
+  const int64_t n_work = a.items ? a.n_items : a.n_rows;
+
+  int fo[NT];
+  bool fv[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    fo[t] = (t * G + lane) * VEC;
+    fv[t] = fo[t] < a.F;
+  }
+
+  for (int64_t it = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> a.lgG; it < n_work; it += ngroups) {
+    int32_t row, beg, end, slot;
+    if (a.items) {
+      const int4 v = a.items[it];
+      row = v.x;
+      beg = v.y;
+      end = v.z;
+      slot = v.w;
+    } else {
+      row = a.rows[it];
+      beg = a.rowptr[row];
+      end = a.rowptr[row + 1];
+      slot = -1;
+    }
+
+    float acc[NT][VEC];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) acc[t][k] = R::init();
+
+    int32_t e = beg;
+    for (; e + U <= end; e += U) {
+      int32_t c[U];
+      float wt[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        c[u] = a.idx[e + u];
+        if constexpr (WEIGHTED) wt[u] = a.w[e + u];
+      }
+      float v[U][NT][VEC];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          if (fv[t]) {
+            vload<VEC>(v[u][t], a.table + int64_t(c[u]) * a.ld_t + fo[t]);
+          } else {
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) v[u][t][k] = 0.0f;
+          }
+        }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int k = 0; k < VEC; ++k) {
+            const float m = WEIGHTED ? __fmul_rn(v[u][t][k], wt[u]) : v[u][t][k];
+            acc[t][k] = R::combine(acc[t][k], R::msg(m));
+          }
+    }
+    if (e < end) {  // tail: n < U edges, all loads issued together
+      const int n = end - e;
+      int32_t c[U];
+      float wt[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int32_t ee = u < n ? e + u : end - 1;
+        c[u] = a.idx[ee];
+        if constexpr (WEIGHTED) wt[u] = a.w[ee];
+      }
+      float v[U][NT][VEC];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          if (fv[t] && u < n) {
+            vload<VEC>(v[u][t], a.table + int64_t(c[u]) * a.ld_t + fo[t]);
+          } else {
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) v[u][t][k] = 0.0f;
+          }
+        }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (u < n) {
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+              const float m = WEIGHTED ? __fmul_rn(v[u][t][k], wt[u]) : v[u][t][k];
+              acc[t][k] = R::combine(acc[t][k], R::msg(m));
+            }
+        }
+      }
+    }
+
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      if (!fv[t]) continue;
+      if (slot >= 0) {  // chunk of a split hub row: raw partial, finished by the fix-up
+        vstore<VEC>(a.partials + int64_t(slot) * a.ld_p + fo[t], acc[t]);
+      } else {
+        float r[VEC];
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) r[k] = R::finish(acc[t][k], end - beg);
+        epilogue<VEC>(a, row, fo[t], r);
+        vstore<VEC>(a.out + int64_t(row) * a.ld_o + fo[t], r);
+      }
+    }
+  }
+}
+
+// Combine the chunk partials of split rows in chunk order, then finish.
+template <int VEC, int NT, int RED>
+__global__ __launch_bounds__(kBlock) void spmm_fixup_kernel(SpmmArgs a) {
+  using R = Reducer<RED>;
+  const int G = a.G;
+  const int lane = threadIdx.x & (G - 1);
+  const int64_t ngroups = (int64_t(gridDim.x) * kBlock) >> a.lgG;
+  for (int64_t it = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> a.lgG; it < a.n_split; it += ngroups) {
+    const int4 s = a.split[it];
+    const int32_t row = s.x, slot0 = s.y, nc = s.z, deg = s.w;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int f = (t * G + lane) * VEC;
+      if (f >= a.F) continue;
+      float acc[VEC];
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) acc[k] = R::init();
+      for (int32_t c = 0; c < nc; ++c) {
+        float p[VEC];
+        vload<VEC>(p, a.partials + int64_t(slot0 + c) * a.ld_p + f);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) acc[k] = R::combine(acc[k], p[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) acc[k] = R::finish(acc[k], deg);
+      epilogue<VEC>(a, row, f, acc);
+      vstore<VEC>(a.out + int64_t(row) * a.ld_o + f, acc);
+    }
+  }
+}
+
+// StdAggregator (aggregators.py:182-228), two sequential passes per row, EXACT.
+template <int VEC, int NT>
+__global__ __launch_bounds__(kBlock) void spmm_std_kernel(SpmmArgs a) {
+  const int G = a.G;
+  const int lane = threadIdx.x & (G - 1);
+  const int64_t ngroups = (int64_t(gridDim.x) * kBlock) >> a.lgG;
+  for (int64_t it = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> a.lgG; it < a.n_rows; it += ngroups) {
+    const int32_t row = a.rows[it];
+    const int32_t beg = a.rowptr[row], end = a.rowptr[row + 1];
+    const float cnt = ref_count_f32(end - beg);
+    const float safe = fmaxf(cnt, 1e-8f);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int f = (t * G + lane) * VEC;
+      if (f >= a.F) continue;
+      float sum[VEC], ssd[VEC], mean[VEC];
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) sum[k] = ssd[k] = 0.0f;
+      for (int32_t e = beg; e < end; ++e) {
+        float v[VEC];
+        vload<VEC>(v, a.table + int64_t(a.idx[e]) * a.ld_t + f);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) sum[k] = __fadd_rn(sum[k], v[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) mean[k] = __fdiv_rn(sum[k], safe);
+      for (int32_t e = beg; e < end; ++e) {
+        float v[VEC];
+        vload<VEC>(v, a.table + int64_t(a.idx[e]) * a.ld_t + f);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+          const float d = __fsub_rn(v[k], mean[k]);
+          ssd[k] = __fadd_rn(ssd[k], __fmul_rn(d, d));
+        }
+      }
+      float r[VEC];
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) {
+        const float var = __fdiv_rn(ssd[k], safe);
+        const float sd = __fsqrt_rn(fmaxf(var, 0.0f) /* maximum(variance, 0) */);
+        r[k] = cnt <= 1.0f ? 0.0f : (var != var ? var : sd);
+      }
+      epilogue<VEC>(a, row, f, r);
+      vstore<VEC>(a.out + int64_t(row) * a.ld_o + f, r);
+    }
+  }
+}
+
+
+
+template <int VEC, int NT, int RED, bool W>
+int launch_main(const SpmmArgs& a, hipStream_t s) {
+  const int64_t work = a.items ? a.n_items : a.n_rows;
+  if (work > 0) {
+    auto k = spmm_kernel<VEC, NT, RED, W>;
+    hipLaunchKernelGGL(k, dim3(resident_grid(k, work, a.G)), dim3(kBlock), 0, s, a);
+    KGX_CHECK_LAUNCH();
+  }
+  if (a.items && a.n_split > 0) {
+    auto k = spmm_fixup_kernel<VEC, NT, RED>;
+    hipLaunchKernelGGL(k, dim3(resident_grid(k, a.n_split, a.G)), dim3(kBlock), 0, s, a);
+    KGX_CHECK_LAUNCH();
+  }
+  return KGX_OK;
+}
+
+template <int VEC, int NT, int RED>
+int dispatch_w(const SpmmArgs& a, hipStream_t s) {
+  if (RED == KGX_STD) {
+    if (a.n_rows > 0) {
+      auto k = spmm_std_kernel<VEC, NT>;
+      hipLaunchKernelGGL(k, dim3(resident_grid(k, a.n_rows, a.G)), dim3(kBlock), 0, s, a);
+      KGX_CHECK_LAUNCH();
+    }
+    return KGX_OK;
+  }
+  constexpr int RR = RED == KGX_STD ? KGX_SUM : RED;
+  return a.w ? launch_main<VEC, NT, RR, true>(a, s) : launch_main<VEC, NT, RR, false>(a, s);
+}
+
+template <int VEC, int NT>
+int dispatch_red(int red, const SpmmArgs& a, hipStream_t s) {
+  switch (red) {
+    case KGX_SUM: return dispatch_w<VEC, NT, KGX_SUM>(a, s);
+    case KGX_MEAN: return dispatch_w<VEC, NT, KGX_MEAN>(a, s);
+    case KGX_MAX: return dispatch_w<VEC, NT, KGX_MAX>(a, s);
+    case KGX_MIN: return dispatch_w<VEC, NT, KGX_MIN>(a, s);
+    case KGX_STD: return dispatch_w<VEC, NT, KGX_STD>(a, s);
+  }
+  set_error("kgx_spmm: unknown reduce %d", red);
+  return KGX_ERR_ARG;
+}
+
+template <int VEC>
+int dispatch_nt(int nt, int red, const SpmmArgs& a, hipStream_t s) {
+  if (nt == 1) return dispatch_red<VEC, 1>(red, a, s);
+  if (nt == 2) return dispatch_red<VEC, 2>(red, a, s);
+  return dispatch_red<VEC, 4>(red, a, s);
+}
+
+bool aligned(const void* p, int bytes) { return p == nullptr || reinterpret_cast<uintptr_t>(p) % bytes == 0; }
+
+}  // namespace
+}  // namespace kgx
+
+using namespace kgx;
+
+extern "C" int kgx_spmm(int reduce, int epilogue, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
+                        const int32_t* items, int64_t n_items, const int32_t* split, int64_t n_split,
+                        const int32_t* idx, const float* w, const float* table, int64_t ld_table, int64_t F,
+                        float* out, int64_t ld_out, const float* bias, const float* xroot, int64_t ld_x,
+                        float gin_scale, float* partials, kgx_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  KGX_REQUIRE(reduce >= KGX_SUM && reduce <= KGX_STD, KGX_ERR_ARG, "kgx_spmm: unknown reduce %d", reduce);
+  KGX_REQUIRE(epilogue >= KGX_EPI_NONE && epilogue <= KGX_EPI_GIN, KGX_ERR_ARG, "kgx_spmm: unknown epilogue %d",
+              epilogue);
+  KGX_REQUIRE(F >= 0 && n_rows >= 0 && n_items >= 0 && n_split >= 0, KGX_ERR_ARG, "kgx_spmm: negative size");
+  if (F == 0 || n_rows == 0) return KGX_OK;
+  KGX_REQUIRE(out && ld_out >= F && ld_table >= F, KGX_ERR_ARG, "kgx_spmm: bad output / leading dimensions");
+  KGX_REQUIRE(rowptr && rows && idx && table, KGX_ERR_ARG, "kgx_spmm: null CSR / table pointer");
+  KGX_REQUIRE(epilogue != KGX_EPI_BIAS || bias, KGX_ERR_ARG, "kgx_spmm: EPI_BIAS needs bias");
+  KGX_REQUIRE(epilogue != KGX_EPI_GIN || (xroot && ld_x >= F), KGX_ERR_ARG, "kgx_spmm: EPI_GIN needs xroot");
+  const bool use_items = items != nullptr && reduce != KGX_STD;
+  KGX_REQUIRE(!use_items || n_split == 0 || (split && partials), KGX_ERR_ARG,
+              "kgx_spmm: split rows need split list and partials");
+
+  SpmmArgs a{};
+  a.rowptr = rowptr;
+  a.rows = rows;
+  a.n_rows = n_rows;
+  a.items = use_items ? reinterpret_cast<const int4*>(items) : nullptr;
+  a.n_items = use_items ? n_items : 0;
+  a.split = reinterpret_cast<const int4*>(split);
+  a.n_split = use_items ? n_split : 0;
+  a.idx = idx;
+  a.w = w;
+  a.epi = epilogue;
+  a.gin_scale = gin_scale;
+  a.ld_t = ld_table;
+  a.ld_o = ld_out;
+  a.ld_x = ld_x;
+  a.ld_p = F;
+
+  // widest vector the shapes and pointers allow
+  auto ok = [&](int v) {
+    const int b = 4 * v;
+    return F % v == 0 && ld_table % v == 0 && ld_out % v == 0 && aligned(table, b) && aligned(out, b) &&
+           (epilogue != KGX_EPI_BIAS || aligned(bias, b)) &&
+           (epilogue != KGX_EPI_GIN || (ld_x % v == 0 && aligned(xroot, b))) && aligned(partials, b);
+  };
+  const int VEC = ok(4) ? 4 : (ok(2) ? 2 : 1);
+  const int64_t fvec = F / VEC;
+  const int G = int(fvec >= 64 ? 64 : next_pow2(int(fvec)));
+  int lg = 0;
+  while ((1 << lg) < G) ++lg;
+  // column slices of at most 4*64*VEC features per launch
+  const int64_t slice = int64_t(4) * 64 * VEC;
+  for (int64_t c0 = 0; c0 < F; c0 += slice) {
+    const int64_t cw = (F - c0) < slice ? (F - c0) : slice;
+    const int64_t cv = cw / VEC;
+    const int nt = cv <= 64 ? 1 : (cv <= 128 ? 2 : 4);
+    SpmmArgs s = a;
+    s.F = int(cw);
+    s.G = G;
+    s.lgG = lg;
+    s.table = table + c0;
+    s.out = out + c0;
+    s.bias = bias ? bias + c0 : nullptr;
+    s.xroot = xroot ? xroot + c0 : nullptr;
+    s.partials = partials ? partials + c0 : nullptr;
+    int rc;
+    if (VEC == 4) rc = dispatch_nt<4>(nt, reduce, s, stream);
+    else if (VEC == 2) rc = dispatch_nt<2>(nt, reduce, s, stream);
+    else rc = dispatch_nt<1>(nt, reduce, s, stream);
+    if (rc != KGX_OK) return rc;
+  }
+  return KGX_OK;
+}

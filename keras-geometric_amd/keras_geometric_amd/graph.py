@@ -1,0 +1,205 @@
+"""Device-resident graph structure: stable destination CSR + row schedule.
+
+The reference re-derives everything from `edge_index` on every call
+(message_passing.py:256-268 casts/caches edge_index by id(); add_self_loops and
+compute_gcn_normalization run per call, gcn_conv.py:328-353).  Here one
+`CSRGraph` is built on the GPU per (edge_index, node count, flags) and cached
+while the edge_index tensor is alive and unmodified (its storage pointer and
+version counter are part of the key and the cache holds a reference, so a
+freed-and-reused address can never alias a stale entry).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from collections import OrderedDict
+from dataclasses import dataclass, field
+
+import torch
+
+from . import _native as nat
+
+_ASSUMED_GROUP_SLOTS = 2048 * 256  # resident lanes (256 CUs x 8 blocks x 256 threads)
+
+
+def _pow2_floor(v: int) -> int:
+    return 1 << (max(int(v), 1).bit_length() - 1)
+
+
+def default_split_len(n_edges: int, n_features: int = 128) -> int:
+    """Hub-split chunk length for a graph.
+
+    Static grid-stride scheduling over degree-sorted items bounds the per-group
+    imbalance by the largest item, so chunks are sized to about a quarter of a
+    group's average share of the edges (power of two, 256..8192).
+    """
+    lanes = max(1, (max(n_features, 1) + 3) // 4)  # float4 lanes per row
+    G = min(64, 1 << (lanes - 1).bit_length())  # lanes per group (pow2)
+    groups = _ASSUMED_GROUP_SLOTS // G
+    share = max(1, n_edges // groups)
+    return int(min(8192, max(256, _pow2_floor(max(share // 4, 1)))))
+
+
+def exact_mode_default() -> bool:
+    return os.environ.get("KGX_EXACT", "0") not in ("", "0", "false", "False")
+
+
+@dataclass
+class CSRGraph:
+    n_src: int
+    n_dst: int
+    n_input_edges: int
+    kept: int  # edges kept in the CSR (incl. self loops)
+    max_degree: int
+    flags: int
+    rowptr: torch.Tensor  # int32 [n_dst+1]
+    col: torch.Tensor  # int32 [kept]   source node per CSR slot
+    eid: torch.Tensor  # int32 [kept]   input edge id per CSR slot (E+i = self loop i)
+    deg: torch.Tensor  # int32 [n_dst]
+    dinv: torch.Tensor | None = None  # fp32 [n_dst]  (GCN_NORM)
+    w: torch.Tensor | None = None  # fp32 [kept]   GCN edge norm in CSR order
+    rows: torch.Tensor | None = None  # int32 [n_dst]  rows in schedule order
+    items: torch.Tensor | None = None  # int32 [n_items, 4]
+    split: torch.Tensor | None = None  # int32 [n_split, 4]
+    n_items: int = 0
+    n_split: int = 0
+    n_slots: int = 0
+    split_len: int = 0
+    extras: dict = field(default_factory=dict)
+
+    @property
+    def device(self) -> torch.device:
+        return self.rowptr.device
+
+    def work(self, exact: bool):
+        """(items, n_items, split, n_split, n_slots) for a launch; exact -> none."""
+        if exact or self.n_items == 0:
+            return None, 0, None, 0, 0
+        return self.items, self.n_items, self.split, self.n_split, self.n_slots
+
+
+def build_csr(
+    src: torch.Tensor,
+    dst: torch.Tensor,
+    n_src: int,
+    n_dst: int,
+    *,
+    self_loops: bool = False,
+    gcn_norm: bool = False,
+    segment_only: bool = False,
+    split_len: int | None = None,
+    n_features: int = 128,
+) -> CSRGraph:
+    """COO (int32 device tensors) -> CSRGraph via kgx_csr_build + kgx_schedule_build."""
+    dev = nat.require_device(src, dst)
+    if src.dtype != torch.int32 or dst.dtype != torch.int32:
+        raise TypeError("build_csr expects int32 src/dst")
+    src = src.contiguous()
+    dst = dst.contiguous()
+    E = int(src.numel())
+    if int(dst.numel()) != E:
+        raise ValueError(f"src/dst length mismatch: {E} vs {dst.numel()}")
+    flags = (
+        (nat.CSR_SELF_LOOPS if self_loops else 0)
+        | (nat.CSR_SEGMENT_ONLY if segment_only else 0)
+        | (nat.CSR_GCN_NORM if gcn_norm else 0)
+    )
+    cap = E + (n_dst if self_loops else 0)
+    L = nat.lib()
+    i32 = dict(dtype=torch.int32, device=dev)
+    rowptr = torch.empty(n_dst + 1, **i32)
+    col = torch.empty(max(cap, 1), **i32)
+    eid = torch.empty(max(cap, 1), **i32)
+    deg = torch.empty(max(n_dst, 1), **i32)
+    dinv = torch.empty(max(n_dst, 1), dtype=torch.float32, device=dev) if gcn_norm else None
+    w = torch.empty(max(cap, 1), dtype=torch.float32, device=dev) if gcn_norm else None
+    nbytes = ctypes.c_size_t(0)
+    nat.check(L.kgx_csr_workspace_bytes(E, n_dst, flags, ctypes.byref(nbytes)), "kgx_csr_workspace_bytes")
+    ws = torch.empty(max(nbytes.value, 1), dtype=torch.uint8, device=dev)
+    info = (ctypes.c_int64 * 4)()
+    nat.check(
+        L.kgx_csr_build(
+            nat.ptr(src), nat.ptr(dst), E, n_src, n_dst, flags,
+            nat.ptr(rowptr), nat.ptr(col), nat.ptr(eid), nat.ptr(deg), nat.ptr(dinv), nat.ptr(w),
+            nat.ptr(ws), nbytes.value, info, nat.stream(dev),
+        ),
+        "kgx_csr_build",
+    )
+    del ws
+    kept, max_deg = int(info[0]), int(info[1])
+    g = CSRGraph(
+        n_src=n_src, n_dst=n_dst, n_input_edges=E, kept=kept, max_degree=max_deg, flags=flags,
+        rowptr=rowptr, col=col[:kept], eid=eid[:kept], deg=deg[:n_dst],
+        dinv=dinv[:n_dst] if dinv is not None else None, w=w[:kept] if w is not None else None,
+    )
+    _build_schedule(g, split_len if split_len is not None else default_split_len(kept, n_features))
+    return g
+
+
+def _build_schedule(g: CSRGraph, split_len: int) -> None:
+    dev = g.device
+    n = g.n_dst
+    if split_len > 0:
+        split_len = _pow2_floor(split_len)
+    g.split_len = split_len
+    if n == 0:
+        g.rows = torch.empty(0, dtype=torch.int32, device=dev)
+        return
+    L = nat.lib()
+    cap_items = n + (g.kept // split_len if split_len > 0 else 0) + 1
+    cap_split = min(n, (g.kept // split_len if split_len > 0 else 0) + 1)
+    rows = torch.empty(n, dtype=torch.int32, device=dev)
+    items = torch.empty((cap_items, 4), dtype=torch.int32, device=dev)
+    split = torch.empty((max(cap_split, 1), 4), dtype=torch.int32, device=dev)
+    nbytes = ctypes.c_size_t(0)
+    nat.check(L.kgx_schedule_workspace_bytes(n, ctypes.byref(nbytes)), "kgx_schedule_workspace_bytes")
+    ws = torch.empty(max(nbytes.value, 1), dtype=torch.uint8, device=dev)
+    info = (ctypes.c_int64 * 4)()
+    nat.check(
+        L.kgx_schedule_build(
+            nat.ptr(g.rowptr), n, split_len, nat.ptr(rows), nat.ptr(items), cap_items, nat.ptr(split),
+            nat.ptr(ws), nbytes.value, info, nat.stream(dev),
+        ),
+        "kgx_schedule_build",
+    )
+    g.rows = rows
+    g.n_items, g.n_split, g.n_slots = int(info[0]), int(info[1]), int(info[2])
+    if g.n_split > cap_split:
+        raise RuntimeError("kgx schedule: split list overflow")
+    g.items = items[: g.n_items]
+    g.split = split[: max(g.n_split, 0)]
+
+
+# ---------------------------------------------------------------------------
+# cache keyed on the caller's edge_index tensor (kept alive by the entry)
+# ---------------------------------------------------------------------------
+_CACHE: "OrderedDict[tuple, tuple[torch.Tensor, CSRGraph]]" = OrderedDict()
+_CACHE_SIZE = int(os.environ.get("KGX_GRAPH_CACHE", "8"))
+
+
+def cache_key(edge_index: torch.Tensor, *extra) -> tuple | None:
+    if not isinstance(edge_index, torch.Tensor):
+        return None
+    return (
+        edge_index.data_ptr(), edge_index._version, tuple(edge_index.shape), tuple(edge_index.stride()),
+        edge_index.dtype, str(edge_index.device), *extra,
+    )
+
+
+def cached(key: tuple | None, anchor, builder) -> CSRGraph:
+    if key is None or _CACHE_SIZE <= 0:
+        return builder()
+    hit = _CACHE.get(key)
+    if hit is not None:
+        _CACHE.move_to_end(key)
+        return hit[1]
+    g = builder()
+    _CACHE[key] = (anchor, g)
+    while len(_CACHE) > _CACHE_SIZE:
+        _CACHE.popitem(last=False)
+    return g
+
+
+def clear_cache() -> None:
+    _CACHE.clear()

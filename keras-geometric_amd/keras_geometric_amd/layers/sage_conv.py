@@ -1,0 +1,170 @@
+"""SAGEConv (mirror of src/keras_geometric/layers/sage_conv.py).
+
+out = act(lin_self(x) + lin_neigh(AGG_{j->i} m_j) + b), optional L2 normalize
+(sage_conv.py:351-439).  m_j = x_j, or pool_mlp(x_j) for aggregator="pooling"
+(PoolingAggregator, aggregators.py:254-274).  pool_mlp is row-wise, so it is
+applied once per NODE and the kgx kernel gathers its rows (same values as the
+reference's per-edge application).
+"""
+
+from __future__ import annotations
+
+from typing import Any
+
+import torch
+
+from .. import ops as kops
+from ._edges import edge_index_tensor, graph_for
+from .base import Dense, get_activation, get_initializer, serialize_activation, serialize_initializer, \
+    to_device_tensor
+from .message_passing import MessagePassing
+
+_VALID = ["mean", "max", "sum", "min", "std", "pooling"]
+
+
+def l2_normalize(x: torch.Tensor, epsilon: float = 1e-7) -> torch.Tensor:
+    """keras.ops.normalize(x, axis=-1, order=2): x * min(rsqrt(sum(x^2)), 1/eps)."""
+    square_sum = torch.sum(torch.square(x), dim=-1, keepdim=True)
+    inv_norm = torch.minimum(torch.rsqrt(square_sum), torch.tensor(1.0 / epsilon, device=x.device))
+    return x * inv_norm
+
+
+class SAGEConv(MessagePassing):
+    def __init__(
+        self,
+        output_dim: int,
+        aggregator: str = "mean",
+        normalize: bool = False,
+        root_weight: bool = True,
+        use_bias: bool = True,
+        activation: str | None = "relu",
+        pool_activation: str | None = "relu",
+        pool_hidden_dim: int | None = None,
+        kernel_initializer="glorot_uniform",
+        bias_initializer="zeros",
+        kernel_regularizer=None,
+        bias_regularizer=None,
+        kernel_constraint=None,
+        bias_constraint=None,
+        dropout_rate: float = 0.0,
+        **kwargs: Any,
+    ) -> None:
+        if aggregator not in _VALID:  # sage_conv.py:99-103
+            raise ValueError(f"Invalid aggregator '{aggregator}'. Must be one of {_VALID}")
+        super().__init__(aggregator="mean" if aggregator == "pooling" else aggregator, **kwargs)
+        self.actual_aggregator = aggregator
+        self.output_dim = output_dim
+        self.normalize = normalize
+        self.root_weight = root_weight
+        self.use_bias = use_bias
+        self.pool_hidden_dim = pool_hidden_dim
+        self.dropout_rate = dropout_rate
+        self.activation = get_activation(activation)
+        self.pool_activation = get_activation(pool_activation)
+        self.kernel_initializer = get_initializer(kernel_initializer)
+        self.bias_initializer = get_initializer(bias_initializer)
+        self.kernel_regularizer = kernel_regularizer
+        self.bias_regularizer = bias_regularizer
+        self.kernel_constraint = kernel_constraint
+        self.bias_constraint = bias_constraint
+        self.lin_neigh = None
+        self.lin_self = None
+        self.pool_mlp = None
+        self.bias = None
+
+    def build(self, input_shape) -> None:
+        if input_shape is None:
+            return
+        if not isinstance(input_shape, (list, tuple)) or len(input_shape) < 2:
+            raise ValueError(f"Expected input_shape to be [(N, F), (2, E)], got {input_shape}")
+        node_shape = input_shape[0]
+        if node_shape is None or len(node_shape) < 2:
+            raise ValueError(f"Expected node shape (N, F), got {node_shape}")
+        input_dim = node_shape[-1]
+        if input_dim is None or input_dim <= 0:
+            raise ValueError(f"Input dimension must be positive, got {input_dim}")
+        dev = getattr(self, "_build_device", None)
+        if self.actual_aggregator == "pooling":
+            self.pool_mlp = Dense(self.pool_hidden_dim or input_dim, activation=self.pool_activation,
+                                  use_bias=self.use_bias, kernel_initializer=self.kernel_initializer,
+                                  bias_initializer=self.bias_initializer, name="pool_mlp")
+            self.pool_mlp._build_device = dev
+            self.pool_mlp.build((None, input_dim))
+        self.lin_neigh = Dense(self.output_dim, use_bias=False, kernel_initializer=self.kernel_initializer,
+                               name="linear_neigh")
+        self.lin_neigh._build_device = dev
+        neigh_dim = (self.pool_hidden_dim or input_dim) if self.actual_aggregator == "pooling" else input_dim
+        self.lin_neigh.build((None, neigh_dim))
+        if self.root_weight:
+            self.lin_self = Dense(self.output_dim, use_bias=False, kernel_initializer=self.kernel_initializer,
+                                  name="linear_self")
+            self.lin_self._build_device = dev
+            self.lin_self.build((None, input_dim))
+        if self.use_bias:
+            self.bias = self.add_weight((self.output_dim,), self.bias_initializer, name="bias")
+        self.built = True
+
+    def compute_output_shape(self, input_shape) -> tuple:
+        node_shape = input_shape[0] if isinstance(input_shape, (list, tuple)) and input_shape else None
+        return (node_shape[0] if node_shape else None, self.output_dim)
+
+    def aggregate_neighbors(self, x, edge_index, num_nodes, training=None, *, edge_index_obj=None):
+        """sage_conv.py:300-348 as one fused kgx reduction over gathered rows."""
+        if edge_index.shape[1] == 0:
+            feat = self.pool_mlp.units if (self.actual_aggregator == "pooling" and self.pool_mlp) else x.shape[1]
+            return torch.zeros((num_nodes, feat), dtype=x.dtype, device=x.device)
+        g = graph_for(edge_index_obj if edge_index_obj is not None else edge_index, edge_index,
+                      x.shape[0], num_nodes, n_features=x.shape[1])
+        if self.actual_aggregator == "pooling":
+            return kops.aggregate(g, self.pool_mlp(x).contiguous(), "max", exact=self.exact)
+        return kops.aggregate(g, x.contiguous(), self.actual_aggregator, exact=self.exact)
+
+    def call(self, inputs, training=None, mask=None):
+        if not isinstance(inputs, (list, tuple)) or len(inputs) < 2:
+            raise ValueError("SAGEConv expects inputs to be a list/tuple of [node_features, edge_index]")
+        x = to_device_tensor(inputs[0], torch.float32)
+        edge_index = inputs[1]
+        ei = edge_index_tensor(edge_index, x.device, allow_transpose=True)
+        if training and self.dropout_rate > 0:
+            raise NotImplementedError(
+                "SAGEConv per-edge dropout in training mode is not implemented by the kgx forward "
+                "engine (sage_conv.py:294-298); use dropout_rate=0 or training=False."
+            )
+        num_nodes = x.shape[0]
+        aggregated = self.aggregate_neighbors(x, ei, num_nodes, training=training, edge_index_obj=edge_index)
+        h_neigh = self.lin_neigh(aggregated)
+        if self.root_weight and self.lin_self is not None:
+            out = self.lin_self(x) + h_neigh
+        else:
+            out = h_neigh
+        if self.use_bias and self.bias is not None:
+            out = out + self.bias
+        if self.activation is not None:
+            out = self.activation(out)
+        if self.normalize:
+            out = l2_normalize(out)
+        return out
+
+    def get_config(self) -> dict[str, Any]:
+        config = super().get_config()
+        config.update(
+            {
+                "output_dim": self.output_dim,
+                "normalize": self.normalize,
+                "root_weight": self.root_weight,
+                "use_bias": self.use_bias,
+                "activation": serialize_activation(self.activation),
+                "pool_activation": serialize_activation(self.pool_activation),
+                "pool_hidden_dim": self.pool_hidden_dim,
+                "kernel_initializer": serialize_initializer(self.kernel_initializer),
+                "bias_initializer": serialize_initializer(self.bias_initializer),
+                "kernel_regularizer": self.kernel_regularizer,
+                "bias_regularizer": self.bias_regularizer,
+                "kernel_constraint": self.kernel_constraint,
+                "bias_constraint": self.bias_constraint,
+                "dropout_rate": self.dropout_rate,
+            }
+        )
+        config.pop("aggregator", None)
+        config["aggregator"] = self.actual_aggregator  # sage_conv.py:467-469
+        return config

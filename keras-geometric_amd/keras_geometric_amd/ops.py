@@ -1,0 +1,228 @@
+"""PyTorch-ROCm operator registration of the kgx C-ABI (torch.ops.kgx.*).
+
+Each op is a `torch.library.custom_op` whose implementation calls straight into
+libkgx.so on torch's current HIP stream, with a fake (meta) kernel so that
+torch.compile / symbolic tracing sees shapes without running the GPU.
+
+  kgx::spmm   fused gather -> message -> segment {sum,mean,max,min,std} -> epilogue
+  kgx::gatv2  fused GATv2 attention aggregation
+  kgx::gather_rows, kgx::scatter_f32   row movement helpers
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import _native as nat
+from .graph import CSRGraph
+
+
+def _f32c(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    if t is None:
+        return None
+    if t.dtype != torch.float32:
+        raise TypeError(f"kgx kernels compute in fp32; got {t.dtype}")
+    return t.contiguous()
+
+
+@torch.library.custom_op("kgx::spmm", mutates_args=())
+def spmm(
+    table: torch.Tensor,
+    rowptr: torch.Tensor,
+    rows: torch.Tensor,
+    items: Optional[torch.Tensor],
+    split: Optional[torch.Tensor],
+    idx: torch.Tensor,
+    w: Optional[torch.Tensor],
+    n_slots: int,
+    reduce: int,
+    epilogue: int,
+    bias: Optional[torch.Tensor],
+    xroot: Optional[torch.Tensor],
+    gin_scale: float,
+) -> torch.Tensor:
+    table = _f32c(table)
+    w, bias, xroot = _f32c(w), _f32c(bias), _f32c(xroot)
+    dev = nat.require_device(table, rowptr, rows, idx, w, bias, xroot, items, split)
+    n_dst = rowptr.numel() - 1
+    F = table.shape[1]
+    out = torch.empty((n_dst, F), dtype=torch.float32, device=dev)
+    if n_dst == 0 or F == 0:
+        return out
+    n_items = 0 if items is None else items.shape[0]
+    n_split = 0 if split is None else split.shape[0]
+    partials = None
+    if items is not None and n_split > 0 and reduce != nat.STD:
+        partials = torch.empty((n_slots, F), dtype=torch.float32, device=dev)
+    nat.check(
+        nat.lib().kgx_spmm(
+            reduce, epilogue, nat.ptr(rowptr), nat.ptr(rows), n_dst,
+            nat.ptr(items), n_items, nat.ptr(split), n_split,
+            nat.ptr(idx), nat.ptr(w), nat.ptr(table), table.stride(0), F,
+            nat.ptr(out), out.stride(0),
+            nat.ptr(bias), nat.ptr(xroot), xroot.stride(0) if xroot is not None else 0, float(gin_scale),
+            nat.ptr(partials), nat.stream(dev),
+        ),
+        "kgx_spmm",
+    )
+    return out
+
+
+@spmm.register_fake
+def _spmm_fake(table, rowptr, rows, items, split, idx, w, n_slots, reduce, epilogue, bias, xroot, gin_scale):
+    return table.new_empty((rowptr.shape[0] - 1, table.shape[1]))
+
+
+@torch.library.custom_op("kgx::gatv2", mutates_args=())
+def gatv2(
+    h_src: torch.Tensor,
+    h_dst: torch.Tensor,
+    rowptr: torch.Tensor,
+    rows: torch.Tensor,
+    items: Optional[torch.Tensor],
+    split: Optional[torch.Tensor],
+    col: torch.Tensor,
+    att: torch.Tensor,
+    heads: int,
+    channels: int,
+    negative_slope: float,
+    bias: Optional[torch.Tensor],
+    n_slots: int,
+) -> torch.Tensor:
+    h_src, h_dst, att, bias = _f32c(h_src), _f32c(h_dst), _f32c(att), _f32c(bias)
+    dev = nat.require_device(h_src, h_dst, rowptr, rows, col, att, bias, items, split)
+    n_dst = rowptr.numel() - 1
+    HC = heads * channels
+    out = torch.empty((n_dst, HC), dtype=torch.float32, device=dev)
+    if n_dst == 0:
+        return out
+    n_items = 0 if items is None else items.shape[0]
+    n_split = 0 if split is None else split.shape[0]
+    partials = None
+    if items is not None and n_split > 0:
+        partials = torch.empty((n_slots, HC + 2 * heads), dtype=torch.float32, device=dev)
+    nat.check(
+        nat.lib().kgx_gatv2(
+            nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, nat.ptr(split), n_split,
+            nat.ptr(col), nat.ptr(h_src), nat.ptr(h_dst), h_src.stride(0), nat.ptr(att), heads, channels,
+            float(negative_slope), nat.ptr(out), out.stride(0), nat.ptr(bias), nat.ptr(partials),
+            nat.stream(dev),
+        ),
+        "kgx_gatv2",
+    )
+    return out
+
+
+@gatv2.register_fake
+def _gatv2_fake(h_src, h_dst, rowptr, rows, items, split, col, att, heads, channels, negative_slope, bias, n_slots):
+    return h_src.new_empty((rowptr.shape[0] - 1, heads * channels))
+
+
+@torch.library.custom_op("kgx::gather_rows", mutates_args=())
+def gather_rows(table: torch.Tensor, rows: torch.Tensor) -> torch.Tensor:
+    table = _f32c(table)
+    dev = nat.require_device(table, rows)
+    n, F = rows.numel(), table.shape[1]
+    out = torch.empty((n, F), dtype=torch.float32, device=dev)
+    nat.check(
+        nat.lib().kgx_gather_rows(
+            nat.ptr(table), table.stride(0), nat.ptr(rows.contiguous()), n, F, nat.ptr(out), out.stride(0),
+            nat.stream(dev),
+        ),
+        "kgx_gather_rows",
+    )
+    return out
+
+
+@gather_rows.register_fake
+def _gather_rows_fake(table, rows):
+    return table.new_empty((rows.shape[0], table.shape[1]))
+
+
+@torch.library.custom_op("kgx::scatter_f32", mutates_args=())
+def scatter_f32(values: torch.Tensor, perm: torch.Tensor, n_out: int) -> torch.Tensor:
+    """out[perm[i]] = values[i]; positions not hit are zero."""
+    values = _f32c(values)
+    dev = nat.require_device(values, perm)
+    out = torch.zeros(n_out, dtype=torch.float32, device=dev)
+    nat.check(
+        nat.lib().kgx_scatter_f32(nat.ptr(values), nat.ptr(perm.contiguous()), values.numel(), nat.ptr(out),
+                                  nat.stream(dev)),
+        "kgx_scatter_f32",
+    )
+    return out
+
+
+@scatter_f32.register_fake
+def _scatter_fake(values, perm, n_out):
+    return values.new_empty((n_out,))
+
+
+# ---------------------------------------------------------------------------
+# graph-level helpers used by the layers
+# ---------------------------------------------------------------------------
+# When a list is installed here, every aggregation launch is bracketed by a
+# pair of torch.cuda.Events recorded on the current stream — the stream the
+# kernels are launched on — so a harness can time the kernels alone.
+EVENT_SINK: list | None = None
+
+
+def _timed(fn):
+    if EVENT_SINK is None:
+        return fn()
+    start = torch.cuda.Event(enable_timing=True)
+    end = torch.cuda.Event(enable_timing=True)
+    start.record()
+    out = fn()
+    end.record()
+    EVENT_SINK.append((start, end))
+    return out
+
+def aggregate(
+    g: CSRGraph,
+    table: torch.Tensor,
+    reduce: str | int = "sum",
+    *,
+    weighted: bool = False,
+    by_edge: bool = False,
+    epilogue: int = nat.EPI_NONE,
+    bias: torch.Tensor | None = None,
+    xroot: torch.Tensor | None = None,
+    gin_scale: float = 1.0,
+    exact: bool = False,
+) -> torch.Tensor:
+    """out[i] = EPI(REDUCE_{e in row i} table[idx[e]] * (w[e] if weighted)).
+
+    by_edge=False gathers node rows through `col` (the fused propagate path);
+    by_edge=True gathers rows of a per-edge message tensor through `eid`
+    (the reference's Aggregator.aggregate(messages, target_idx, dim_size)).
+    """
+    red = nat.REDUCE_IDS[reduce] if isinstance(reduce, str) else int(reduce)
+    items, _, split, _, n_slots = g.work(exact or red == nat.STD)
+    idx = g.eid if by_edge else g.col
+    w = g.w if weighted else None
+    if weighted and w is None:
+        raise ValueError("graph was built without GCN normalisation weights")
+    return _timed(lambda: torch.ops.kgx.spmm(
+        table, g.rowptr, g.rows, items, split, idx, w, n_slots, red, epilogue, bias, xroot, float(gin_scale)
+    ))
+
+
+def gatv2_aggregate(
+    g: CSRGraph,
+    h_src: torch.Tensor,
+    h_dst: torch.Tensor,
+    att: torch.Tensor,
+    heads: int,
+    channels: int,
+    negative_slope: float,
+    bias: torch.Tensor | None = None,
+    exact: bool = False,
+) -> torch.Tensor:
+    items, _, split, _, n_slots = g.work(exact)
+    return _timed(lambda: torch.ops.kgx.gatv2(
+        h_src, h_dst, g.rowptr, g.rows, items, split, g.col, att.reshape(-1), heads, channels,
+        float(negative_slope), bias, n_slots,
+    ))

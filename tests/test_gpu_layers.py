@@ -1,0 +1,255 @@
+"""Drop-in layer API on the GPU vs the reference restatement / golden fixtures.
+
+Mirrors the reference tests' toy graphs and contracts (tests/test_*_conv.py,
+tests/test_message_passing.py, tests/unit/test_error_handling.py).  Full-layer
+outputs use the north-star tolerance |a-b| <= 1e-5*max(1,|b|) (node-level X W
+GEMM vs the reference's per-edge matmul, 1-ulp pow); aggregations are exact.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+import keras_geometric_amd as kgx
+from keras_geometric_amd.layers import GATv2Conv, GCNConv, GINConv, MessagePassing, SAGEConv
+from oracle import reference as R
+
+pytestmark = pytest.mark.gpu
+T = torch.from_numpy
+
+
+def assert_tol(a, b, tol=1e-5):
+    a = a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
+    a = a.astype(np.float64)
+    b = np.asarray(b, np.float64)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    assert (np.isnan(a) == np.isnan(b)).all()
+    m = ~np.isnan(b)
+    err = np.abs(a[m] - b[m]) / np.maximum(1.0, np.abs(b[m]))
+    assert err.size == 0 or err.max() <= tol, f"max scaled err {err.max():.3e}"
+
+
+def exact(a, b):
+    a = a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else a
+    np.testing.assert_array_equal(a, b)
+
+
+# ---------------------------------------------------------------- GCN
+@pytest.mark.parametrize("name,cfg", [
+    ("default", dict(use_bias=True, normalize=True, add_self_loops=True)),
+    ("nobias", dict(use_bias=False, normalize=True, add_self_loops=True)),
+    ("nonorm", dict(use_bias=True, normalize=False, add_self_loops=True)),
+    ("noloops", dict(use_bias=True, normalize=True, add_self_loops=False)),
+])
+def test_gcn_toy(dev, golden, name, cfg):
+    g = golden("toy_gcn")
+    layer = GCNConv(output_dim=12, **cfg)
+    x = T(g["x"]).to(dev)
+    ei = T(g["edge_index"]).to(dev)
+    layer([x, ei])
+    layer.set_weights([g["kernel"], g["bias"]] if cfg["use_bias"] else [g["kernel"]])
+    assert_tol(layer([x, ei]), g[f"y_{name}"])
+
+
+def test_gcn_edge_index_transposed_and_numpy(dev, golden):
+    g = golden("toy_gcn")
+    layer = GCNConv(output_dim=12)
+    layer([g["x"], g["edge_index"]])
+    layer.set_weights([g["kernel"], g["bias"]])
+    assert_tol(layer([g["x"], g["edge_index"].T.copy()]), g["y_transposed_input"])
+    assert_tol(layer([g["x"].astype(np.float64), g["edge_index"].astype(np.int64)]), g["y_default"])
+
+
+def test_gcn_rmat_and_cora(dev, golden):
+    g = golden("rmat_small")
+    layer = GCNConv(output_dim=32)
+    x, ei = T(g["x"]).to(dev), T(g["edge_index"]).to(dev)
+    layer([x, ei])
+    layer.set_weights([g["gcn_W"], g["gcn_b"]])
+    assert_tol(layer([x, ei]), g["gcn_y"])
+    c = golden("cora_like")
+    xc = np.unpackbits(c["x_packed"], axis=1)[:, : int(c["n_features"])].astype(np.float32)
+    xc, eic = T(xc).to(dev), T(c["edge_index"]).to(dev)
+    l1, l2 = GCNConv(64), GCNConv(7)
+    l1([xc, eic])
+    l1.set_weights([c["W1"], c["b1"]])
+    h = torch.relu(l1([xc, eic]))
+    assert_tol(h, c["h1"])
+    l2([h, eic])
+    l2.set_weights([c["W2"], c["b2"]])
+    assert_tol(l2([h, eic]), c["y"])
+
+
+def test_gcn_edge_cases(dev, golden):
+    e = golden("edge_cases")
+    layer = GCNConv(output_dim=16)
+    x = T(e["x"]).to(dev)
+    layer([x, T(e["ei_dup"]).to(dev)])
+    layer.set_weights([e["W"], e["b"]])
+    for key in ("dup", "neg"):
+        assert_tol(layer([x, T(e[f"ei_{key}"]).to(dev)]), e[f"y_{key}"])
+    for key in ("nan", "inf"):
+        y = layer([T(e[f"x_{key}"]).to(dev), T(e["ei_r"]).to(dev)])
+        assert_tol(y, e[f"y_{key}"])
+    # empty graph / no edges (test_gcn_conv.py:310-359)
+    assert tuple(layer([torch.zeros((0, 8), device=dev), torch.zeros((2, 0), dtype=torch.int32)]).shape) == (0, 16)
+    y = GCNConv(16, add_self_loops=False)
+    out = y([x, torch.zeros((2, 0), dtype=torch.int32, device=dev)])
+    exact(out, (x @ y.kernel + y.bias).detach().cpu().numpy())
+    with pytest.raises(ValueError):
+        layer([x, torch.randint(0, 10, (3, 20), device=dev)])
+    with pytest.raises(IndexError):
+        layer([x, torch.tensor([[0, 1, 15], [1, 2, 3]], device=dev)])
+    with pytest.raises(ValueError):
+        layer([x])
+
+
+def test_gcn_deterministic(dev, golden):
+    g = golden("rmat_small")
+    layer = GCNConv(output_dim=32)
+    x, ei = T(g["x"]).to(dev), T(g["edge_index"]).to(dev)
+    a = layer([x, ei])
+    kgx.clear_cache()
+    b = layer([x, ei])
+    exact(a, b.detach().cpu().numpy())
+
+
+# ---------------------------------------------------------------- GIN
+@pytest.mark.parametrize("aggr", ["sum", "mean", "max"])
+@pytest.mark.parametrize("eps", [0.0, 0.5])
+def test_gin_toy(dev, golden, aggr, eps):
+    g = golden("toy_gin")
+    layer = GINConv(output_dim=12, mlp_hidden=[16], aggregator=aggr, eps_init=eps, exact=True)
+    x, ei = T(g["x"]).to(dev), T(g["edge_index"]).to(dev)
+    layer([x, ei])
+    layer.set_weights([g["W1"], g["b1"], g["W2"], g["b2"]])
+    assert_tol(layer([x, ei]), g[f"y_{aggr}_{eps}"])
+
+
+def test_gin_train_eps_and_no_edges(dev, golden):
+    g = golden("toy_gin")
+    layer = GINConv(output_dim=12, mlp_hidden=[16], eps_init=0.5, train_eps=True)
+    x, ei = T(g["x"]).to(dev), T(g["edge_index"]).to(dev)
+    layer([x, ei])
+    layer.set_weights([np.array([0.5], np.float32), g["W1"], g["b1"], g["W2"], g["b2"]])
+    assert_tol(layer([x, ei]), g["y_sum_0.5"])
+    out = layer([x, torch.zeros((2, 0), dtype=torch.int32, device=dev)])
+    assert tuple(out.shape) == (6, 12)
+
+
+# ---------------------------------------------------------------- SAGE
+@pytest.mark.parametrize("aggr", ["mean", "max", "sum", "min", "std"])
+@pytest.mark.parametrize("root", [True, False])
+@pytest.mark.parametrize("norm", [False, True])
+def test_sage_toy(dev, golden, aggr, root, norm):
+    g = golden("toy_sage")
+    layer = SAGEConv(output_dim=12, aggregator=aggr, root_weight=root, normalize=norm, exact=True)
+    x, ei = T(g["x"]).to(dev), T(g["edge_index"]).to(dev)
+    layer([x, ei])
+    w = [g["b"], g["Wn"]] + ([g["Ws"]] if root else [])
+    layer.set_weights(w)
+    assert_tol(layer([x, ei]), g[f"y_{aggr}_{int(root)}_{int(norm)}"])
+    exact(layer.aggregate_neighbors(x, ei, x.shape[0]), g[f"aggr_{aggr}"])
+
+
+def test_sage_pooling(dev, golden):
+    g = golden("toy_sage")
+    layer = SAGEConv(output_dim=12, aggregator="pooling")
+    x, ei = T(g["x"]).to(dev), T(g["edge_index"]).to(dev)
+    layer([x, ei])
+    layer.set_weights([g["b"], g["Wp"], g["bp"], g["Wnp"], g["Ws"]])
+    assert_tol(layer([x, ei]), g["y_pooling"])
+
+
+# ---------------------------------------------------------------- GATv2
+@pytest.mark.parametrize("heads,C", [(1, 8), (4, 8), (2, 16)])
+@pytest.mark.parametrize("concat", [True, False])
+def test_gatv2_toy(dev, golden, heads, C, concat):
+    g = golden("toy_gat")
+    key = f"h{heads}_c{C}_{int(concat)}"
+    layer = GATv2Conv(output_dim=C, heads=heads, concat=concat)
+    x, ei = T(g["x"]).to(dev), T(g["edge_index"]).to(dev)
+    layer([x, ei])
+    layer.set_weights([g[f"att_{key}"], g[f"b_{key}"], g[f"W_{key}"]])
+    assert_tol(layer([x, ei]), g[f"y_{key}"])
+
+
+def test_gatv2_rmat(dev, golden):
+    g = golden("rmat_small")
+    layer = GATv2Conv(output_dim=8, heads=4)
+    x, ei = T(g["x"]).to(dev), T(g["edge_index"]).to(dev)
+    layer([x, ei])
+    layer.set_weights([g["gat_att"], g["gat_b"], g["gat_W"]])
+    assert_tol(layer([x, ei]), g["gat_y"])
+
+
+# ---------------------------------------------------------------- MessagePassing
+def test_message_passing_known_answers(dev):
+    """tests/test_message_passing.py:54-155 through the layer API on the GPU."""
+    cases = {
+        "mean": ([[1, 2], [3, 4], [5, 6]], [0, 0, 1], 3, [[2, 3], [5, 6], [0, 0]]),
+        "max": ([[1, 5], [3, 2], [2, 4]], [0, 0, 1], 3, [[3, 5], [2, 4], [0, 0]]),
+        "sum": ([[1, 2], [3, 4], [5, 6]], [0, 0, 1], 3, [[4, 6], [5, 6], [0, 0]]),
+        "min": ([[1, 5], [3, 2], [2, 4]], [0, 0, 1], 3, [[1, 2], [2, 4], [0, 0]]),
+        "std": ([[1, 2], [3, 4], [5, 6], [7, 8]], [0, 0, 1, 1], 2, [[1, 1], [1, 1]]),
+    }
+    for aggr, (m, tgt, n, want) in cases.items():
+        layer = MessagePassing(aggregator=aggr)
+        out = layer.aggregate(np.array(m, np.float32), np.array(tgt, np.int32), num_nodes=n)
+        np.testing.assert_allclose(out.cpu().numpy(), np.array(want, np.float32), rtol=1e-5)
+    with pytest.raises(ValueError, match="Invalid aggregator"):
+        MessagePassing(aggregator="invalid")
+
+
+def test_message_passing_propagate_and_hooks(dev, golden):
+    g = golden("rmat_small")
+    x, ei = T(g["x"]).to(dev), T(g["edge_index"]).to(dev)
+    for aggr in ("sum", "mean", "max", "min", "std"):
+        mp = MessagePassing(aggregator=aggr, exact=True)
+        exact(mp([x, ei]), g[f"aggr_{aggr}"])
+
+    class Scaled(MessagePassing):
+        def pre_aggregate(self, messages):
+            return messages * 2
+
+        def post_update(self, x, x_updated):
+            return x_updated + 1
+
+    out = Scaled(aggregator="sum", exact=True)([x, ei])
+    assert_tol(out, g["aggr_sum"] * 2 + 1)
+
+    class EdgeMsg(MessagePassing):
+        def message(self, x_i, x_j, edge_attr=None, **kw):
+            return x_j - x_i
+
+    ref = R.propagate(T(g["x"]), T(g["edge_index"]), "mean", message=lambda xi, xj: xj - xi)
+    exact(EdgeMsg(aggregator="mean", exact=True)([x, ei]), ref.numpy())
+    e = golden("edge_cases")
+    out = MessagePassing(aggregator="sum").propagate(
+        x=(T(e["x_dst"]).to(dev), T(e["x_src"]).to(dev)), edge_index=T(e["ei_bip"]).to(dev))
+    exact(out, e["aggr_bip_sum"])
+    mp = MessagePassing()
+    assert tuple(mp.propagate(x=torch.zeros((0, 8), device=dev), edge_index=torch.zeros((2, 0))).shape) == (0, 8)
+    with pytest.raises(ValueError):
+        mp("invalid_input")
+    with pytest.raises(ValueError):
+        mp([x])
+
+
+def test_edge_index_cache_int32(dev):
+    mp = MessagePassing()
+    x = torch.randn(5, 8, device=dev)
+    ei = np.array([[0, 1, 2, 3, 4, 0], [1, 2, 3, 4, 0, 2]], dtype=np.int64)
+    mp([x, ei])
+    assert mp._cached_edge_idx.dtype == torch.int32
+    assert tuple(mp._cached_edge_idx.shape) == ei.shape
+
+
+def test_utils(dev, golden):
+    g = golden("rmat_small")
+    ei = T(g["edge_index"]).to(dev)
+    N = g["x"].shape[0]
+    loops = kgx.add_self_loops(ei, N)
+    exact(loops, R.add_self_loops(T(g["edge_index"]), N).numpy())
+    norm = kgx.compute_gcn_normalization(loops, N).cpu().numpy()
+    assert_tol(norm, g["gcn_norm_loops"], tol=2e-7)

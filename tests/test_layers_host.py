@@ -1,0 +1,73 @@
+"""Host-side layer logic that needs no GPU (CPU)."""
+
+import numpy as np
+import pytest
+import torch
+
+from keras_geometric_amd import graph as G
+from keras_geometric_amd.layers import (
+    AggregatorFactory,
+    GATv2Conv,
+    GCNConv,
+    GINConv,
+    MessagePassing,
+    SAGEConv,
+)
+
+
+def test_invalid_aggregators():
+    """tests/unit/test_error_handling.py:26-40."""
+    for bad in ["invalid", "median", "variance", ""]:
+        with pytest.raises(ValueError, match="Invalid aggregator"):
+            MessagePassing(aggregator=bad)
+        with pytest.raises(ValueError, match="Invalid aggregator"):
+            GINConv(output_dim=16, aggregator=bad)
+        with pytest.raises(ValueError, match="Invalid aggregator"):
+            SAGEConv(output_dim=16, aggregator=bad)
+    with pytest.raises(ValueError, match="Invalid aggregator"):
+        GINConv(output_dim=16, aggregator="min")
+    assert AggregatorFactory.get_available_aggregators() == ["mean", "max", "sum", "min", "std"]
+
+
+def test_message_passing_input_contract():
+    mp = MessagePassing(aggregator="mean")
+    with pytest.raises(ValueError):
+        mp.call("invalid_input")
+    with pytest.raises(ValueError):
+        mp.call([])
+    with pytest.raises(ValueError):
+        mp([np.zeros((3, 2), np.float32)])
+
+
+def test_configs_round_trip():
+    for layer in (GCNConv(8, add_self_loops=False), GINConv(8, mlp_hidden=[4], eps_init=0.1),
+                  SAGEConv(8, aggregator="pooling", pool_hidden_dim=6), GATv2Conv(4, heads=2, concat=False)):
+        cfg = layer.get_config()
+        again = type(layer).from_config(cfg)
+        assert again.get_config() == cfg
+    assert GCNConv(8).get_config()["aggregator"] == "sum"
+    assert SAGEConv(8, aggregator="pooling").get_config()["aggregator"] == "pooling"
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU failure mode")
+def test_no_cpu_fallback():
+    layer = GCNConv(4)
+    with pytest.raises(RuntimeError, match="no CPU execution path"):
+        layer([np.zeros((3, 2), np.float32), np.array([[0, 1], [1, 2]])])
+
+
+def test_split_len_policy():
+    assert G.default_split_len(10_000, 128) == 256
+    assert G.default_split_len(110_000_000, 128) == 1024
+    assert G.default_split_len(11_000_000, 128) == 256
+    for e in (0, 1, 10**9):
+        v = G.default_split_len(e, 100)
+        assert 256 <= v <= 8192 and v & (v - 1) == 0
+
+
+def test_cache_key_tracks_version():
+    t = torch.zeros((2, 4), dtype=torch.int32)
+    k1 = G.cache_key(t, 1)
+    t[0, 0] = 1
+    assert G.cache_key(t, 1) != k1
+    assert G.cache_key(np.zeros((2, 4)), 1) is None
