@@ -14,6 +14,7 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include "kgx_internal.h"
+#include "kgx_vec.h"
 
 namespace kgx {
 namespace {
@@ -92,9 +93,6 @@ __global__ void csr_col_kernel(const int32_t* __restrict__ eid, const int32_t* _
 
 // Integer in-degree; fp32 degree as the reference computes it: a sequential
 // fp32 sum of ones (utils/main.py:23-24, aggregators.py:66-69) saturates at 2^24.
-__device__ __forceinline__ float ref_degree_f32(int32_t deg) {
-  return float(deg < (1 << 24) ? deg : (1 << 24));
-}
 
 __global__ void csr_deg_kernel(const int32_t* __restrict__ rowptr, int64_t n_dst, int flags,
                                int32_t* __restrict__ deg, float* __restrict__ dinv,
@@ -108,8 +106,8 @@ __global__ void csr_deg_kernel(const int32_t* __restrict__ rowptr, int64_t n_dst
     if (flags & KGX_CSR_GCN_NORM) {
       // pow(deg + 1e-12, -0.5), correctly rounded (= 1/sqrt in IEEE RN); deg 0 -> 1e6.
       // (torch's tensor-exponent powf may differ by 1 ulp: DESIGN.md "GCN norm".)
-      const float x = __fadd_rn(ref_degree_f32(d), 1e-12f);
-      dinv[r] = __fdiv_rn(1.0f, __fsqrt_rn(x));
+      const float x = __fadd_rn(ref_count_f32(d), 1e-12f);
+      dinv[r] = __fdiv_rn(1.0f, sqrt_rn(x));
     }
   }
   // wave max then one atomic per wave

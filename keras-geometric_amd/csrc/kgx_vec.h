@@ -56,4 +56,10 @@ __device__ __forceinline__ float amax_update(float acc, float v) {
 
 __device__ __forceinline__ bool is_inf(float v) { return __builtin_isinf(v); }
 
+// IEEE round-to-nearest sqrt.  NOTE: on gfx950 `__fsqrt_rn` lowers to a bare
+// v_sqrt_f32 (~1 ulp); plain sqrtf under hipcc's default
+// -fhip-fp32-correctly-rounded-divide-sqrt expands to v_sqrt + an fma-based
+// correction and is correctly rounded, like the CPU's vsqrtps.
+__device__ __forceinline__ float sqrt_rn(float x) { return sqrtf(x); }
+
 }  // namespace kgx

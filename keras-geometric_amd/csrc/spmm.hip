@@ -284,7 +284,7 @@ __global__ __launch_bounds__(kBlock) void spmm_std_kernel(SpmmArgs a) {
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
         const float var = __fdiv_rn(ssd[k], safe);
-        const float sd = __fsqrt_rn(fmaxf(var, 0.0f) /* maximum(variance, 0) */);
+        const float sd = sqrt_rn(fmaxf(var, 0.0f) /* maximum(variance, 0) */);
         r[k] = cnt <= 1.0f ? 0.0f : (var != var ? var : sd);
       }
       epilogue<VEC>(a, row, f, r);

@@ -36,6 +36,10 @@ class Aggregator(ABC):
             return torch.zeros((dim_size, messages.shape[1]), dtype=messages.dtype, device=messages.device)
         if graph is None:
             tgt = to_device_tensor(target_idx, torch.int32, messages.device).reshape(-1)
+            if self.reduce == "std" and bool((tgt >= dim_size).any()):
+                # StdAggregator gathers mean[target] with take() (aggregators.py:208),
+                # which raises on ids >= dim_size; the segment sums alone would drop them.
+                raise IndexError("index out of range in self")
             ei = torch.stack([torch.zeros_like(tgt), tgt])
             graph = graph_for(target_idx, ei, 0, int(dim_size), segment_only=True, n_features=messages.shape[1])
         return self._reduce(graph, messages, exact)

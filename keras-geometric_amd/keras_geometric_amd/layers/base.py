@@ -202,16 +202,25 @@ class Layer(torch.nn.Module):
         while attr in self._parameters:
             attr = f"{name}_{i}"
             i += 1
+        if attr in self.__dict__:  # placeholder attribute (e.g. self.kernel = None in __init__)
+            del self.__dict__[attr]
         self.register_parameter(attr, p)
         self._weight_order.append(attr)
         return p
 
     @property
     def weights(self) -> list[torch.nn.Parameter]:
+        """Own weights in creation order, then sub-layers' (Keras Layer.weights order)."""
         out = [self._parameters[k] for k in self._weight_order]
-        for m in self.children():
-            if isinstance(m, Layer):
-                out.extend(m.weights)
+
+        def visit(mod):
+            for m in mod.children():
+                if isinstance(m, Layer):
+                    out.extend(m.weights)
+                else:  # containers such as ModuleList
+                    visit(m)
+
+        visit(self)
         return out
 
     def get_weights(self) -> list[np.ndarray]:

@@ -24,7 +24,8 @@ def assert_tol(a, b, tol=1e-5):
     b = np.asarray(b, np.float64)
     assert a.shape == b.shape, (a.shape, b.shape)
     assert (np.isnan(a) == np.isnan(b)).all()
-    m = ~np.isnan(b)
+    assert (np.isinf(a) == np.isinf(b)).all() and (a[np.isinf(b)] == b[np.isinf(b)]).all()
+    m = np.isfinite(b)
     err = np.abs(a[m] - b[m]) / np.maximum(1.0, np.abs(b[m]))
     assert err.size == 0 or err.max() <= tol, f"max scaled err {err.max():.3e}"
 
@@ -149,7 +150,11 @@ def test_sage_toy(dev, golden, aggr, root, norm):
     w = [g["b"], g["Wn"]] + ([g["Ws"]] if root else [])
     layer.set_weights(w)
     assert_tol(layer([x, ei]), g[f"y_{aggr}_{int(root)}_{int(norm)}"])
-    exact(layer.aggregate_neighbors(x, ei, x.shape[0]), g[f"aggr_{aggr}"])
+    aggr_out = layer.aggregate_neighbors(x, ei, x.shape[0]).cpu().numpy()
+    if aggr == "std":  # correctly rounded sqrt vs ATen's Sleef sqrt: <= 1 ulp
+        assert_tol(aggr_out, g[f"aggr_{aggr}"], tol=2.5e-7)
+    else:
+        exact(aggr_out, g[f"aggr_{aggr}"])
 
 
 def test_sage_pooling(dev, golden):
@@ -206,7 +211,10 @@ def test_message_passing_propagate_and_hooks(dev, golden):
     x, ei = T(g["x"]).to(dev), T(g["edge_index"]).to(dev)
     for aggr in ("sum", "mean", "max", "min", "std"):
         mp = MessagePassing(aggregator=aggr, exact=True)
-        exact(mp([x, ei]), g[f"aggr_{aggr}"])
+        if aggr == "std":
+            assert_tol(mp([x, ei]), g[f"aggr_{aggr}"], tol=2.5e-7)
+        else:
+            exact(mp([x, ei]), g[f"aggr_{aggr}"])
 
     class Scaled(MessagePassing):
         def pre_aggregate(self, messages):
