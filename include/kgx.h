@@ -93,6 +93,18 @@ int kgx_csr_build(const int32_t* src, const int32_t* dst, int64_t E,
                   int64_t* info, kgx_stream_t stream);
 
 /* ---------------------------------------------------------------------------
+ * GCN normalisation for a CSR whose sources index a different table than its
+ * rows (a destination-range shard: rows = owned nodes, sources = owned + halo
+ * nodes).  Same arithmetic as KGX_CSR_GCN_NORM (utils/main.py:20-33):
+ *   dinv[i] = (float(min(deg[i], 2^24)) + 1e-12f)^-0.5  (correctly rounded)
+ *   w[e]    = dinv_dst[row(e)] * dinv_src[col[e]]       (CSR order)
+ * ------------------------------------------------------------------------- */
+int kgx_gcn_dinv(const int32_t* deg, int64_t n, float* dinv, kgx_stream_t stream);
+int kgx_gcn_edge_norm(const int32_t* rowptr, const int32_t* col, int64_t n_dst,
+                      const float* dinv_dst, const float* dinv_src, float* w,
+                      kgx_stream_t stream);
+
+/* ---------------------------------------------------------------------------
  * Row schedule (no reference counterpart: the reference has one device and no
  * scheduling).  Orders destination rows by descending degree (log2 buckets,
  * stable) so hub rows start first, and cuts rows with deg >= split_len into

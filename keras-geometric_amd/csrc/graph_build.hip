@@ -94,6 +94,11 @@ __global__ void csr_col_kernel(const int32_t* __restrict__ eid, const int32_t* _
 // Integer in-degree; fp32 degree as the reference computes it: a sequential
 // fp32 sum of ones (utils/main.py:23-24, aggregators.py:66-69) saturates at 2^24.
 
+__device__ __forceinline__ float gcn_dinv(int32_t d) {
+  // pow(deg + 1e-12, -0.5), correctly rounded (= 1/sqrt in IEEE RN); deg 0 -> 1e6.
+  return __fdiv_rn(1.0f, sqrt_rn(__fadd_rn(ref_count_f32(d), 1e-12f)));
+}
+
 __global__ void csr_deg_kernel(const int32_t* __restrict__ rowptr, int64_t n_dst, int flags,
                                int32_t* __restrict__ deg, float* __restrict__ dinv,
                                CsrStatus* __restrict__ st) {
@@ -103,12 +108,8 @@ __global__ void csr_deg_kernel(const int32_t* __restrict__ rowptr, int64_t n_dst
     const int32_t d = rowptr[r + 1] - rowptr[r];
     deg[r] = d;
     mx = d > (int64_t)mx ? (unsigned long long)d : mx;
-    if (flags & KGX_CSR_GCN_NORM) {
-      // pow(deg + 1e-12, -0.5), correctly rounded (= 1/sqrt in IEEE RN); deg 0 -> 1e6.
-      // (torch's tensor-exponent powf may differ by 1 ulp: DESIGN.md "GCN norm".)
-      const float x = __fadd_rn(ref_count_f32(d), 1e-12f);
-      dinv[r] = __fdiv_rn(1.0f, sqrt_rn(x));
-    }
+    // (torch's tensor-exponent powf may differ by 1 ulp: DESIGN.md "GCN norm".)
+    if (flags & KGX_CSR_GCN_NORM) dinv[r] = gcn_dinv(d);
   }
   // wave max then one atomic per wave
   for (int o = 32; o > 0; o >>= 1) {
@@ -160,6 +161,23 @@ CsrLayout csr_layout(void* ws, int64_t total, int64_t n_dst) {
   L.sort_tmp = c.take<char>(L.sort_bytes);
   L.total = c.used();
   return L;
+}
+
+__global__ void gcn_dinv_kernel(const int32_t* __restrict__ deg, int64_t n, float* __restrict__ dinv) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) dinv[i] = gcn_dinv(deg[i]);
+}
+
+// one wave per row, lanes stride over the row's edges (coalesced)
+__global__ void gcn_edge_norm_kernel(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                                     int64_t n_dst, const float* __restrict__ dinv_dst,
+                                     const float* __restrict__ dinv_src, float* __restrict__ w) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t r = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; r < n_dst; r += nw) {
+    const float dr = dinv_dst[r];
+    for (int32_t e = rowptr[r] + lane; e < rowptr[r + 1]; e += 64) w[e] = __fmul_rn(dr, dinv_src[col[e]]);
+  }
 }
 
 // --------------------------------------------------------------------------
@@ -607,6 +625,25 @@ extern "C" int kgx_scatter_f32(const float* in, const int32_t* perm, int64_t n, 
   if (n == 0) return KGX_OK;
   KGX_REQUIRE(in && perm && out, KGX_ERR_ARG, "kgx_scatter_f32: null pointer");
   hipLaunchKernelGGL(scatter_f32_kernel, dim3(grid_for(n)), dim3(kBlock), 0, stream, in, perm, n, out);
+  KGX_CHECK_LAUNCH();
+  return KGX_OK;
+}
+
+extern "C" int kgx_gcn_dinv(const int32_t* deg, int64_t n, float* dinv, kgx_stream_t stream_) {
+  KGX_REQUIRE(n >= 0 && (n == 0 || (deg && dinv)), KGX_ERR_ARG, "kgx_gcn_dinv: bad arguments");
+  if (n == 0) return KGX_OK;
+  hipLaunchKernelGGL(gcn_dinv_kernel, dim3(grid_for(n, 8192)), dim3(kBlock), 0, as_stream(stream_), deg, n, dinv);
+  KGX_CHECK_LAUNCH();
+  return KGX_OK;
+}
+
+extern "C" int kgx_gcn_edge_norm(const int32_t* rowptr, const int32_t* col, int64_t n_dst, const float* dinv_dst,
+                                 const float* dinv_src, float* w, kgx_stream_t stream_) {
+  KGX_REQUIRE(n_dst >= 0 && (n_dst == 0 || (rowptr && col && dinv_dst && dinv_src && w)), KGX_ERR_ARG,
+              "kgx_gcn_edge_norm: bad arguments");
+  if (n_dst == 0) return KGX_OK;
+  hipLaunchKernelGGL(gcn_edge_norm_kernel, dim3(grid_for(n_dst * 64, 8192)), dim3(kBlock), 0, as_stream(stream_),
+                     rowptr, col, n_dst, dinv_dst, dinv_src, w);
   KGX_CHECK_LAUNCH();
   return KGX_OK;
 }

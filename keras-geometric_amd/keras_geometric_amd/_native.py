@@ -40,6 +40,8 @@ _SIGNATURES = {
         _i32p, _i32p, _i32p, _i32p, _f32p, _f32p,
         ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p,
     ],
+    "kgx_gcn_dinv": [_i32p, _i64, _f32p, ctypes.c_void_p],
+    "kgx_gcn_edge_norm": [_i32p, _i32p, _i64, _f32p, _f32p, _f32p, ctypes.c_void_p],
     "kgx_schedule_workspace_bytes": [_i64, ctypes.POINTER(ctypes.c_size_t)],
     "kgx_schedule_build": [
         _i32p, _i64, ctypes.c_int32, _i32p, _i32p, _i64, _i32p,

@@ -1,0 +1,142 @@
+"""Multi-process (world_size 2, gloo, CPU) test of the destination-range
+sharding and halo-exchange logic of keras_geometric_amd.distributed.
+
+The device work is done by a CPU backend built on the oracle (sequential
+accumulation in CSR order), so the sharded result must be BIT-IDENTICAL to the
+same computation on the unsharded graph — the property the HIP backend keeps
+on the GPU (each row's edges stay in global input order on its owner)."""
+
+import os
+import socket
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from keras_geometric_amd import _native as nat
+from keras_geometric_amd import distributed as kd
+from oracle import keras_torch as K
+from oracle import reference as R
+from oracle.rmat import rmat_edges, scale_for
+
+
+class OracleBackend:
+    """CPU stand-in for KgxBackend (test infrastructure)."""
+
+    def build_graph(self, src, dst, n_src, n_dst, n_features):
+        rowptr, col, eid, deg = R.csr_by_destination(src.numpy(), dst.numpy(), n_src, n_dst, self_loops=False)
+        t = torch.from_numpy
+        return SimpleNamespace(rowptr=t(rowptr), col=t(col), eid=t(eid), deg=t(deg), n_dst=n_dst,
+                               kept=int(rowptr[-1]), dinv=None, w=None, device=torch.device("cpu"))
+
+    def dinv(self, deg):
+        d = torch.clamp(deg, max=1 << 24).float() + torch.tensor(1e-12, dtype=torch.float32)
+        return (1.0 / torch.from_numpy(np.sqrt(d.numpy()))).float()
+
+    def edge_norm(self, g, dinv_dst, dinv_src):
+        rows = torch.repeat_interleave(torch.arange(g.n_dst), g.deg.long())
+        return dinv_dst[rows] * dinv_src[g.col.long()]
+
+    def gather_rows(self, table, rows):
+        return table[rows.long()]
+
+    def aggregate(self, g, table, reduce="sum", weighted=False, epilogue=nat.EPI_NONE, bias=None, **_):
+        rows = torch.repeat_interleave(torch.arange(g.n_dst), g.deg.long())
+        msg = table[g.col.long()]
+        if weighted:
+            msg = msg * g.w.unsqueeze(1)
+        out = R.aggregate(reduce, msg, rows, g.n_dst)
+        if epilogue == nat.EPI_BIAS:
+            out = K.add(out, bias)
+        return out
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+N, E, F_IN, F_OUT = 1000, 12000, 16, 8
+
+
+def _graph():
+    s, d = rmat_edges(21, scale_for(N), N, 0, E)
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((N, F_IN)).astype(np.float32)
+    W = (rng.standard_normal((F_IN, F_OUT)) * 0.3).astype(np.float32)
+    b = rng.standard_normal(F_OUT).astype(np.float32)
+    return s, d, x, W, b
+
+
+def _full_graph_reference(world_size=1):
+    """The same backend on the unsharded graph (world of one)."""
+    s, d, x, W, b = _graph()
+    be = OracleBackend()
+    n = N
+    src = torch.from_numpy(s).long()
+    dst = torch.from_numpy(d).long()
+    ar = torch.arange(n)
+    g = be.build_graph(torch.cat([src, ar]).int(), torch.cat([dst, ar]).int(), n, n, F_OUT)
+    dinv = be.dinv(g.deg)
+    g.w = be.edge_norm(g, dinv, dinv)
+    h = torch.from_numpy(x) @ torch.from_numpy(W)
+    return be.aggregate(g, h, "sum", weighted=True, epilogue=nat.EPI_BIAS, bias=torch.from_numpy(b)), \
+        be.aggregate(g, torch.from_numpy(x), "max")
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        s, d, x, W, b = _graph()
+        bounds = kd.equal_bounds(N, world)
+        lo, hi = bounds[rank], bounds[rank + 1]
+        keep = (d >= lo) & (d < hi)  # stable: global input order kept
+        sg = kd.ShardedGraph.build(torch.from_numpy(s[keep]), torch.from_numpy(d[keep]), bounds,
+                                   backend=OracleBackend(), n_features=F_OUT)
+        h = torch.from_numpy(x[lo:hi]) @ torch.from_numpy(W)
+        table = sg.new_table(F_OUT, h)
+        table[: sg.n_local] = h
+        sg.halo_exchange(table)
+        gcn = sg.backend.aggregate(sg.graph, table, "sum", weighted=True, epilogue=nat.EPI_BIAS,
+                                   bias=torch.from_numpy(b))
+        mx = sg.propagate(torch.from_numpy(x[lo:hi]), "max")
+        q.put((rank, gcn.numpy(), mx.numpy(), sg.n_halo, sum(sg.send_counts)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_equals_unsharded_bitwise(world):
+    if torch.cuda.is_initialized():
+        pytest.skip("never start processes from a process that has initialised the GPU")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    for _ in range(world):
+        rank, gcn, mx, n_halo, n_send = q.get(timeout=90)
+        results[rank] = (gcn, mx, n_halo, n_send)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    gcn = np.concatenate([results[r][0] for r in range(world)])
+    mx = np.concatenate([results[r][1] for r in range(world)])
+    ref_gcn, ref_max = _full_graph_reference()
+    np.testing.assert_array_equal(gcn, ref_gcn.numpy())
+    np.testing.assert_array_equal(mx, ref_max.numpy())
+    assert sum(results[r][2] for r in range(world)) == sum(results[r][3] for r in range(world)) > 0
+    # and the oracle GCN layer within the north-star tolerance (1-ulp dinv differences)
+    s, d, x, W, b = _graph()
+    y = R.gcn_forward(torch.from_numpy(x), torch.from_numpy(np.stack([s, d])), torch.from_numpy(W),
+                      torch.from_numpy(b)).numpy()
+    err = np.abs(gcn - y) / np.maximum(1, np.abs(y))
+    assert err.max() <= 1e-5
