@@ -151,6 +151,24 @@ int kgx_spmm(int reduce, int epilogue,
              float* partials, kgx_stream_t stream);
 
 /* ---------------------------------------------------------------------------
+ * Fused aggregate -> dense transform (+ bias), one launch (plus a fix-up for
+ * split hub rows):
+ *   out[i,:] = bias + PRE( REDUCE_{e in row i} x[idx[e],:] * (w ? w[e] : 1) ) @ W
+ *   PRE = identity, or gin_scale * x[i,:] + aggr when pre_gin != 0.
+ * Replaces GCNConv's per-edge x_j @ W + segment_sum + bias (gcn_conv.py:233-272)
+ * and GINConv's (1+eps)x + aggr -> single-Dense MLP (gin_conv.py:216-225) by the
+ * algebraically equal aggregate-then-transform order (W applied once per row
+ * on f32 MFMA); tolerance-equal to the reference, not bit-equal.
+ * Shapes: F_in == 128, F_out a multiple of 16 <= 128, W [F_in, F_out] row-major.
+ * reduce in {SUM, MEAN, MAX, MIN}; partials: n_slots * 128 floats.
+ * ------------------------------------------------------------------------- */
+int kgx_spmm_gemm(int reduce, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
+                  const int32_t* items, int64_t n_items, const int32_t* split, int64_t n_split,
+                  const int32_t* idx, const float* w, const float* x, int64_t ld_x, int64_t F_in,
+                  const float* W, int64_t F_out, const float* bias, int pre_gin, float gin_scale,
+                  float* out, int64_t ld_out, float* partials, kgx_stream_t stream);
+
+/* ---------------------------------------------------------------------------
  * Fused GATv2 attention aggregation (single pass, online segment softmax).
  *   s[e,h]  = sum_c att[h,c] * leaky_relu(h_dst[i,h,c] + h_src[j,h,c], slope)
  *   alpha   = exp(s - max_i) / (sum_i exp(s - max_i) + 1e-10)

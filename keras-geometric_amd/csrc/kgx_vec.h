@@ -42,6 +42,32 @@ __device__ __forceinline__ void vstore(float* __restrict__ p, const float (&d)[V
   }
 }
 
+// Non-temporal variants (global_load/store ... nt): for data streamed once
+// (CSR indices / weights, output rows) so it does not displace reused rows.
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
+template <int VEC>
+__device__ __forceinline__ void vstore_nt(float* __restrict__ p, const float (&d)[VEC]) {
+  if constexpr (VEC >= 4) {
+#pragma unroll
+    for (int i = 0; i < VEC / 4; ++i) {
+      f32x4_t v = {d[4 * i], d[4 * i + 1], d[4 * i + 2], d[4 * i + 3]};
+      __builtin_nontemporal_store(v, reinterpret_cast<f32x4_t*>(p) + i);
+    }
+  } else if constexpr (VEC == 2) {
+    f32x2_t v = {d[0], d[1]};
+    __builtin_nontemporal_store(v, reinterpret_cast<f32x2_t*>(p));
+  } else {
+    __builtin_nontemporal_store(d[0], p);
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ T ld_nt(const T* p) {
+  return __builtin_nontemporal_load(p);
+}
+
 // fp32 degree as the reference computes it: segment_sum of fp32 ones, which a
 // sequential fp32 accumulation saturates at 2^24 (aggregators.py:66-69,194-196).
 __device__ __forceinline__ float ref_count_f32(int32_t n) {

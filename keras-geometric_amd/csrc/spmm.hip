@@ -20,6 +20,8 @@
 //   std  : layers/aggregators.py:182-228 (two-pass, N divisor, count<=1 -> 0)
 //   GCN message x_j W * norm (gcn_conv.py:233-248) with W pre-applied per node,
 //   GCN update + bias (gcn_conv.py:266-272), GIN (1+eps)*x + aggr (gin_conv.py:216-222).
+#include <cstdlib>
+
 #include "kgx_internal.h"
 #include "kgx_vec.h"
 
@@ -50,6 +52,7 @@ struct SpmmArgs {
   int epi;
   int G;
   int lgG;
+  int hints;  // bit0: nt loads of idx/w, bit1: nt stores of out (experiment knob, KGX_SPMM_HINTS)
 };
 
 template <int RED>
@@ -135,10 +138,18 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
     for (; e + U <= end; e += U) {
       int32_t c[U];
       float wt[U];
+      if (a.hints & 1) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        c[u] = a.idx[e + u];
-        if constexpr (WEIGHTED) wt[u] = a.w[e + u];
+        for (int u = 0; u < U; ++u) {
+          c[u] = ld_nt(a.idx + e + u);
+          if constexpr (WEIGHTED) wt[u] = ld_nt(a.w + e + u);
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          c[u] = a.idx[e + u];
+          if constexpr (WEIGHTED) wt[u] = a.w[e + u];
+        }
       }
       float v[U][NT][VEC];
 #pragma unroll
@@ -208,7 +219,8 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
 #pragma unroll
         for (int k = 0; k < VEC; ++k) r[k] = R::finish(acc[t][k], end - beg);
         epilogue<VEC>(a, row, fo[t], r);
-        vstore<VEC>(a.out + int64_t(row) * a.ld_o + fo[t], r);
+        if (a.hints & 2) vstore_nt<VEC>(a.out + int64_t(row) * a.ld_o + fo[t], r);
+        else vstore<VEC>(a.out + int64_t(row) * a.ld_o + fo[t], r);
       }
     }
   }
@@ -387,6 +399,11 @@ extern "C" int kgx_spmm(int reduce, int epilogue, const int32_t* rowptr, const i
   a.ld_o = ld_out;
   a.ld_x = ld_x;
   a.ld_p = F;
+  static const int hints = [] {
+    const char* h = getenv("KGX_SPMM_HINTS");
+    return h ? atoi(h) : 0;
+  }();
+  a.hints = hints;
 
   // widest vector the shapes and pointers allow
   auto ok = [&](int v) {

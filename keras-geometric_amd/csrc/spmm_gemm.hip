@@ -1,0 +1,340 @@
+// Fused aggregate -> dense transform for the kgx engine (gfx950, wave64).
+//
+//   out[i, :] = bias + PRE( REDUCE_{e in CSR row i} x[col_e, :] * (w_e) ) @ W
+//
+// GCNConv's reference order is transform-then-aggregate (per-edge x_j @ W,
+// gcn_conv.py:233-248); for F_in <= F_out the same linear map applied after
+// the (linear) aggregation reads the narrower rows and needs no [N, F_out]
+// intermediate: the separate X.W GEMM pass (read X, write H: 10.24 GB at the
+// north-star size) disappears.  The result differs from the reference's by
+// re-association only (tolerance-checked, not bit-checked).
+//
+// Block = 512 threads = 16 row-groups of 32 lanes (F_in = 128: float4 per
+// lane).  Per iteration the block takes 16 consecutive schedule items; each
+// group reduces its item's edges exactly like spmm_kernel (8 gathers in
+// flight, sequential RN adds) into an LDS tile row; then wave w (of 8)
+// computes output columns [16w, 16w+16) of the 16-row tile with 32
+// v_mfma_f32_16x16x4_f32 (K = 128), W's 16 columns held in 32 VGPRs per lane
+// for the whole kernel.  K order is permuted so each lane's A fragment is 32
+// contiguous floats of its tile row (8 ds_read_b128): k-step s uses
+// k = 32*(lane>>4) + s.  Hub-row chunks write raw partials; the fix-up kernel
+// combines them and applies W with VALU.
+#include "kgx_internal.h"
+#include "kgx_vec.h"
+
+namespace kgx {
+namespace {
+
+constexpr int kFin = 128;
+constexpr int kGroups = 16;       // rows per block iteration
+constexpr int kThreads = kGroups * 32;
+constexpr int kTileLd = kFin + 4;  // padded LDS row
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct FusedArgs {
+  const int32_t* rowptr;
+  const int32_t* rows;
+  int64_t n_rows;
+  const int4* items;
+  int64_t n_items;
+  const int4* split;
+  int64_t n_split;
+  const int32_t* idx;
+  const float* w;
+  const float* x;  // [*, 128] gathered rows
+  int64_t ld_x;
+  const float* W;  // [128, F_out] row-major
+  int F_out;
+  const float* bias;  // [F_out] or null
+  float* out;
+  int64_t ld_o;
+  float* partials;  // [n_slots, 128]
+  int pre_gin;      // apply gin_scale * x[row] + aggr before the transform
+  float gin_scale;
+};
+
+template <int RED>
+struct Red {
+  static __device__ __forceinline__ float init() {
+    if constexpr (RED == KGX_MAX || RED == KGX_MIN) return -__builtin_inff();
+    return 0.0f;
+  }
+  static __device__ __forceinline__ float msg(float v) {
+    if constexpr (RED == KGX_MIN) return -v;
+    return v;
+  }
+  static __device__ __forceinline__ float combine(float a, float v) {
+    if constexpr (RED == KGX_MAX || RED == KGX_MIN) return amax_update(a, v);
+    return __fadd_rn(a, v);
+  }
+  static __device__ __forceinline__ float finish(float a, int32_t deg) {
+    if constexpr (RED == KGX_MEAN) return __fdiv_rn(a, fmaxf(ref_count_f32(deg), 1e-8f));
+    if constexpr (RED == KGX_MAX) return is_inf(a) ? 0.0f : a;
+    if constexpr (RED == KGX_MIN) {
+      const float r = -a;
+      return is_inf(r) ? 0.0f : r;
+    }
+    return a;
+  }
+};
+
+template <int RED, bool WEIGHTED>
+__global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
+  using R = Red<RED>;
+  constexpr int U = 8;
+  __shared__ float tile[kGroups][kTileLd];
+  __shared__ int32_t tile_row[kGroups];
+
+  const int tid = threadIdx.x;
+  const int g = tid >> 5;     // row-group 0..15
+  const int lane = tid & 31;  // lane in the group
+  const int f = lane * 4;
+  const int wave = tid >> 6;  // 0..7 -> output columns [16 wave, 16 wave + 16)
+  const int wl = tid & 63;    // lane in the wave
+  const int n_col = wave * 16 + (wl & 15);
+  const int q = wl >> 4;
+  const bool mfma_wave = wave * 16 < a.F_out;
+
+  // W fragment for this wave's 16 columns, K permuted: k = 32 q + s.
+  float wb[32];
+#pragma unroll
+  for (int s = 0; s < 32; ++s) wb[s] = mfma_wave ? a.W[int64_t(32 * q + s) * a.F_out + n_col] : 0.0f;
+  const float bcol = (mfma_wave && a.bias) ? a.bias[n_col] : 0.0f;
+
+  const int64_t n_work = a.items ? a.n_items : a.n_rows;
+  for (int64_t base = int64_t(blockIdx.x) * kGroups; base < n_work; base += int64_t(gridDim.x) * kGroups) {
+    const int64_t it = base + g;
+    int32_t row = -1, beg = 0, end = 0, slot = -1;
+    if (it < n_work) {
+      if (a.items) {
+        const int4 v = a.items[it];
+        row = v.x;
+        beg = v.y;
+        end = v.z;
+        slot = v.w;
+      } else {
+        row = a.rows[it];
+        beg = a.rowptr[row];
+        end = a.rowptr[row + 1];
+      }
+    }
+    float acc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] = R::init();
+    int32_t e = beg;
+    for (; e + U <= end; e += U) {
+      int32_t c[U];
+      float wt[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        c[u] = a.idx[e + u];
+        if constexpr (WEIGHTED) wt[u] = a.w[e + u];
+      }
+      float v[U][4];
+#pragma unroll
+      for (int u = 0; u < U; ++u) vload<4>(v[u], a.x + int64_t(c[u]) * a.ld_x + f);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float m = WEIGHTED ? __fmul_rn(v[u][k], wt[u]) : v[u][k];
+          acc[k] = R::combine(acc[k], R::msg(m));
+        }
+    }
+    if (e < end) {
+      const int n = end - e;
+      int32_t c[U];
+      float wt[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int32_t ee = u < n ? e + u : end - 1;
+        c[u] = a.idx[ee];
+        if constexpr (WEIGHTED) wt[u] = a.w[ee];
+      }
+      float v[U][4];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (u < n) {
+          vload<4>(v[u], a.x + int64_t(c[u]) * a.ld_x + f);
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) v[u][k] = 0.0f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (u < n) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float m = WEIGHTED ? __fmul_rn(v[u][k], wt[u]) : v[u][k];
+            acc[k] = R::combine(acc[k], R::msg(m));
+          }
+        }
+      }
+    }
+    const bool full_row = row >= 0 && slot < 0;
+    if (row >= 0 && slot >= 0) {
+      vstore<4>(a.partials + int64_t(slot) * kFin + f, acc);
+    }
+    float r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r[k] = full_row ? R::finish(acc[k], end - beg) : 0.0f;
+    if (full_row && a.pre_gin) {
+      float xv[4];
+      vload<4>(xv, a.x + int64_t(row) * a.ld_x + f);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) r[k] = __fadd_rn(__fmul_rn(a.gin_scale, xv[k]), r[k]);
+    }
+    *reinterpret_cast<float4*>(&tile[g][f]) = make_float4(r[0], r[1], r[2], r[3]);
+    if (lane == 0) tile_row[g] = full_row ? row : -1;
+    __syncthreads();
+
+    if (mfma_wave) {
+      const int m = wl & 15;
+      float af[32];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float4 t4 = *reinterpret_cast<const float4*>(&tile[m][32 * q + 4 * i]);
+        af[4 * i + 0] = t4.x;
+        af[4 * i + 1] = t4.y;
+        af[4 * i + 2] = t4.z;
+        af[4 * i + 3] = t4.w;
+      }
+      f32x4 d = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int s = 0; s < 32; ++s) d = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], wb[s], d, 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int rr = tile_row[4 * q + j];
+        if (rr >= 0) a.out[int64_t(rr) * a.ld_o + n_col] = d[j] + bcol;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Split rows: combine chunk partials in order, finish, then out = v @ W + b (VALU).
+template <int RED>
+__global__ __launch_bounds__(256) void spmm_gemm_fixup_kernel(FusedArgs a) {
+  using R = Red<RED>;
+  __shared__ float vrow[8][kFin];
+  const int g = threadIdx.x >> 5, lane = threadIdx.x & 31;
+  for (int64_t base = int64_t(blockIdx.x) * 8; base < a.n_split; base += int64_t(gridDim.x) * 8) {
+    const int64_t it = base + g;
+    int32_t row = -1;
+    if (it < a.n_split) {
+      const int4 s = a.split[it];
+      row = s.x;
+      float acc[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[k] = R::init();
+      for (int32_t c = 0; c < s.z; ++c) {
+        float p[4];
+        vload<4>(p, a.partials + int64_t(s.y + c) * kFin + lane * 4);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[k] = R::combine(acc[k], p[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[k] = R::finish(acc[k], s.w);
+      if (a.pre_gin) {
+        float xv[4];
+        vload<4>(xv, a.x + int64_t(row) * a.ld_x + lane * 4);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[k] = __fadd_rn(__fmul_rn(a.gin_scale, xv[k]), acc[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) vrow[g][lane * 4 + k] = acc[k];
+    }
+    __syncthreads();
+    if (row >= 0) {
+      for (int c = lane; c < a.F_out; c += 32) {
+        float s = 0.0f;
+        for (int k = 0; k < kFin; ++k) s = fmaf(vrow[g][k], a.W[int64_t(k) * a.F_out + c], s);
+        a.out[int64_t(row) * a.ld_o + c] = s + (a.bias ? a.bias[c] : 0.0f);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int RED, bool W>
+int launch(const FusedArgs& a, hipStream_t s) {
+  const int64_t work = a.items ? a.n_items : a.n_rows;
+  if (work > 0) {
+    static int cus = 0;
+    if (cus == 0) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
+    }
+    int per_cu = 0;
+    auto k = spmm_gemm_kernel<RED, W>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, 0) != hipSuccess || per_cu <= 0)
+      per_cu = 2;
+    const int64_t need = (work + kGroups - 1) / kGroups;
+    const int64_t cap = int64_t(per_cu) * cus;
+    hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kThreads), 0, s, a);
+    KGX_CHECK_LAUNCH();
+  }
+  if (a.items && a.n_split > 0) {
+    const int64_t blocks = (a.n_split + 7) / 8;
+    hipLaunchKernelGGL(spmm_gemm_fixup_kernel<RED>, dim3(unsigned(blocks < 4096 ? blocks : 4096)), dim3(256), 0,
+                       s, a);
+    KGX_CHECK_LAUNCH();
+  }
+  return KGX_OK;
+}
+
+}  // namespace
+}  // namespace kgx
+
+using namespace kgx;
+
+extern "C" int kgx_spmm_gemm(int reduce, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
+                             const int32_t* items, int64_t n_items, const int32_t* split, int64_t n_split,
+                             const int32_t* idx, const float* w, const float* x, int64_t ld_x, int64_t F_in,
+                             const float* W, int64_t F_out, const float* bias, int pre_gin, float gin_scale,
+                             float* out, int64_t ld_out, float* partials, kgx_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  KGX_REQUIRE(reduce >= KGX_SUM && reduce <= KGX_MIN, KGX_ERR_ARG, "kgx_spmm_gemm: reduce %d unsupported", reduce);
+  KGX_REQUIRE(F_in == kFin, KGX_ERR_UNSUPPORTED, "kgx_spmm_gemm: F_in must be %d (got %lld)", kFin,
+              (long long)F_in);
+  KGX_REQUIRE(F_out > 0 && F_out <= 128 && F_out % 16 == 0, KGX_ERR_UNSUPPORTED,
+              "kgx_spmm_gemm: F_out must be a multiple of 16 <= 128 (got %lld)", (long long)F_out);
+  KGX_REQUIRE(n_rows >= 0 && n_items >= 0 && n_split >= 0, KGX_ERR_ARG, "kgx_spmm_gemm: negative size");
+  if (n_rows == 0) return KGX_OK;
+  KGX_REQUIRE(rowptr && rows && idx && x && W && out, KGX_ERR_ARG, "kgx_spmm_gemm: null pointer");
+  KGX_REQUIRE(ld_x % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0 && ld_out >= F_out, KGX_ERR_ARG,
+              "kgx_spmm_gemm: x must be 16-byte aligned with ld %% 4 == 0");
+  KGX_REQUIRE(!items || n_split == 0 || (split && partials), KGX_ERR_ARG,
+              "kgx_spmm_gemm: split rows need split list and partials");
+  FusedArgs a{};
+  a.rowptr = rowptr;
+  a.rows = rows;
+  a.n_rows = n_rows;
+  a.items = reinterpret_cast<const int4*>(items);
+  a.n_items = items ? n_items : 0;
+  a.split = reinterpret_cast<const int4*>(split);
+  a.n_split = items ? n_split : 0;
+  a.idx = idx;
+  a.w = w;
+  a.x = x;
+  a.ld_x = ld_x;
+  a.W = W;
+  a.F_out = int(F_out);
+  a.bias = bias;
+  a.out = out;
+  a.ld_o = ld_out;
+  a.partials = partials;
+  a.pre_gin = pre_gin;
+  a.gin_scale = gin_scale;
+  const bool wt = w != nullptr;
+  switch (reduce) {
+    case KGX_SUM: return wt ? launch<KGX_SUM, true>(a, stream) : launch<KGX_SUM, false>(a, stream);
+    case KGX_MEAN: return wt ? launch<KGX_MEAN, true>(a, stream) : launch<KGX_MEAN, false>(a, stream);
+    case KGX_MAX: return wt ? launch<KGX_MAX, true>(a, stream) : launch<KGX_MAX, false>(a, stream);
+    default: return wt ? launch<KGX_MIN, true>(a, stream) : launch<KGX_MIN, false>(a, stream);
+  }
+}

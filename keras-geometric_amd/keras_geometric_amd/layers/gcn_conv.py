@@ -109,8 +109,12 @@ class GCNConv(MessagePassing):
             return out + self.bias if (self.use_bias and self.bias is not None) else out
         g = graph_for(edge_index, ei, N, N, self_loops=self.add_self_loops, gcn_norm=self.normalize,
                       n_features=self.output_dim)
-        h = torch.matmul(x, self.kernel)  # node-level X W (MFMA GEMM)
         use_b = self.use_bias and self.bias is not None
+        if not self.exact and kops.fused_transform_supported(x.shape[1], self.output_dim):
+            # aggregate-then-transform in one launch (W on f32 MFMA in the epilogue)
+            return kops.aggregate_transform(g, x.contiguous(), self.kernel, "sum", weighted=self.normalize,
+                                            bias=self.bias if use_b else None)
+        h = torch.matmul(x, self.kernel)  # node-level X W (MFMA GEMM)
         return kops.aggregate(
             g, h, "sum", weighted=self.normalize,
             epilogue=nat.EPI_BIAS if use_b else nat.EPI_NONE, bias=self.bias if use_b else None,

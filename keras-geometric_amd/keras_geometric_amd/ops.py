@@ -75,6 +75,60 @@ def _spmm_fake(table, rowptr, rows, items, split, idx, w, n_slots, reduce, epilo
     return table.new_empty((rowptr.shape[0] - 1, table.shape[1]))
 
 
+@torch.library.custom_op("kgx::spmm_gemm", mutates_args=())
+def spmm_gemm(
+    x: torch.Tensor,
+    rowptr: torch.Tensor,
+    rows: torch.Tensor,
+    items: Optional[torch.Tensor],
+    split: Optional[torch.Tensor],
+    idx: torch.Tensor,
+    w: Optional[torch.Tensor],
+    n_slots: int,
+    reduce: int,
+    W: torch.Tensor,
+    bias: Optional[torch.Tensor],
+    pre_gin: bool,
+    gin_scale: float,
+) -> torch.Tensor:
+    x, w, W, bias = _f32c(x), _f32c(w), _f32c(W), _f32c(bias)
+    dev = nat.require_device(x, rowptr, rows, idx, w, W, bias, items, split)
+    n_dst = rowptr.numel() - 1
+    F_out = W.shape[1]
+    out = torch.empty((n_dst, F_out), dtype=torch.float32, device=dev)
+    if n_dst == 0:
+        return out
+    n_items = 0 if items is None else items.shape[0]
+    n_split = 0 if split is None else split.shape[0]
+    partials = None
+    if items is not None and n_split > 0:
+        partials = torch.empty((n_slots, x.shape[1]), dtype=torch.float32, device=dev)
+    nat.check(
+        nat.lib().kgx_spmm_gemm(
+            reduce, nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, nat.ptr(split), n_split,
+            nat.ptr(idx), nat.ptr(w), nat.ptr(x), x.stride(0), x.shape[1], nat.ptr(W), F_out, nat.ptr(bias),
+            int(pre_gin), float(gin_scale), nat.ptr(out), out.stride(0), nat.ptr(partials), nat.stream(dev),
+        ),
+        "kgx_spmm_gemm",
+    )
+    return out
+
+
+@spmm_gemm.register_fake
+def _spmm_gemm_fake(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale):
+    return x.new_empty((rowptr.shape[0] - 1, W.shape[1]))
+
+
+def fused_transform_supported(f_in: int, f_out: int) -> bool:
+    """Shapes kgx_spmm_gemm implements (aggregate-then-transform is also only
+    worth it when F_in <= F_out)."""
+    import os
+
+    if os.environ.get("KGX_FUSED", "1") in ("0", "false", "False"):
+        return False
+    return f_in == 128 and f_out % 16 == 0 and 0 < f_out <= 128 and f_in <= f_out
+
+
 @torch.library.custom_op("kgx::gatv2", mutates_args=())
 def gatv2(
     h_src: torch.Tensor,
@@ -207,6 +261,29 @@ def aggregate(
         raise ValueError("graph was built without GCN normalisation weights")
     return _timed(lambda: torch.ops.kgx.spmm(
         table, g.rowptr, g.rows, items, split, idx, w, n_slots, red, epilogue, bias, xroot, float(gin_scale)
+    ))
+
+
+def aggregate_transform(
+    g: CSRGraph,
+    x: torch.Tensor,
+    W: torch.Tensor,
+    reduce: str | int = "sum",
+    *,
+    weighted: bool = False,
+    bias: torch.Tensor | None = None,
+    pre_gin: bool = False,
+    gin_scale: float = 1.0,
+    exact: bool = False,
+) -> torch.Tensor:
+    """out = bias + PRE(REDUCE_{e in row} x[col_e] * w_e) @ W in one fused launch."""
+    red = nat.REDUCE_IDS[reduce] if isinstance(reduce, str) else int(reduce)
+    items, _, split, _, n_slots = g.work(exact)
+    w = g.w if weighted else None
+    if weighted and w is None:
+        raise ValueError("graph was built without GCN normalisation weights")
+    return _timed(lambda: torch.ops.kgx.spmm_gemm(
+        x, g.rowptr, g.rows, items, split, g.col, w, n_slots, red, W, bias, bool(pre_gin), float(gin_scale)
     ))
 
 

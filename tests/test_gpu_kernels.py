@@ -293,3 +293,42 @@ def test_gather_and_scatter_rows(dev):
     ref = torch.zeros(64)
     ref[perm.cpu().long()] = v.cpu()
     exact(out, ref)
+
+
+def assert_dot_bound(got, a64, W64, b64, k_eps=4e-6):
+    """|got - a@W - b| <= k_eps * (|a|@|W| + |b|) + 1e-6: the forward-error bound of
+    an fp32 K=128 dot product, independent of cancellation in the output."""
+    ref = a64 @ W64 + b64
+    bound = k_eps * (np.abs(a64) @ np.abs(W64) + np.abs(b64)) + 1e-6
+    err = np.abs(got.astype(np.float64) - ref)
+    assert (err <= bound).all(), f"max err/bound {(err / bound).max():.2f}"
+
+
+@pytest.mark.parametrize("F_out", [128, 64, 16])
+@pytest.mark.parametrize("split_len", [0, 16])
+def test_fused_aggregate_transform(dev, F_out, split_len):
+    """kgx_spmm_gemm: REDUCE(x_j * w) @ W + b (f32 MFMA epilogue) vs the oracle's
+    reduction followed by a float64 matmul (dot-product error bound); the GCN
+    layer vs the reference order at the north-star tolerance."""
+    N, E, F = 3000, 40000, 128
+    s, d = rmat_edges(8, scale_for(N), N, 0, E)
+    rng = np.random.default_rng(F_out)
+    x = rng.standard_normal((N, F)).astype(np.float32)
+    W = (rng.standard_normal((F, F_out)) * 0.1).astype(np.float32)
+    b = rng.standard_normal(F_out).astype(np.float32)
+    ei_l = R.add_self_loops(T(np.stack([s, d])), N)
+    csr = build(np.stack([s, d]), N, dev, self_loops=True, gcn_norm=True, split_len=split_len)
+    xd, Wd, bd = T(x).to(dev), T(W).to(dev), T(b).to(dev)
+    W64, b64 = W.astype(np.float64), b.astype(np.float64)
+    for red in ("sum", "mean", "max", "min"):
+        aggr = R.aggregate(red, T(x)[ei_l[0].long()], ei_l[1], N).numpy().astype(np.float64)
+        got = kops.aggregate_transform(csr, xd, Wd, red, bias=bd, exact=split_len == 0).cpu().numpy()
+        if split_len == 0 or red in ("max", "min"):
+            assert_dot_bound(got, aggr, W64, b64)
+        else:  # split hub rows also re-associate the sum
+            assert_dot_bound(got, aggr, W64, b64, k_eps=2e-5)
+    y = kops.aggregate_transform(csr, xd, Wd, "sum", weighted=True, bias=bd, exact=split_len == 0).cpu().numpy()
+    assert_tol(y, R.gcn_forward(T(x), T(np.stack([s, d])), T(W), T(b)).numpy())
+    g = kops.aggregate_transform(csr, xd, Wd, "max", bias=None, pre_gin=True, gin_scale=1.5).cpu().numpy()
+    h = (1.5 * T(x) + R.aggregate("max", T(x)[ei_l[0].long()], ei_l[1], N)).numpy().astype(np.float64)
+    assert_dot_bound(g, h, W64, np.zeros_like(b64))

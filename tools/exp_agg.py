@@ -1,0 +1,99 @@
+"""Aggregation-kernel experiments on the GPU (timing sweeps + PMC calibration).
+
+  python tools/exp_agg.py sweep        # NS graph: exact vs split lengths, event timing
+  python tools/exp_agg.py calib        # permutation graph with a known byte count (run under rocprofv3 --pmc)
+
+Not part of the product; a measurement helper whose results feed DESIGN.md.
+"""
+
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "keras-geometric_amd")]
+
+import torch  # noqa: E402
+
+from keras_geometric_amd import graph as G  # noqa: E402
+from keras_geometric_amd import ops as kops  # noqa: E402
+from keras_geometric_amd import synthetic  # noqa: E402
+
+
+def timeit(fn, reps=10):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def b_alg(n, e, f, weighted=True):
+    return 4 * (n + 1) + e * (4 + (4 if weighted else 0) + 4 * f) + 4 * n * f
+
+
+def sweep(n=10_000_000, e=100_000_000, f=128):
+    dev = torch.device("cuda", 0)
+    ei = synthetic.rmat_edge_index(n, e, seed=0, device=dev)
+    h = torch.randn(n, f, device=dev)
+    out = {}
+    for T in [0, 256, 512, 1024, 2048, 4096, 8192]:
+        g = G.build_csr(ei[0].contiguous(), ei[1].contiguous(), n, n, self_loops=True, gcn_norm=True,
+                        split_len=T if T else 0)
+        ms = timeit(lambda: kops.aggregate(g, h, "sum", weighted=True, exact=(T == 0)))
+        out[f"split{T}"] = {"ms": ms, "TBps_alg": b_alg(n, g.kept, f) / ms / 1e9, "n_items": g.n_items,
+                            "n_split": g.n_split}
+        print(T, out[f"split{T}"], flush=True)
+        del g
+        torch.cuda.empty_cache()
+    for red in ["sum", "mean", "max"]:
+        g = G.build_csr(ei[0].contiguous(), ei[1].contiguous(), n, n, self_loops=False)
+        ms = timeit(lambda: kops.aggregate(g, h, red))
+        out[f"unweighted_{red}_noloops"] = {"ms": ms, "TBps_alg": b_alg(n, g.kept, f, False) / ms / 1e9}
+        print(red, out[f"unweighted_{red}_noloops"], flush=True)
+        del g
+    # GEMM for reference
+    W = torch.randn(f, f, device=dev)
+    out["gemm_ms"] = timeit(lambda: h @ W)
+    print(json.dumps(out))
+
+
+def calib(n=10_000_000, f=128):
+    """Each row has exactly one in-edge from a distinct random source: the table is
+    read exactly once -> known bytes.  Run under rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE."""
+    dev = torch.device("cuda", 0)
+    gen = torch.Generator(device=dev).manual_seed(0)
+    src = torch.randperm(n, device=dev, generator=gen).to(torch.int32)
+    dst = torch.arange(n, device=dev, dtype=torch.int32)
+    h = torch.randn(n, f, device=dev)
+    for name, s in (("perm", src), ("ident", dst.clone())):
+        g = G.build_csr(s, dst, n, n, split_len=0)
+        torch.cuda.synchronize()
+        for _ in range(3):
+            kops.aggregate(g, h, "sum", exact=True)
+        torch.cuda.synchronize()
+        known = n * f * 4 + n * 4 + n * 4 + (n + 1) * 4  # table + col + rows + rowptr
+        print(json.dumps({"case": name, "known_read_bytes": known, "write_bytes": n * f * 4}), flush=True)
+        time.sleep(0.1)
+
+
+def ns_once(n=10_000_000, e=100_000_000, f=128, split=512):
+    """One NS weighted aggregation timing (env knobs such as KGX_SPMM_HINTS apply)."""
+    import os
+
+    dev = torch.device("cuda", 0)
+    ei = synthetic.rmat_edge_index(n, e, seed=0, device=dev)
+    h = torch.randn(n, f, device=dev)
+    g = G.build_csr(ei[0].contiguous(), ei[1].contiguous(), n, n, self_loops=True, gcn_norm=True, split_len=split)
+    ms = timeit(lambda: kops.aggregate(g, h, "sum", weighted=True), reps=20)
+    print(json.dumps({"hints": os.environ.get("KGX_SPMM_HINTS", "0"), "split": split, "ms": ms,
+                      "TBps_alg": b_alg(n, g.kept, f) / ms / 1e9}), flush=True)
+
+
+if __name__ == "__main__":
+    {"sweep": sweep, "calib": calib, "ns": ns_once}[sys.argv[1]]()
