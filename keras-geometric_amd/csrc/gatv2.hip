@@ -14,7 +14,9 @@
 //
 // Numerics: algebraically identical to the reference; the score reduction order
 // over C, exp, and the division placement differ at the ulp level, so GATv2 is
-// tolerance-checked (|a-b| <= 1e-5*max(1,|b|)), not bit-checked.
+// tolerance-checked (|a-b| <= 1e-5*max(1,|b|)), not bit-checked.  The softmax
+// numerator and denominator are accumulated in fp64 (exact to ~1e-7 even on
+// 10^5-edge hub rows; the fp64 FMAs are free in this HBM-bound kernel).
 #include "kgx_internal.h"
 #include "kgx_vec.h"
 
@@ -81,15 +83,18 @@ __global__ __launch_bounds__(kBlock) void gatv2_kernel(GatArgs a) {
       end = a.rowptr[row + 1];
       slot = -1;
     }
-    float hd[K], acc[K];
+    // softmax numerator / denominator accumulated in fp64: a hub row sums
+    // 10^5 terms, whose fp32 rounding (~sqrt(n) ulp) would exceed 1e-5.
+    float hd[K];
+    double acc[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       hd[k] = 0.0f;
-      acc[k] = 0.0f;
+      acc[k] = 0.0;
     }
     if (valid) vload<K>(hd, a.h_dst + int64_t(row) * a.ld_h + f);
     float m = -__builtin_inff();
-    float l = 0.0f;
+    double l = 0.0;
 
     for (int32_t e = beg; e < end; e += U) {
       const int n = (end - e) < U ? (end - e) : U;
@@ -122,17 +127,17 @@ __global__ __launch_bounds__(kBlock) void gatv2_kernel(GatArgs a) {
         if (u < n) mc = fmaxf(mc, p);
       }
       const float m_new = fmaxf(m, mc);
-      const float scale = expf(m - m_new);
+      const double scale = double(expf(m - m_new));
       l *= scale;
 #pragma unroll
       for (int k = 0; k < K; ++k) acc[k] *= scale;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (u < n) {
-          const float pu = expf(s[u] - m_new);
+          const double pu = double(expf(s[u] - m_new));
           l += pu;
 #pragma unroll
-          for (int k = 0; k < K; ++k) acc[k] += pu * hs[u][k];
+          for (int k = 0; k < K; ++k) acc[k] = fma(pu, double(hs[u][k]), acc[k]);
         }
       }
       m = m_new;
@@ -141,16 +146,19 @@ __global__ __launch_bounds__(kBlock) void gatv2_kernel(GatArgs a) {
     if (!valid) continue;
     if (slot >= 0) {
       float* p = a.partials + int64_t(slot) * (HC + 2 * a.H);
-      vstore<K>(p + f, acc);
+      float accf[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) accf[k] = float(acc[k]);
+      vstore<K>(p + f, accf);
       if (sub == 0) {
         p[HC + head] = m;
-        p[HC + a.H + head] = l;
+        p[HC + a.H + head] = float(l);
       }
     } else {
-      const float den = l + 1e-10f;
+      const double den = l + 1e-10;
       float r[K];
 #pragma unroll
-      for (int k = 0; k < K; ++k) r[k] = acc[k] / den;
+      for (int k = 0; k < K; ++k) r[k] = float(acc[k] / den);
       if (a.bias) {
         float b[K];
         vload<K>(b, a.bias + f);
@@ -179,22 +187,22 @@ __global__ __launch_bounds__(kBlock) void gatv2_fixup_kernel(GatArgs a) {
     float M = -__builtin_inff();
     for (int32_t c = 0; c < nc; ++c)
       M = fmaxf(M, a.partials[int64_t(slot0 + c) * (HC + 2 * a.H) + HC + head]);
-    float L = 0.0f, acc[K];
+    double L = 0.0, acc[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) acc[k] = 0.0f;
+    for (int k = 0; k < K; ++k) acc[k] = 0.0;
     for (int32_t c = 0; c < nc; ++c) {
       const float* p = a.partials + int64_t(slot0 + c) * (HC + 2 * a.H);
-      const float sc = expf(p[HC + head] - M);
-      L += p[HC + a.H + head] * sc;
+      const double sc = double(expf(p[HC + head] - M));
+      L += double(p[HC + a.H + head]) * sc;
       float v[K];
       vload<K>(v, p + f);
 #pragma unroll
-      for (int k = 0; k < K; ++k) acc[k] += v[k] * sc;
+      for (int k = 0; k < K; ++k) acc[k] += double(v[k]) * sc;
     }
-    const float den = L + 1e-10f;
+    const double den = L + 1e-10;
     float r[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) r[k] = acc[k] / den;
+    for (int k = 0; k < K; ++k) r[k] = float(acc[k] / den);
     if (a.bias) {
       float b[K];
       vload<K>(b, a.bias + f);

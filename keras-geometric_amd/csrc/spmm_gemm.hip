@@ -19,6 +19,8 @@
 // contiguous floats of its tile row (8 ds_read_b128): k-step s uses
 // k = 32*(lane>>4) + s.  Hub-row chunks write raw partials; the fix-up kernel
 // combines them and applies W with VALU.
+#include <cstdlib>
+
 #include "kgx_internal.h"
 #include "kgx_vec.h"
 
@@ -52,6 +54,7 @@ struct FusedArgs {
   float* partials;  // [n_slots, 128]
   int pre_gin;      // apply gin_scale * x[row] + aggr before the transform
   float gin_scale;
+  int debug;        // experiment knob (KGX_FUSED_DEBUG): 1 = skip the MFMA phase
 };
 
 template <int RED>
@@ -84,6 +87,7 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
   using R = Red<RED>;
   constexpr int U = 8;
   __shared__ float tile[kGroups][kTileLd];
+  __shared__ float otile[kGroups][kTileLd];  // MFMA results, re-read as whole rows
   __shared__ int32_t tile_row[kGroups];
 
   const int tid = threadIdx.x;
@@ -103,9 +107,18 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
   const float bcol = (mfma_wave && a.bias) ? a.bias[n_col] : 0.0f;
 
   const int64_t n_work = a.items ? a.n_items : a.n_rows;
-  for (int64_t base = int64_t(blockIdx.x) * kGroups; base < n_work; base += int64_t(gridDim.x) * kGroups) {
-    const int64_t it = base + g;
-    int32_t row = -1, beg = 0, end = 0, slot = -1;
+  const int64_t stride = int64_t(gridDim.x) * kGroups;
+
+  // software pipeline: the next item's descriptor and its first U neighbour rows
+  // are loaded before the MFMA phase of the current tile, so the gathers are in
+  // flight while the matrix pipe works.
+  int32_t row = -1, beg = 0, end = 0, slot = -1;
+  int pn = 0;
+  float pv[U][4], pw[U];
+  auto fetch = [&](int64_t it) {
+    row = -1;
+    beg = end = 0;
+    slot = -1;
     if (it < n_work) {
       if (a.items) {
         const int4 v = a.items[it];
@@ -119,10 +132,41 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
         end = a.rowptr[row + 1];
       }
     }
+    pn = (end - beg) < U ? (end - beg) : U;
+    int32_t c[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int32_t ee = u < pn ? beg + u : beg;
+      c[u] = u < pn ? a.idx[ee] : 0;
+      if constexpr (WEIGHTED) pw[u] = u < pn ? a.w[ee] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u < pn) {
+        vload<4>(pv[u], a.x + int64_t(c[u]) * a.ld_x + f);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) pv[u][k] = 0.0f;
+      }
+    }
+  };
+
+  fetch(int64_t(blockIdx.x) * kGroups + g);
+  for (int64_t base = int64_t(blockIdx.x) * kGroups; base < n_work; base += stride) {
     float acc[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) acc[k] = R::init();
-    int32_t e = beg;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u < pn) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float m = WEIGHTED ? __fmul_rn(pv[u][k], pw[u]) : pv[u][k];
+          acc[k] = R::combine(acc[k], R::msg(m));
+        }
+      }
+    }
+    int32_t e = beg + U;
     for (; e + U <= end; e += U) {
       int32_t c[U];
       float wt[U];
@@ -174,9 +218,7 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
       }
     }
     const bool full_row = row >= 0 && slot < 0;
-    if (row >= 0 && slot >= 0) {
-      vstore<4>(a.partials + int64_t(slot) * kFin + f, acc);
-    }
+    if (row >= 0 && slot >= 0) vstore<4>(a.partials + int64_t(slot) * kFin + f, acc);
     float r[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) r[k] = full_row ? R::finish(acc[k], end - beg) : 0.0f;
@@ -190,27 +232,30 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
     if (lane == 0) tile_row[g] = full_row ? row : -1;
     __syncthreads();
 
-    if (mfma_wave) {
+    fetch(base + stride + g);  // next tile's first gathers fly during the MFMAs
+
+    if (mfma_wave && !(a.debug & 1)) {
       const int m = wl & 15;
-      float af[32];
+      f32x4 d0 = {0.0f, 0.0f, 0.0f, 0.0f};
+      f32x4 d1 = {0.0f, 0.0f, 0.0f, 0.0f};  // two chains: the f32 MFMA's dependent latency is 40 > 32 cycles
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float4 t4 = *reinterpret_cast<const float4*>(&tile[m][32 * q + 4 * i]);
-        af[4 * i + 0] = t4.x;
-        af[4 * i + 1] = t4.y;
-        af[4 * i + 2] = t4.z;
-        af[4 * i + 3] = t4.w;
+      for (int s0 = 0; s0 < 32; s0 += 4) {
+        const float4 t4 = *reinterpret_cast<const float4*>(&tile[m][32 * q + s0]);
+        d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(t4.x, wb[s0 + 0], d0, 0, 0, 0);
+        d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(t4.y, wb[s0 + 1], d1, 0, 0, 0);
+        d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(t4.z, wb[s0 + 2], d0, 0, 0, 0);
+        d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(t4.w, wb[s0 + 3], d1, 0, 0, 0);
       }
-      f32x4 d = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-      for (int s = 0; s < 32; ++s) d = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], wb[s], d, 0, 0, 0);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int rr = tile_row[4 * q + j];
-        if (rr >= 0) a.out[int64_t(rr) * a.ld_o + n_col] = d[j] + bcol;
-      }
+      for (int j = 0; j < 4; ++j) otile[4 * q + j][n_col] = (d0[j] + d1[j]) + bcol;
     }
     __syncthreads();
+    // whole-row dwordx4 stores: group g writes its tile row (F_out/4 lanes)
+    if (!(a.debug & 2)) {
+      const int rr = tile_row[g];
+      if (rr >= 0 && f < a.F_out)
+        *reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + f) = *reinterpret_cast<const float4*>(&otile[g][f]);
+    }
   }
 }
 
@@ -330,6 +375,11 @@ extern "C" int kgx_spmm_gemm(int reduce, const int32_t* rowptr, const int32_t* r
   a.partials = partials;
   a.pre_gin = pre_gin;
   a.gin_scale = gin_scale;
+  static const int dbg = [] {
+    const char* h = getenv("KGX_FUSED_DEBUG");
+    return h ? atoi(h) : 0;
+  }();
+  a.debug = dbg;
   const bool wt = w != nullptr;
   switch (reduce) {
     case KGX_SUM: return wt ? launch<KGX_SUM, true>(a, stream) : launch<KGX_SUM, false>(a, stream);

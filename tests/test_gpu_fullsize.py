@@ -1,0 +1,118 @@
+"""Full-size parity (north-star graph: R-MAT 10M nodes / 100M edges + self
+loops) through size-independent properties — the CPU oracle cannot run the
+whole graph in test time, so:
+
+* CSR integer invariants, checked bit-exactly over ALL 110M slots: degrees ==
+  bincount(dst)+1, eid a permutation, input order kept inside every row, the
+  self loop last in every row;
+* EXACT aggregation of sampled rows (including the ten highest-degree hub rows)
+  == a sequential float32 accumulation on the host, bit for bit;
+* split-hub (default) vs EXACT over all rows within the north-star tolerance,
+  unsplit rows bit-identical;
+* linearity checksum: column sums of the weighted aggregation == sum over edges
+  of w_e * x[src_e] (float64), and the fused aggregate->transform GCN layer ==
+  the GEMM-then-aggregate layer within tolerance;
+* GATv2 (C3-sized, 1M / 10M): with identical h rows every softmax-weighted
+  average equals that row.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from keras_geometric_amd import graph as G
+from keras_geometric_amd import ops as kops
+from keras_geometric_amd import synthetic
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow, pytest.mark.timeout(600)]
+
+N, E, F = 10_000_000, 100_000_000, 128
+
+
+@pytest.fixture(scope="module")
+def big(dev):
+    ei = synthetic.rmat_edge_index(N, E, seed=0, device=dev)
+    g = G.build_csr(ei[0].contiguous(), ei[1].contiguous(), N, N, self_loops=True, gcn_norm=True)
+    x = torch.randn(N, F, device=dev, generator=torch.Generator(device=dev).manual_seed(1))
+    yield ei, g, x
+    G.clear_cache()
+
+
+def test_csr_invariants_fullsize(big):
+    ei, g, _ = big
+    rowptr, col, eid, deg = g.rowptr.long(), g.col.long(), g.eid.long(), g.deg.long()
+    assert g.kept == E + N and int(rowptr[0]) == 0 and int(rowptr[-1]) == E + N
+    assert bool((rowptr[1:] >= rowptr[:-1]).all())
+    torch.testing.assert_close(deg, torch.bincount(ei[1].long(), minlength=N) + 1, rtol=0, atol=0)
+    assert bool((torch.bincount(eid, minlength=E + N) == 1).all())  # permutation
+    row_of = torch.repeat_interleave(torch.arange(N, device=deg.device), deg)
+    same_row = row_of[1:] == row_of[:-1]
+    assert bool((eid[1:] > eid[:-1])[same_row].all())  # input order kept within each row
+    last = rowptr[1:] - 1
+    torch.testing.assert_close(eid[last], E + torch.arange(N, device=deg.device), rtol=0, atol=0)
+    src = torch.cat([ei[0].long(), torch.arange(N, device=deg.device)])
+    torch.testing.assert_close(col, src[eid], rtol=0, atol=0)
+    assert g.max_degree == int(deg.max())
+
+
+def test_exact_sampled_rows_bitwise(big):
+    _, g, x = big
+    out = kops.aggregate(g, x, "sum", weighted=True, exact=True)
+    deg = g.deg.long()
+    hubs = torch.topk(deg, 10).indices
+    rng = np.random.default_rng(0)
+    rows = torch.cat([hubs, torch.from_numpy(rng.integers(0, N, 200)).to(deg.device)]).tolist()
+    rowptr = g.rowptr.cpu().numpy()
+    for r in rows:
+        b, e = int(rowptr[r]), int(rowptr[r + 1])
+        c = g.col[b:e].long()
+        msg = (x[c] * g.w[b:e].unsqueeze(1)).cpu().numpy()  # fp32 products, as the reference
+        acc = np.zeros(F, np.float32)
+        for k in range(msg.shape[0]):  # sequential RN accumulation in edge order
+            acc = acc + msg[k]
+        np.testing.assert_array_equal(out[r].cpu().numpy(), acc)
+
+
+def test_split_vs_exact_fullsize(big):
+    _, g, x = big
+    ex = kops.aggregate(g, x, "sum", weighted=True, exact=True)
+    sp = kops.aggregate(g, x, "sum", weighted=True)
+    err = ((sp - ex).abs() / ex.abs().clamp_min(1.0)).max().item()
+    assert err <= 1e-5
+    unsplit = g.deg < g.split_len
+    assert bool((sp[unsplit] == ex[unsplit]).all())
+    for red in ("max", "min"):
+        assert bool((kops.aggregate(g, x, red) == kops.aggregate(g, x, red, exact=True)).all())
+
+
+def test_linearity_checksum_and_fused_layer(big):
+    _, g, x = big
+    out = kops.aggregate(g, x, "sum", weighted=True)
+    colsum = out.double().sum(0)
+    ref = torch.zeros(F, dtype=torch.float64, device=x.device)
+    for s in range(0, g.kept, 20_000_000):
+        c = g.col[s:s + 20_000_000].long()
+        ref += (x[c].double() * g.w[s:s + 20_000_000].double().unsqueeze(1)).sum(0)
+    torch.testing.assert_close(colsum, ref, rtol=1e-6, atol=1e-3)
+    W = torch.randn(F, F, device=x.device) * (1.0 / F) ** 0.5
+    b = torch.randn(F, device=x.device)
+    fused = kops.aggregate_transform(g, x, W, "sum", weighted=True, bias=b)
+    unfused = kops.aggregate(g, (x @ W).contiguous(), "sum", weighted=True, epilogue=1, bias=b)
+    err = ((fused - unfused).abs() / unfused.abs().clamp_min(1.0)).max().item()
+    assert err <= 1e-5
+
+
+def test_gatv2_softmax_convexity_c3(dev):
+    n, e, H, C = 1_000_000, 10_000_000, 8, 16
+    ei = synthetic.rmat_edge_index(n, e, seed=2, device=dev)
+    g = G.build_csr(ei[0].contiguous(), ei[1].contiguous(), n, n, self_loops=True)
+    row = torch.randn(H * C, device=dev)
+    h = row.expand(n, H * C).contiguous()
+    att = torch.randn(H * C, device=dev)
+    out = kops.gatv2_aggregate(g, h, h, att, H, C, 0.2)
+    err = ((out - row).abs() / row.abs().clamp_min(1.0)).max().item()
+    assert err <= 1e-5
+    hr = torch.randn(n, H * C, device=dev)
+    a = kops.gatv2_aggregate(g, hr, hr, att, H, C, 0.2)
+    b = kops.gatv2_aggregate(g, hr, hr, att, H, C, 0.2, exact=True)
+    assert ((a - b).abs() / b.abs().clamp_min(1.0)).max().item() <= 1e-5
