@@ -8,13 +8,21 @@
 
 namespace kgx {
 
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
 // Load/store VEC consecutive floats (VEC in {1,2,4,8,16}; >=4 uses float4 pieces).
 template <int VEC>
 __device__ __forceinline__ void vload(float (&d)[VEC], const float* __restrict__ p) {
   if constexpr (VEC >= 4) {
 #pragma unroll
     for (int i = 0; i < VEC / 4; ++i) {
+#ifdef KGX_ROW_NT  // experiment: gathered rows with the non-temporal policy
+      const f32x4_t w4 = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(p) + i);
+      const float4 v = make_float4(w4[0], w4[1], w4[2], w4[3]);
+#else
       const float4 v = reinterpret_cast<const float4*>(p)[i];
+#endif
       d[4 * i + 0] = v.x;
       d[4 * i + 1] = v.y;
       d[4 * i + 2] = v.z;
@@ -44,8 +52,6 @@ __device__ __forceinline__ void vstore(float* __restrict__ p, const float (&d)[V
 
 // Non-temporal variants (global_load/store ... nt): for data streamed once
 // (CSR indices / weights, output rows) so it does not displace reused rows.
-typedef float f32x4_t __attribute__((ext_vector_type(4)));
-typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
 template <int VEC>
 __device__ __forceinline__ void vstore_nt(float* __restrict__ p, const float (&d)[VEC]) {

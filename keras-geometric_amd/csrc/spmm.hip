@@ -57,6 +57,9 @@ struct SpmmArgs {
 
 template <int RED>
 struct Reducer {
+  // init() is also the identity of combine(): +0 for sums (the accumulator
+  // starts at +0 and an RN sum never produces -0 from it, so acc + 0 == acc
+  // bit for bit, NaN and inf included) and -inf for the amax form.
   static __device__ __forceinline__ float init() {
     if constexpr (RED == KGX_MAX || RED == KGX_MIN) return -__builtin_inff();
     return 0.0f;
@@ -96,6 +99,45 @@ __device__ __forceinline__ void epilogue(const SpmmArgs& a, int32_t row, int f, 
   }
 }
 
+// U consecutive edges [e, e+U) of a row ending at `end`: U index (and weight)
+// loads, then U row gathers, all unconditional (indices past `end` are clamped
+// to end-1, whose row is already being fetched), then an in-order fold where
+// clamped edges contribute the reduction's identity.  No load sits under a
+// lane-dependent branch, so hipcc keeps all U gathers in flight.
+template <int U, int VEC, int NT, int RED, bool WEIGHTED>
+__device__ __forceinline__ void edge_block(const SpmmArgs& a, int32_t e, int32_t end, const int (&fl)[NT],
+                                           float (&acc)[NT][VEC]) {
+  using R = Reducer<RED>;
+  const int n = end - e;
+  int32_t c[U];
+  float wt[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int32_t ee = u < n ? e + u : end - 1;
+    if (a.hints & 1) {
+      c[u] = ld_nt(a.idx + ee);
+      if constexpr (WEIGHTED) wt[u] = ld_nt(a.w + ee);
+    } else {
+      c[u] = a.idx[ee];
+      if constexpr (WEIGHTED) wt[u] = a.w[ee];
+    }
+  }
+  float v[U][NT][VEC];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) vload<VEC>(v[u][t], a.table + int64_t(c[u]) * a.ld_t + fl[t]);
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) {
+        const float m = WEIGHTED ? __fmul_rn(v[u][t][k], wt[u]) : v[u][t][k];
+        acc[t][k] = R::combine(acc[t][k], u < n ? R::msg(m) : R::init());
+      }
+}
+
 template <int VEC, int NT, int RED, bool WEIGHTED>
 __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
   using R = Reducer<RED>;
@@ -105,12 +147,17 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
   const int64_t ngroups = (int64_t(gridDim.x) * kBlock) >> a.lgG;
   const int64_t n_work = a.items ? a.n_items : a.n_rows;
 
-  int fo[NT];
+  // Every global load below is unconditional (clamped to a valid address) and
+  // masked work is folded in as the reduction's identity: a load under a
+  // lane-dependent branch makes hipcc wait for it at the branch join, which
+  // would serialise the U gathers that are meant to be in flight together.
+  int fo[NT], fl[NT];
   bool fv[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     fo[t] = (t * G + lane) * VEC;
     fv[t] = fo[t] < a.F;
+    fl[t] = fv[t] ? fo[t] : a.F - VEC;  // load offset, always in range
   }
 
   for (int64_t it = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> a.lgG; it < n_work; it += ngroups) {
@@ -135,79 +182,10 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
       for (int k = 0; k < VEC; ++k) acc[t][k] = R::init();
 
     int32_t e = beg;
-    for (; e + U <= end; e += U) {
-      int32_t c[U];
-      float wt[U];
-      if (a.hints & 1) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          c[u] = ld_nt(a.idx + e + u);
-          if constexpr (WEIGHTED) wt[u] = ld_nt(a.w + e + u);
-        }
-      } else {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          c[u] = a.idx[e + u];
-          if constexpr (WEIGHTED) wt[u] = a.w[e + u];
-        }
-      }
-      float v[U][NT][VEC];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          if (fv[t]) {
-            vload<VEC>(v[u][t], a.table + int64_t(c[u]) * a.ld_t + fo[t]);
-          } else {
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) v[u][t][k] = 0.0f;
-          }
-        }
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-          for (int k = 0; k < VEC; ++k) {
-            const float m = WEIGHTED ? __fmul_rn(v[u][t][k], wt[u]) : v[u][t][k];
-            acc[t][k] = R::combine(acc[t][k], R::msg(m));
-          }
-    }
-    if (e < end) {  // tail: n < U edges, all loads issued together
-      const int n = end - e;
-      int32_t c[U];
-      float wt[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int32_t ee = u < n ? e + u : end - 1;
-        c[u] = a.idx[ee];
-        if constexpr (WEIGHTED) wt[u] = a.w[ee];
-      }
-      float v[U][NT][VEC];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          if (fv[t] && u < n) {
-            vload<VEC>(v[u][t], a.table + int64_t(c[u]) * a.ld_t + fo[t]);
-          } else {
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) v[u][t][k] = 0.0f;
-          }
-        }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (u < n) {
-#pragma unroll
-          for (int t = 0; t < NT; ++t)
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) {
-              const float m = WEIGHTED ? __fmul_rn(v[u][t][k], wt[u]) : v[u][t][k];
-              acc[t][k] = R::combine(acc[t][k], R::msg(m));
-            }
-        }
-      }
-    }
+    for (; e + U <= end; e += U) edge_block<U, VEC, NT, RED, WEIGHTED>(a, e, end, fl, acc);
+    // tail in half-width blocks: at most TU-1 clamped (redundant, cache-hit) loads
+    constexpr int TU = U > 1 ? U / 2 : 1;
+    for (; e < end; e += TU) edge_block<TU, VEC, NT, RED, WEIGHTED>(a, e, end, fl, acc);
 
 #pragma unroll
     for (int t = 0; t < NT; ++t) {

@@ -57,6 +57,15 @@ struct FusedArgs {
   int debug;        // experiment knob (KGX_FUSED_DEBUG): 1 = skip the MFMA phase
 };
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops
+// (lgkmcnt) but NOT for its outstanding global loads (vmcnt), unlike
+// __syncthreads(), so gathers prefetched for the next tile stay in flight.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 template <int RED>
 struct Red {
   static __device__ __forceinline__ float init() {
@@ -133,22 +142,18 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
       }
     }
     pn = (end - beg) < U ? (end - beg) : U;
+    // unconditional loads from clamped addresses (idx/w hold >= 1 element);
+    // masking happens when the values are folded in, never around a load
     int32_t c[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int32_t ee = u < pn ? beg + u : beg;
-      c[u] = u < pn ? a.idx[ee] : 0;
-      if constexpr (WEIGHTED) pw[u] = u < pn ? a.w[ee] : 0.0f;
+      const int32_t ee = pn > 0 ? beg + (u < pn ? u : pn - 1) : 0;
+      const int32_t ci = a.idx[ee];
+      c[u] = pn > 0 ? ci : 0;
+      if constexpr (WEIGHTED) pw[u] = a.w[ee];
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (u < pn) {
-        vload<4>(pv[u], a.x + int64_t(c[u]) * a.ld_x + f);
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) pv[u][k] = 0.0f;
-      }
-    }
+    for (int u = 0; u < U; ++u) vload<4>(pv[u], a.x + int64_t(c[u]) * a.ld_x + f);
   };
 
   fetch(int64_t(blockIdx.x) * kGroups + g);
@@ -157,36 +162,13 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) acc[k] = R::init();
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (u < pn) {
+    for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float m = WEIGHTED ? __fmul_rn(pv[u][k], pw[u]) : pv[u][k];
-          acc[k] = R::combine(acc[k], R::msg(m));
-        }
+      for (int k = 0; k < 4; ++k) {
+        const float m = WEIGHTED ? __fmul_rn(pv[u][k], pw[u]) : pv[u][k];
+        acc[k] = R::combine(acc[k], u < pn ? R::msg(m) : R::init());
       }
-    }
-    int32_t e = beg + U;
-    for (; e + U <= end; e += U) {
-      int32_t c[U];
-      float wt[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        c[u] = a.idx[e + u];
-        if constexpr (WEIGHTED) wt[u] = a.w[e + u];
-      }
-      float v[U][4];
-#pragma unroll
-      for (int u = 0; u < U; ++u) vload<4>(v[u], a.x + int64_t(c[u]) * a.ld_x + f);
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float m = WEIGHTED ? __fmul_rn(v[u][k], wt[u]) : v[u][k];
-          acc[k] = R::combine(acc[k], R::msg(m));
-        }
-    }
-    if (e < end) {
+    for (int32_t e = beg + U; e < end; e += U) {
       const int n = end - e;
       int32_t c[U];
       float wt[U];
@@ -198,24 +180,14 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
       }
       float v[U][4];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (u < n) {
-          vload<4>(v[u], a.x + int64_t(c[u]) * a.ld_x + f);
-        } else {
+      for (int u = 0; u < U; ++u) vload<4>(v[u], a.x + int64_t(c[u]) * a.ld_x + f);
 #pragma unroll
-          for (int k = 0; k < 4; ++k) v[u][k] = 0.0f;
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float m = WEIGHTED ? __fmul_rn(v[u][k], wt[u]) : v[u][k];
+          acc[k] = R::combine(acc[k], u < n ? R::msg(m) : R::init());
         }
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (u < n) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const float m = WEIGHTED ? __fmul_rn(v[u][k], wt[u]) : v[u][k];
-            acc[k] = R::combine(acc[k], R::msg(m));
-          }
-        }
-      }
     }
     const bool full_row = row >= 0 && slot < 0;
     if (row >= 0 && slot >= 0) vstore<4>(a.partials + int64_t(slot) * kFin + f, acc);
@@ -230,7 +202,7 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
     }
     *reinterpret_cast<float4*>(&tile[g][f]) = make_float4(r[0], r[1], r[2], r[3]);
     if (lane == 0) tile_row[g] = full_row ? row : -1;
-    __syncthreads();
+    lds_barrier();
 
     fetch(base + stride + g);  // next tile's first gathers fly during the MFMAs
 
@@ -249,7 +221,7 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) otile[4 * q + j][n_col] = (d0[j] + d1[j]) + bcol;
     }
-    __syncthreads();
+    lds_barrier();
     // whole-row dwordx4 stores: group g writes its tile row (F_out/4 lanes)
     if (!(a.debug & 2)) {
       const int rr = tile_row[g];

@@ -1,0 +1,127 @@
+"""Per-config GPU measurements for BASELINE.json's configs (one MI355X).
+
+  python tools/bench_configs.py [c1 c2 c3 c4 c5 ...]
+
+C1 Cora-shaped 2-layer GCN; C2 GCN 1M/10M F128; C3 GATv2 1M/10M H8xC16;
+C4 GIN-sum 10M/100M F256 (one GPU; the 8-GPU sharded run is bench.py --gpus 8
+with GCN); C5 SAGE-mean ogbn-products-shaped 2,449,029 / 123,718,280 F100.
+Reports layer ms, aggregation-kernel ms (events on the launch stream),
+algorithmic GB/s (SURVEY.md §8d byte model) and edges/s.  A measurement
+helper, not part of the product.
+"""
+
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "keras-geometric_amd")]
+
+import torch  # noqa: E402
+
+import keras_geometric_amd as kgx  # noqa: E402
+from keras_geometric_amd import ops as kops  # noqa: E402
+from keras_geometric_amd import synthetic  # noqa: E402
+
+
+def run(step, steps=10, warmup=2):
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    kops.EVENT_SINK = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps * 1e3
+    ev = kops.EVENT_SINK
+    kops.EVENT_SINK = None
+    per_step = len(ev) // steps
+    agg = sum(s.elapsed_time(e) for s, e in ev) / steps
+    return dt, agg, per_step
+
+
+def graph(layer_obj):
+    return next(reversed(kgx.graph._CACHE.values()))[1]
+
+
+def spmm_bytes(n, e, f_gather, f_out, weighted):
+    return 4 * (n + 1) + e * (4 + (4 if weighted else 0) + 4 * f_gather) + 4 * n * f_out
+
+
+def c2(dev):
+    n, e, f = 1_000_000, 10_000_000, 128
+    ei = synthetic.rmat_edge_index(n, e, seed=0, device=dev)
+    x = torch.randn(n, f, device=dev)
+    layer = kgx.GCNConv(f)
+    layer([x, ei])
+    g = graph(layer)
+    ms, agg, _ = run(lambda: layer([x, ei]))
+    b = spmm_bytes(n, g.kept, f, f, True)
+    return dict(config="C2 GCN 1M/10M F128", layer_ms=ms, agg_ms=agg, e_agg=g.kept,
+                edges_per_s=g.kept / ms * 1e3, alg_GBps=b / agg / 1e6)
+
+
+def c3(dev):
+    n, e, H, C, fin = 1_000_000, 10_000_000, 8, 16, 128
+    ei = synthetic.rmat_edge_index(n, e, seed=0, device=dev)
+    x = torch.randn(n, fin, device=dev)
+    layer = kgx.GATv2Conv(C, heads=H)
+    layer([x, ei])
+    g = graph(layer)
+    ms, agg, _ = run(lambda: layer([x, ei]))
+    hc = H * C
+    b = 4 * (n + 1) + g.kept * (4 + 4 * hc) + 8 * n * hc
+    return dict(config="C3 GATv2 1M/10M H8xC16", layer_ms=ms, agg_ms=agg, e_agg=g.kept,
+                edges_per_s=g.kept / ms * 1e3, alg_GBps=b / agg / 1e6)
+
+
+def c4(dev):
+    n, e, f = 10_000_000, 100_000_000, 256
+    ei = synthetic.rmat_edge_index(n, e, seed=0, device=dev)
+    x = torch.randn(n, f, device=dev)
+    layer = kgx.GINConv(f, aggregator="sum")
+    layer([x, ei])
+    g = graph(layer)
+    ms, agg, _ = run(lambda: layer([x, ei]), steps=5)
+    b = spmm_bytes(n, g.kept, f, f, False) + 4 * n * f  # + x root row for the GIN epilogue
+    return dict(config="C4 GIN-sum 10M/100M F256 (1 GPU)", layer_ms=ms, agg_ms=agg, e_agg=g.kept,
+                edges_per_s=g.kept / ms * 1e3, alg_GBps=b / agg / 1e6)
+
+
+def c5(dev):
+    n, e, f = 2_449_029, 123_718_280, 100
+    ei = synthetic.rmat_edge_index(n, e, seed=0, device=dev)
+    x = torch.randn(n, f, device=dev)
+    layer = kgx.SAGEConv(f, aggregator="mean")
+    layer([x, ei])
+    g = graph(layer)
+    ms, agg, _ = run(lambda: layer([x, ei]), steps=5)
+    b = spmm_bytes(n, g.kept, f, f, False)
+    return dict(config="C5 SAGE-mean 2.45M/123.7M F100 (1 GPU)", layer_ms=ms, agg_ms=agg, e_agg=g.kept,
+                edges_per_s=g.kept / ms * 1e3, alg_GBps=b / agg / 1e6)
+
+
+def c1(dev):
+    n, e, fin = 2708, 10556, 1433
+    ei = synthetic.rmat_edge_index(n, e, seed=0, device=dev)
+    x = (torch.rand(n, fin, device=dev) < 0.0127).float()
+    l1, l2 = kgx.GCNConv(64), kgx.GCNConv(7)
+
+    def fwd():
+        return l2([torch.relu(l1([x, ei])), ei])
+
+    fwd()
+    ms, agg, _ = run(fwd, steps=50, warmup=5)
+    return dict(config="C1 Cora-shaped 2-layer GCN 1433-64-7", layer_ms=ms, agg_ms=agg)
+
+
+if __name__ == "__main__":
+    dev = torch.device("cuda", 0)
+    names = sys.argv[1:] or ["c1", "c2", "c3", "c4", "c5"]
+    for name in names:
+        r = globals()[name](dev)
+        print(json.dumps(r), flush=True)
+        kgx.clear_cache()
+        torch.cuda.empty_cache()
