@@ -52,6 +52,23 @@ def b_alg_spmm(n: int, e_agg: int, f: int, weighted: bool, f_out: int | None = N
     return 4 * (n + 1) + e_agg * (4 + (4 if weighted else 0) + 4 * f) + 4 * n * f_out
 
 
+def pmc_traffic(config: str, kernel: str) -> tuple[float | None, str | None]:
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC
+    summary (profiles/r*/pmc_<config>.json, written by tools/pmc_summary.py),
+    used only if it was profiled from the kernel sources being run."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("pmc_summary", ROOT / "tools" / "pmc_summary.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    for path in sorted(ROOT.glob(f"profiles/r*/pmc_{config}.json"), reverse=True):
+        d = json.loads(path.read_text())
+        if d.get("source_hash") != mod.source_hash() or kernel not in d.get("kernels", {}):
+            continue
+        return d["kernels"][kernel]["traffic_bytes_per_launch"], str(path.relative_to(ROOT))
+    return None, None
+
+
 def log(msg: str) -> None:
     if int(os.environ.get("RANK", "0")) == 0:
         print(f"[bench] {msg}", file=sys.stderr, flush=True)
@@ -181,6 +198,9 @@ def main() -> None:
     fused = world == 1 and not args.exact and _ops.fused_transform_supported(f_in, f_out)
     balg = b_alg_spmm(n_rows, e_agg, f_in if fused else f_out, weighted=True, f_out=f_out)
     achieved = balg / (kern_ms * 1e-3) / 1e9
+    traffic, traffic_src = (None, None)
+    if world == 1:
+        traffic, traffic_src = pmc_traffic(args.config, "spmm_gemm_kernel" if fused else "spmm_kernel")
     result = {
         "metric": METRIC,
         "value": value,
@@ -203,7 +223,7 @@ def main() -> None:
             "e_agg_per_gpu": e_agg,
             "max_in_degree": max_deg,
             "features": [f_in, f_out],
-            "mode": ("exact" if args.exact else "split-hub") + (", fused aggregate->transform (f32 MFMA)"
+            "mode": ("exact" if args.exact else "split-hub") + (", fused aggregate->transform (W on bf16x3-split MFMA, f32-accurate)"
                                                                  if fused else ", X.W GEMM then aggregate"),
             "parallelism": f"dst-shard{world}" if world > 1 else "single",
         },
@@ -216,7 +236,8 @@ def main() -> None:
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
             "algorithmic_bytes_per_launch": balg,
         },
         **shard_info,

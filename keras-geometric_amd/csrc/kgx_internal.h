@@ -7,6 +7,8 @@
 #include <cstdint>
 #include <cstdio>
 
+#include <cstdlib>
+
 #include "kgx.h"
 
 namespace kgx {

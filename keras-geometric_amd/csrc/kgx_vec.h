@@ -17,12 +17,7 @@ __device__ __forceinline__ void vload(float (&d)[VEC], const float* __restrict__
   if constexpr (VEC >= 4) {
 #pragma unroll
     for (int i = 0; i < VEC / 4; ++i) {
-#ifdef KGX_ROW_NT  // experiment: gathered rows with the non-temporal policy
-      const f32x4_t w4 = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(p) + i);
-      const float4 v = make_float4(w4[0], w4[1], w4[2], w4[3]);
-#else
       const float4 v = reinterpret_cast<const float4*>(p)[i];
-#endif
       d[4 * i + 0] = v.x;
       d[4 * i + 1] = v.y;
       d[4 * i + 2] = v.z;

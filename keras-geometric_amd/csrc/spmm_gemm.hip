@@ -11,15 +11,21 @@
 //
 // Block = 512 threads = 16 row-groups of 32 lanes (F_in = 128: float4 per
 // lane).  Per iteration the block takes 16 consecutive schedule items; each
-// group reduces its item's edges exactly like spmm_kernel (8 gathers in
-// flight, sequential RN adds) into an LDS tile row; then wave w (of 8)
-// computes output columns [16w, 16w+16) of the 16-row tile with 32
-// v_mfma_f32_16x16x4_f32 (K = 128), W's 16 columns held in 32 VGPRs per lane
-// for the whole kernel.  K order is permuted so each lane's A fragment is 32
-// contiguous floats of its tile row (8 ds_read_b128): k-step s uses
-// k = 32*(lane>>4) + s.  Hub-row chunks write raw partials; the fix-up kernel
-// combines them and applies W with VALU.
+// group reduces its item's edges exactly like spmm_kernel (4 gathers in
+// flight, sequential RN adds) and writes the row, split three ways into bf16
+// hi/mid/lo planes, to an LDS tile; then wave w (of 8) computes output columns
+// [16w, 16w+16) of the 16-row tile with 24 v_mfma_f32_16x16x32_bf16 (the six
+// significant cross products of the split operands over K = 128), W's split
+// fragments held in 48 VGPRs per lane for the whole kernel.  The split product
+// is f32-accurate (dropped terms <= 2^-24 |x w|) and runs at 16x the per-clock
+// rate of the f32-input MFMA, which on this kernel could not be hidden behind
+// the gathers (NS: 11.37 ms with f32 MFMA, 10.43 with the split; 10.3 with no
+// MFMA at all).  The next tile's first U rows are prefetched before the MFMA
+// phase; barriers are LDS-only so those gathers stay in flight.  Hub-row
+// chunks write raw partials; the fix-up kernel combines them and applies W in
+// f32 on the VALU.
 #include <cstdlib>
+#include <type_traits>
 
 #include "kgx_internal.h"
 #include "kgx_vec.h"
@@ -31,6 +37,9 @@ constexpr int kFin = 128;
 constexpr int kGroups = 16;       // rows per block iteration
 constexpr int kThreads = kGroups * 32;
 constexpr int kTileLd = kFin + 4;  // padded LDS row
+#ifndef KGX_FUSED_BF16X3
+#define KGX_FUSED_BF16X3 1  // 0: f32-input MFMA (exact f32 products, 16x slower per clock)
+#endif
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -54,7 +63,7 @@ struct FusedArgs {
   float* partials;  // [n_slots, 128]
   int pre_gin;      // apply gin_scale * x[row] + aggr before the transform
   float gin_scale;
-  int debug;        // experiment knob (KGX_FUSED_DEBUG): 1 = skip the MFMA phase
+  int debug;        // experiment knob (KGX_FUSED_DEBUG): 1 skip the MFMA phase, 2 skip stores
 };
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops
@@ -64,6 +73,31 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+}
+
+// ---- three-way bf16 split of f32 operands (the "bf16x3" product) ---------
+// x = hi + mid + lo exactly (each a bf16, round-to-nearest-even residuals;
+// non-finite x keeps hi = x and zero residuals).  x*w is then taken as the six
+// bf16 x bf16 products whose orders sum to <= 2 (dropped terms are <= 2^-24
+// |x w|, the f32 rounding level), each exact in the MFMA's f32 accumulator,
+// on v_mfma_f32_16x16x32_bf16 -- 16x the per-clock rate of the f32-input MFMA.
+typedef short bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short bf16x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ short bf16_bits(float x) {
+  const __bf16 h = static_cast<__bf16>(x);  // v_cvt_pk_bf16_f32 (RNE, NaN-preserving)
+  return __builtin_bit_cast(short, h);
+}
+__device__ __forceinline__ float bf16_value(short b) {
+  return __builtin_bit_cast(float, static_cast<uint32_t>(static_cast<uint16_t>(b)) << 16);
+}
+__device__ __forceinline__ __attribute__((unused)) void split3(float x, short& hi, short& mid, short& lo) {
+  hi = bf16_bits(x);
+  const float h = bf16_value(hi);
+  float r = __builtin_isfinite(h) ? __fsub_rn(x, h) : 0.0f;  // exact
+  mid = bf16_bits(r);
+  r = __fsub_rn(r, bf16_value(mid));  // exact
+  lo = bf16_bits(r);
 }
 
 template <int RED>
@@ -94,8 +128,17 @@ struct Red {
 template <int RED, bool WEIGHTED>
 __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
   using R = Red<RED>;
-  constexpr int U = 8;
+#ifdef KGX_FUSED_U
+  constexpr int U = KGX_FUSED_U;
+#else
+  constexpr int U = 4;  // gathers in flight per group (measured: 4 beats 6 and 8 here)
+#endif
+  constexpr int PF = U;  // rows prefetched per group for the next tile
+#if KGX_FUSED_BF16X3
+  __shared__ short tile3[3][kGroups][kFin + 8];  // hi / mid / lo planes of the aggregated rows
+#else
   __shared__ float tile[kGroups][kTileLd];
+#endif
   __shared__ float otile[kGroups][kTileLd];  // MFMA results, re-read as whole rows
   __shared__ int32_t tile_row[kGroups];
 
@@ -110,9 +153,26 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
   const bool mfma_wave = wave * 16 < a.F_out;
 
   // W fragment for this wave's 16 columns, K permuted: k = 32 q + s.
+#if KGX_FUSED_BF16X3
+  // B fragments: k-step s (0..3) of lane group q covers k = 32 q + 8 s + j (j = 0..7),
+  // so each A fragment is 8 contiguous bf16 of a tile row (one ds_read_b128).
+  bf16x8_t wfh[4], wfm[4], wfl[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = mfma_wave ? a.W[int64_t(32 * q + 8 * s + j) * a.F_out + n_col] : 0.0f;
+      short h, m_, l;
+      split3(v, h, m_, l);
+      wfh[s][j] = h;
+      wfm[s][j] = m_;
+      wfl[s][j] = l;
+    }
+#else
   float wb[32];
 #pragma unroll
   for (int s = 0; s < 32; ++s) wb[s] = mfma_wave ? a.W[int64_t(32 * q + s) * a.F_out + n_col] : 0.0f;
+#endif
   const float bcol = (mfma_wave && a.bias) ? a.bias[n_col] : 0.0f;
 
   const int64_t n_work = a.items ? a.n_items : a.n_rows;
@@ -123,7 +183,7 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
   // flight while the matrix pipe works.
   int32_t row = -1, beg = 0, end = 0, slot = -1;
   int pn = 0;
-  float pv[U][4], pw[U];
+  float pv[PF][4], pw[PF];
   auto fetch = [&](int64_t it) {
     row = -1;
     beg = end = 0;
@@ -141,19 +201,22 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
         end = a.rowptr[row + 1];
       }
     }
-    pn = (end - beg) < U ? (end - beg) : U;
+    pn = (end - beg) < PF ? (end - beg) : PF;
     // unconditional loads from clamped addresses (idx/w hold >= 1 element);
     // masking happens when the values are folded in, never around a load
-    int32_t c[U];
+    int32_t c[PF];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+    for (int u = 0; u < PF; ++u) {
       const int32_t ee = pn > 0 ? beg + (u < pn ? u : pn - 1) : 0;
       const int32_t ci = a.idx[ee];
       c[u] = pn > 0 ? ci : 0;
       if constexpr (WEIGHTED) pw[u] = a.w[ee];
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) vload<4>(pv[u], a.x + int64_t(c[u]) * a.ld_x + f);
+    for (int u = 0; u < PF; ++u) {
+      if (u < pn)  // exec-masked: rows of degree < PF issue no redundant loads
+        vload<4>(pv[u], a.x + int64_t(c[u]) * a.ld_x + f);
+    }
   };
 
   fetch(int64_t(blockIdx.x) * kGroups + g);
@@ -162,33 +225,38 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) acc[k] = R::init();
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int u = 0; u < PF; ++u)
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const float m = WEIGHTED ? __fmul_rn(pv[u][k], pw[u]) : pv[u][k];
         acc[k] = R::combine(acc[k], u < pn ? R::msg(m) : R::init());
       }
-    for (int32_t e = beg + U; e < end; e += U) {
+    auto block = [&](auto UB, int32_t e) {
+      constexpr int B = decltype(UB)::value;
       const int n = end - e;
-      int32_t c[U];
-      float wt[U];
+      int32_t c[B];
+      float wt[B];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
+      for (int u = 0; u < B; ++u) {
         const int32_t ee = u < n ? e + u : end - 1;
         c[u] = a.idx[ee];
         if constexpr (WEIGHTED) wt[u] = a.w[ee];
       }
-      float v[U][4];
+      float v[B][4];
 #pragma unroll
-      for (int u = 0; u < U; ++u) vload<4>(v[u], a.x + int64_t(c[u]) * a.ld_x + f);
+      for (int u = 0; u < B; ++u) vload<4>(v[u], a.x + int64_t(c[u]) * a.ld_x + f);
 #pragma unroll
-      for (int u = 0; u < U; ++u)
+      for (int u = 0; u < B; ++u)
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const float m = WEIGHTED ? __fmul_rn(v[u][k], wt[u]) : v[u][k];
           acc[k] = R::combine(acc[k], u < n ? R::msg(m) : R::init());
         }
-    }
+    };
+    int32_t e = beg + PF;
+    // full blocks, then half-width tail blocks (at most U/2 - 1 clamped redundant loads)
+    for (; e + U <= end; e += U) block(std::integral_constant<int, U>{}, e);
+    for (; e < end; e += U / 2) block(std::integral_constant<int, U / 2>{}, e);
     const bool full_row = row >= 0 && slot < 0;
     if (row >= 0 && slot >= 0) vstore<4>(a.partials + int64_t(slot) * kFin + f, acc);
     float r[4];
@@ -200,7 +268,24 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) r[k] = __fadd_rn(__fmul_rn(a.gin_scale, xv[k]), r[k]);
     }
+#if KGX_FUSED_BF16X3
+    {
+      bf16x4_t ph, pm, pl;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        short h, m_, l;
+        split3(r[k], h, m_, l);
+        ph[k] = h;
+        pm[k] = m_;
+        pl[k] = l;
+      }
+      *reinterpret_cast<bf16x4_t*>(&tile3[0][g][f]) = ph;
+      *reinterpret_cast<bf16x4_t*>(&tile3[1][g][f]) = pm;
+      *reinterpret_cast<bf16x4_t*>(&tile3[2][g][f]) = pl;
+    }
+#else
     *reinterpret_cast<float4*>(&tile[g][f]) = make_float4(r[0], r[1], r[2], r[3]);
+#endif
     if (lane == 0) tile_row[g] = full_row ? row : -1;
     lds_barrier();
 
@@ -210,14 +295,31 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
       const int m = wl & 15;
       f32x4 d0 = {0.0f, 0.0f, 0.0f, 0.0f};
       f32x4 d1 = {0.0f, 0.0f, 0.0f, 0.0f};  // two chains: the f32 MFMA's dependent latency is 40 > 32 cycles
+#if KGX_FUSED_BF16X3
 #pragma unroll
-      for (int s0 = 0; s0 < 32; s0 += 4) {
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const bf16x8_t ah = *reinterpret_cast<const bf16x8_t*>(&tile3[0][m][32 * q + 8 * s4]);
+        const bf16x8_t am = *reinterpret_cast<const bf16x8_t*>(&tile3[1][m][32 * q + 8 * s4]);
+        const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(&tile3[2][m][32 * q + 8 * s4]);
+        // small terms first
+        d1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, wfh[s4], d1, 0, 0, 0);
+        d0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfl[s4], d0, 0, 0, 0);
+        d1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, wfm[s4], d1, 0, 0, 0);
+        d0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, wfh[s4], d0, 0, 0, 0);
+        d1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfm[s4], d1, 0, 0, 0);
+        d0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfh[s4], d0, 0, 0, 0);
+      }
+#else
+      constexpr int s_end = 32;
+#pragma unroll
+      for (int s0 = 0; s0 < s_end; s0 += 4) {
         const float4 t4 = *reinterpret_cast<const float4*>(&tile[m][32 * q + s0]);
         d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(t4.x, wb[s0 + 0], d0, 0, 0, 0);
         d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(t4.y, wb[s0 + 1], d1, 0, 0, 0);
         d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(t4.z, wb[s0 + 2], d0, 0, 0, 0);
         d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(t4.w, wb[s0 + 3], d1, 0, 0, 0);
       }
+#endif
 #pragma unroll
       for (int j = 0; j < 4; ++j) otile[4 * q + j][n_col] = (d0[j] + d1[j]) + bcol;
     }

@@ -10,3 +10,6 @@ timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/p
   --kernel-include-regex spmm -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof/fetch.log 2>&1 || exit $?
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof/write -o run \
   --kernel-include-regex spmm -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof/write.log 2>&1 || exit $?
+F=$(find gpurun_out/prof/fetch -name '*counter_collection.csv' | head -n 1)
+W=$(find gpurun_out/prof/write -name '*counter_collection.csv' | head -n 1)
+python tools/pmc_summary.py "$F" "$W" gpurun_out/prof/pmc_ns.json --config ns

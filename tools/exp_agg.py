@@ -95,5 +95,50 @@ def ns_once(n=10_000_000, e=100_000_000, f=128, split=512):
                       "TBps_alg": b_alg(n, g.kept, f) / ms / 1e9}), flush=True)
 
 
+def ns_both(n=10_000_000, e=100_000_000, f=128):
+    """NS timing of the unfused weighted aggregation and the fused GCN kernel
+    with the library named by KGX_LIB (used by `ab`)."""
+    import os
+
+    dev = torch.device("cuda", 0)
+    ei = synthetic.rmat_edge_index(n, e, seed=0, device=dev)
+    h = torch.randn(n, f, device=dev)
+    W = torch.randn(f, f, device=dev) * (1.0 / f) ** 0.5
+    g = G.build_csr(ei[0].contiguous(), ei[1].contiguous(), n, n, self_loops=True, gcn_norm=True)
+    ms = timeit(lambda: kops.aggregate(g, h, "sum", weighted=True), reps=20)
+    msf = timeit(lambda: kops.aggregate_transform(g, h, W, "sum", weighted=True), reps=20)
+    print(json.dumps({"lib": os.path.basename(os.environ.get("KGX_LIB", "libkgx.so")),
+                      "env": {k: v for k, v in os.environ.items() if k.startswith("KGX_") and k != "KGX_LIB"},
+                      "spmm_ms": round(ms, 3), "fused_ms": round(msf, 3),
+                      "TBps_alg": round(b_alg(n, g.kept, f) / ms / 1e9, 3)}), flush=True)
+
+
+def ab(specs, rounds=2):
+    """A/B over library variants / env knobs, each in its own process, interleaved.
+    spec = "libname[:KEY=VAL,...]" with libname "main" or a lib/variants/libkgx_<name>.so.
+    This parent never touches the GPU (children are started before any HIP call)."""
+    import os
+    import subprocess
+
+    for r in range(rounds):
+        for spec in specs:
+            name, _, kv = spec.partition(":")
+            env = dict(os.environ)
+            if name != "main":
+                env["KGX_LIB"] = str(ROOT / "keras-geometric_amd" / "lib" / "variants" / f"libkgx_{name}.so")
+            for item in filter(None, kv.split(",")):
+                k, _, v = item.partition("=")
+                env[k] = v
+            res = subprocess.run([sys.executable, __file__, "both"], env=env, timeout=300,
+                                 capture_output=True, text=True)
+            line = " | ".join(res.stdout.strip().splitlines()[-2:]) if res.stdout.strip() else res.stderr[-2000:]
+            print(f"round{r} {spec}: {line}", flush=True)
+            if res.returncode != 0:
+                raise SystemExit(res.returncode)
+
+
 if __name__ == "__main__":
-    {"sweep": sweep, "calib": calib, "ns": ns_once}[sys.argv[1]]()
+    if sys.argv[1] == "ab":
+        ab(sys.argv[2:])
+    else:
+        {"sweep": sweep, "calib": calib, "ns": ns_once, "both": ns_both}[sys.argv[1]]()

@@ -1,0 +1,78 @@
+"""Summarise rocprofv3 PMC passes into the per-launch HBM traffic bench.py reports.
+
+  python tools/pmc_summary.py FETCH_CSV WRITE_CSV OUT_JSON [--config ns]
+
+FETCH_CSV / WRITE_CSV are rocprofv3 `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE`
+counter_collection.csv files of the same bench.py command.  Per kernel the
+median over dispatches is taken (the first launches include graph-build
+effects).  Corrections follow /opt/skills/guides/MI355X_MICROARCH.md (HBM /
+rocprofv3): both counters are in KiB; on gfx950 FETCH_SIZE reports half the
+bytes of 16-B-per-lane reads (TCC_EA0_RDREQ x 64 B for 128-B requests), so it
+is doubled -- verified for this kernel family's row-gather pattern by the
+calibration in tools/exp_agg.py `calib`.
+WRITE_SIZE is exact for 16-B-per-lane stores.
+
+The output carries a hash of the kernel sources; bench.py only attaches the
+traffic when the hash matches the sources it runs, so a stale profile is never
+reported against a changed kernel.
+"""
+
+from __future__ import annotations
+
+import csv
+import hashlib
+import json
+import statistics
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+CSRC = ROOT / "keras-geometric_amd" / "csrc"
+
+
+def source_hash() -> str:
+    h = hashlib.sha256()
+    for p in sorted(CSRC.glob("*")):
+        if p.suffix in (".hip", ".cpp", ".h"):
+            h.update(p.name.encode())
+            h.update(p.read_bytes())
+    return h.hexdigest()[:16]
+
+
+def per_kernel(path: str, counter: str) -> dict[str, float]:
+    vals: dict[str, list[float]] = {}
+    with open(path, newline="") as f:
+        for r in csv.DictReader(f):
+            if r["Counter_Name"] != counter:
+                continue
+            name = r["Kernel_Name"]
+            vals.setdefault(name, []).append(float(r["Counter_Value"]))
+    return {k: statistics.median(v) for k, v in vals.items()}
+
+
+def short(name: str) -> str:
+    base = name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
+    return base.split("::")[-1].split("<")[0]
+
+
+def main() -> None:
+    fetch_csv, write_csv, out = sys.argv[1:4]
+    config = sys.argv[sys.argv.index("--config") + 1] if "--config" in sys.argv else "ns"
+    fetch = per_kernel(fetch_csv, "FETCH_SIZE")
+    write = per_kernel(write_csv, "WRITE_SIZE")
+    kernels = {}
+    for name in sorted(set(fetch) | set(write)):
+        fk, wk = fetch.get(name), write.get(name)
+        kernels[short(name)] = {
+            "kernel": name,
+            "fetch_size_kib_median": fk,
+            "write_size_kib_median": wk,
+            "traffic_bytes_per_launch": (2 * fk * 1024 if fk is not None else 0) + (wk * 1024 if wk is not None else 0),
+        }
+    json.dump({"config": config, "source_hash": source_hash(), "correction": "FETCH_SIZE x 2 x 1024 + WRITE_SIZE x 1024",
+               "kernels": kernels}, open(out, "w"), indent=1)
+    print(json.dumps({k: v["traffic_bytes_per_launch"] / 1e9 for k, v in kernels.items()}))
+
+
+if __name__ == "__main__":
+    main()
