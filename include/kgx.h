@@ -153,19 +153,23 @@ int kgx_spmm(int reduce, int epilogue,
 /* ---------------------------------------------------------------------------
  * Fused aggregate -> dense transform (+ bias), one launch (plus a fix-up for
  * split hub rows):
- *   out[i,:] = bias + PRE( REDUCE_{e in row i} x[idx[e],:] * (w ? w[e] : 1) ) @ W
- *   PRE = identity, or gin_scale * x[i,:] + aggr when pre_gin != 0.
+ *   out[i,:] (+)= bias + PRE( REDUCE_{e in row i} x[idx[e],:] * (w ? w[e] : 1) ) @ W
+ *   PRE = identity, or gin_scale * x[i,:] + aggr with KGX_FUSED_PRE_GIN;
+ *   "+=" (read-add-write of out) with KGX_FUSED_ACCUMULATE, used to add the
+ *   halo-source part of a sharded row after its local part (distributed.py).
  * Replaces GCNConv's per-edge x_j @ W + segment_sum + bias (gcn_conv.py:233-272)
  * and GINConv's (1+eps)x + aggr -> single-Dense MLP (gin_conv.py:216-225) by the
  * algebraically equal aggregate-then-transform order (W applied once per row
- * on f32 MFMA); tolerance-equal to the reference, not bit-equal.
+ * on MFMA as the six significant products of a three-way bf16 split of both
+ * operands: f32-accurate); tolerance-equal to the reference, not bit-equal.
  * Shapes: F_in == 128, F_out a multiple of 16 <= 128, W [F_in, F_out] row-major.
  * reduce in {SUM, MEAN, MAX, MIN}; partials: n_slots * 128 floats.
  * ------------------------------------------------------------------------- */
+enum { KGX_FUSED_PRE_GIN = 1, KGX_FUSED_ACCUMULATE = 2 };
 int kgx_spmm_gemm(int reduce, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
                   const int32_t* items, int64_t n_items, const int32_t* split, int64_t n_split,
                   const int32_t* idx, const float* w, const float* x, int64_t ld_x, int64_t F_in,
-                  const float* W, int64_t F_out, const float* bias, int pre_gin, float gin_scale,
+                  const float* W, int64_t F_out, const float* bias, int flags, float gin_scale,
                   float* out, int64_t ld_out, float* partials, kgx_stream_t stream);
 
 /* ---------------------------------------------------------------------------

@@ -62,6 +62,7 @@ struct FusedArgs {
   int64_t ld_o;
   float* partials;  // [n_slots, 128]
   int pre_gin;      // apply gin_scale * x[row] + aggr before the transform
+  int accumulate;   // out += result
   float gin_scale;
   int debug;        // experiment knob (KGX_FUSED_DEBUG): 1 skip the MFMA phase, 2 skip stores
 };
@@ -327,8 +328,15 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
     // whole-row dwordx4 stores: group g writes its tile row (F_out/4 lanes)
     if (!(a.debug & 2)) {
       const int rr = tile_row[g];
-      if (rr >= 0 && f < a.F_out)
-        *reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + f) = *reinterpret_cast<const float4*>(&otile[g][f]);
+      if (rr >= 0 && f < a.F_out) {
+        float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + f);
+        float4 v = *reinterpret_cast<const float4*>(&otile[g][f]);
+        if (a.accumulate) {
+          const float4 p = *dst;
+          v = make_float4(__fadd_rn(p.x, v.x), __fadd_rn(p.y, v.y), __fadd_rn(p.z, v.z), __fadd_rn(p.w, v.w));
+        }
+        *dst = v;
+      }
     }
   }
 }
@@ -370,7 +378,9 @@ __global__ __launch_bounds__(256) void spmm_gemm_fixup_kernel(FusedArgs a) {
       for (int c = lane; c < a.F_out; c += 32) {
         float s = 0.0f;
         for (int k = 0; k < kFin; ++k) s = fmaf(vrow[g][k], a.W[int64_t(k) * a.F_out + c], s);
-        a.out[int64_t(row) * a.ld_o + c] = s + (a.bias ? a.bias[c] : 0.0f);
+        float v = s + (a.bias ? a.bias[c] : 0.0f);
+        if (a.accumulate) v = __fadd_rn(a.out[int64_t(row) * a.ld_o + c], v);
+        a.out[int64_t(row) * a.ld_o + c] = v;
       }
     }
     __syncthreads();
@@ -414,7 +424,7 @@ using namespace kgx;
 extern "C" int kgx_spmm_gemm(int reduce, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
                              const int32_t* items, int64_t n_items, const int32_t* split, int64_t n_split,
                              const int32_t* idx, const float* w, const float* x, int64_t ld_x, int64_t F_in,
-                             const float* W, int64_t F_out, const float* bias, int pre_gin, float gin_scale,
+                             const float* W, int64_t F_out, const float* bias, int flags, float gin_scale,
                              float* out, int64_t ld_out, float* partials, kgx_stream_t stream_) {
   hipStream_t stream = as_stream(stream_);
   KGX_REQUIRE(reduce >= KGX_SUM && reduce <= KGX_MIN, KGX_ERR_ARG, "kgx_spmm_gemm: reduce %d unsupported", reduce);
@@ -423,6 +433,8 @@ extern "C" int kgx_spmm_gemm(int reduce, const int32_t* rowptr, const int32_t* r
   KGX_REQUIRE(F_out > 0 && F_out <= 128 && F_out % 16 == 0, KGX_ERR_UNSUPPORTED,
               "kgx_spmm_gemm: F_out must be a multiple of 16 <= 128 (got %lld)", (long long)F_out);
   KGX_REQUIRE(n_rows >= 0 && n_items >= 0 && n_split >= 0, KGX_ERR_ARG, "kgx_spmm_gemm: negative size");
+  KGX_REQUIRE((flags & ~(KGX_FUSED_PRE_GIN | KGX_FUSED_ACCUMULATE)) == 0, KGX_ERR_ARG,
+              "kgx_spmm_gemm: unknown flags 0x%x", flags);
   if (n_rows == 0) return KGX_OK;
   KGX_REQUIRE(rowptr && rows && idx && x && W && out, KGX_ERR_ARG, "kgx_spmm_gemm: null pointer");
   KGX_REQUIRE(ld_x % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0 && ld_out >= F_out, KGX_ERR_ARG,
@@ -447,7 +459,8 @@ extern "C" int kgx_spmm_gemm(int reduce, const int32_t* rowptr, const int32_t* r
   a.out = out;
   a.ld_o = ld_out;
   a.partials = partials;
-  a.pre_gin = pre_gin;
+  a.pre_gin = (flags & KGX_FUSED_PRE_GIN) != 0;
+  a.accumulate = (flags & KGX_FUSED_ACCUMULATE) != 0;
   a.gin_scale = gin_scale;
   static const int dbg = [] {
     const char* h = getenv("KGX_FUSED_DEBUG");

@@ -10,9 +10,16 @@ Sources owned by other ranks ("halo" rows) are fetched once per layer with a
 single all-to-all-v over RCCL (torch.distributed "nccl" = RCCL on ROCm, over
 xGMI): the send lists are planned once per graph.
 
-Per layer:   table[:n_local] = x_local @ W          (GEMM)
-             table[n_local:] = halo all-to-all(gather(table, send_rows))
-             out = fused kgx aggregation over the local CSR (sources index table)
+GCN layer, default mode (aggregate-then-transform, exchange overlapped):
+    side stream:  send = gather(x_local, send_rows); RCCL all-to-all -> halo
+    main stream:  out  = bias + (A_own x_local) W        fused kgx kernel
+                  wait for the halo
+                  out += (A_halo halo) W                  same kernel, accumulate
+  (each row's sum is split own-sources-then-halo: tolerance-equal to one GPU)
+EXACT mode (and the generic propagate):
+    table[:n_local] = x_local (@ W);  table[n_local:] = halo all-to-all
+    out = kgx aggregation over the shard CSR in global input order
+  (bit-identical to the single-GPU EXACT result)
 
 The device work goes through a backend object; the default is the HIP engine.
 Tests substitute a CPU backend built on the oracle to check the planning and
@@ -56,6 +63,16 @@ class KgxBackend:
     def gather_rows(self, table: torch.Tensor, rows: torch.Tensor) -> torch.Tensor:
         return kops.gather_rows(table, rows)
 
+    def split_by_source(self, g, n_own: int):
+        return G.split_by_source(g, n_own)
+
+    def supports_fused(self, f_in: int, f_out: int) -> bool:
+        return kops.fused_transform_supported(f_in, f_out)
+
+    def aggregate_transform(self, g, x, W, bias=None, out=None):
+        """GCN sum with the edge weights, then @ W (+ bias); out += ... if given."""
+        return kops.aggregate_transform(g, x, W, "sum", weighted=True, bias=bias, out=out)
+
     def aggregate(self, g, table, reduce="sum", weighted=False, epilogue=nat.EPI_NONE, bias=None, xroot=None,
                   gin_scale=1.0, exact=False):
         return kops.aggregate(g, table, reduce, weighted=weighted, epilogue=epilogue, bias=bias, xroot=xroot,
@@ -77,6 +94,12 @@ class TorchComm:
 
     def all_to_all_single(self, out, inp, out_splits=None, in_splits=None) -> None:
         dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+
+    def all_to_all_start(self, out, inp, out_splits=None, in_splits=None):
+        """Enqueue the all-to-all behind the CURRENT stream's work and return a
+        handle whose wait() makes the then-current stream wait for it (RCCL runs
+        it on its own stream, so kernels on other streams overlap it)."""
+        return dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group, async_op=True)
 
     def broadcast(self, t, src: int = 0) -> None:
         dist.broadcast(t, src=src, group=self.group)
@@ -105,6 +128,9 @@ class ShardedGraph:
     backend: object
     comm: object = None
     exact: bool = False
+    _parts: tuple | None = None  # (own-source CSR, halo-source CSR), built on first use
+    _side: object = None  # HIP stream for the halo exchange
+    _halo_buf: dict | None = None
 
     @property
     def lo(self) -> int:
@@ -193,6 +219,48 @@ class ShardedGraph:
             table.new_empty((0, table.shape[1]))
         self.comm.all_to_all_single(table[self.n_local:], send, self.recv_counts, self.send_counts)
 
+    def own_halo_parts(self):
+        """The shard CSR split into own-source and halo-source parts (CSR order
+        kept inside each), halo sources indexed from 0 within the halo rows."""
+        if self._parts is None:
+            self._parts = self.backend.split_by_source(self.graph, self.n_local)
+        return self._parts
+
+    def halo_buffer(self, features: int, like: torch.Tensor) -> torch.Tensor:
+        """Persistent [n_halo, features] receive buffer (reused every layer call)."""
+        if self._halo_buf is None:
+            self._halo_buf = {}
+        key = (features, like.device)
+        buf = self._halo_buf.get(key)
+        if buf is None:
+            buf = torch.empty((self.n_halo, features), dtype=torch.float32, device=like.device)
+            self._halo_buf[key] = buf
+        return buf
+
+    def start_halo_exchange(self, x_local: torch.Tensor, halo: torch.Tensor):
+        """Pack the rows other ranks need and start the all-to-all into `halo`
+        on a side stream; returns a handle with wait() (or None if done)."""
+        def run():
+            send = self.backend.gather_rows(x_local, self.send_rows) if self.send_rows.numel() else \
+                x_local.new_empty((0, x_local.shape[1]))
+            start = getattr(self.comm, "all_to_all_start", None)
+            if start is None:
+                self.comm.all_to_all_single(halo, send, self.recv_counts, self.send_counts)
+                return None
+            return start(halo, send, self.recv_counts, self.send_counts)
+
+        if not x_local.is_cuda:
+            return run()
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=x_local.device)
+        cur = torch.cuda.current_stream(x_local.device)
+        self._side.wait_stream(cur)
+        with torch.cuda.stream(self._side):
+            work = run()
+        if work is None:  # synchronous comm: order the halo rows before later work
+            cur.wait_stream(self._side)
+        return work
+
     def propagate(self, x_local: torch.Tensor, reduce: str = "sum", **kw) -> torch.Tensor:
         """Sharded MessagePassing.propagate with the default message x_j."""
         table = self.new_table(x_local.shape[1], x_local)
@@ -230,11 +298,34 @@ class ShardedGCNConv(Layer):
             self._build_device = x_local.device
             self.build(tuple(x_local.shape))
         sg = self.sg
+        use_b = self.use_bias and self.bias is not None
+        if not sg.exact and sg.backend.supports_fused(x_local.shape[1], self.output_dim):
+            return self._forward_overlapped(x_local, self.bias if use_b else None)
         table = sg.new_table(self.output_dim, x_local)
         with torch.no_grad():  # forward engine: X W written straight into the table's own-rows slice
             torch.matmul(x_local, self.kernel, out=table[: sg.n_local])
         sg.halo_exchange(table)
-        use_b = self.use_bias and self.bias is not None
         return sg.backend.aggregate(sg.graph, table, "sum", weighted=True,
                                     epilogue=nat.EPI_BIAS if use_b else nat.EPI_NONE,
                                     bias=self.bias if use_b else None, exact=sg.exact)
+
+    def _forward_overlapped(self, x_local: torch.Tensor, bias) -> torch.Tensor:
+        """Aggregate-then-transform with the halo exchange overlapped:
+        side stream: pack send rows of X -> RCCL all-to-all into the halo buffer;
+        main stream: out = bias + (A_own X_own) W   (fused kernel, own sources);
+        then, once the halo has landed: out += (A_halo X_halo) W   (same kernel,
+        accumulate mode).  Each row's sum is split own-then-halo, a
+        re-association of the one-pass order (tolerance-equal; EXACT mode keeps
+        the one-pass order and waits for the halo)."""
+        sg = self.sg
+        g_own, g_halo = sg.own_halo_parts()
+        x_local = x_local.contiguous()
+        halo = sg.halo_buffer(x_local.shape[1], x_local)
+        with torch.no_grad():
+            work = sg.start_halo_exchange(x_local, halo)
+            out = sg.backend.aggregate_transform(g_own, x_local, self.kernel, bias=bias)
+            if work is not None:
+                work.wait()
+            if g_halo.kept:
+                sg.backend.aggregate_transform(g_halo, halo, self.kernel, out=out)
+        return out

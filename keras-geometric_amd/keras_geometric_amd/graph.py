@@ -171,6 +171,37 @@ def _build_schedule(g: CSRGraph, split_len: int) -> None:
     g.split = split[: max(g.n_split, 0)]
 
 
+def split_by_source(g: CSRGraph, n_own: int) -> tuple[CSRGraph, CSRGraph]:
+    """Split every CSR row into its edges from sources < n_own ("own") and the
+    rest ("other", sources re-based to col - n_own), each part in CSR order and
+    carrying its slice of the edge weights.  Used by the sharded layers to start
+    on a row's own-source part while its halo rows are still in flight
+    (distributed.py); sum(own) + sum(other) re-associates the row's sum, so the
+    split path is tolerance-equal, not bit-equal, to the one-pass row."""
+    if g.n_dst and int(g.kept):
+        row_of = torch.repeat_interleave(torch.arange(g.n_dst, device=g.device, dtype=torch.int32),
+                                         g.deg.long(), output_size=g.kept)
+    else:
+        row_of = torch.empty(0, dtype=torch.int32, device=g.device)
+    own = g.col < n_own
+    parts = []
+    for m, base, n_src in ((own, 0, n_own), (~own, n_own, g.n_src - n_own)):
+        deg = torch.bincount(row_of[m], minlength=g.n_dst).to(torch.int32)[: g.n_dst]
+        rowptr = torch.zeros(g.n_dst + 1, dtype=torch.int32, device=g.device)
+        rowptr[1:] = torch.cumsum(deg, 0)
+        col = g.col[m] - base if base else g.col[m]
+        kept = int(col.numel())
+        sub = CSRGraph(
+            n_src=n_src, n_dst=g.n_dst, n_input_edges=kept, kept=kept,
+            max_degree=int(deg.max()) if g.n_dst else 0, flags=g.flags,
+            rowptr=rowptr, col=col.contiguous(), eid=g.eid[m].contiguous(), deg=deg,
+            dinv=g.dinv, w=g.w[m].contiguous() if g.w is not None else None,
+        )
+        _build_schedule(sub, default_split_len(kept))
+        parts.append(sub)
+    return parts[0], parts[1]
+
+
 # ---------------------------------------------------------------------------
 # cache keyed on the caller's edge_index tensor (kept alive by the entry)
 # ---------------------------------------------------------------------------

@@ -119,6 +119,49 @@ def _spmm_gemm_fake(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, b
     return x.new_empty((rowptr.shape[0] - 1, W.shape[1]))
 
 
+@torch.library.custom_op("kgx::spmm_gemm_acc_", mutates_args=("out",))
+def spmm_gemm_acc_(
+    out: torch.Tensor,
+    x: torch.Tensor,
+    rowptr: torch.Tensor,
+    rows: torch.Tensor,
+    items: Optional[torch.Tensor],
+    split: Optional[torch.Tensor],
+    idx: torch.Tensor,
+    w: Optional[torch.Tensor],
+    n_slots: int,
+    reduce: int,
+    W: torch.Tensor,
+    bias: Optional[torch.Tensor],
+) -> None:
+    """out += bias + REDUCE(...) @ W (KGX_FUSED_ACCUMULATE), in place."""
+    x, w, W, bias = _f32c(x), _f32c(w), _f32c(W), _f32c(bias)
+    dev = nat.require_device(out, x, rowptr, rows, idx, w, W, bias, items, split)
+    n_dst = rowptr.numel() - 1
+    if out.dtype != torch.float32 or out.shape != (n_dst, W.shape[1]) or out.stride(1) != 1:
+        raise ValueError(f"spmm_gemm_acc_: out must be float32 [{n_dst}, {W.shape[1]}] with unit column stride")
+    if n_dst == 0:
+        return
+    n_items = 0 if items is None else items.shape[0]
+    n_split = 0 if split is None else split.shape[0]
+    partials = None
+    if items is not None and n_split > 0:
+        partials = torch.empty((n_slots, x.shape[1]), dtype=torch.float32, device=dev)
+    nat.check(
+        nat.lib().kgx_spmm_gemm(
+            reduce, nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, nat.ptr(split), n_split,
+            nat.ptr(idx), nat.ptr(w), nat.ptr(x), x.stride(0), x.shape[1], nat.ptr(W), W.shape[1], nat.ptr(bias),
+            nat.FUSED_ACCUMULATE, 1.0, nat.ptr(out), out.stride(0), nat.ptr(partials), nat.stream(dev),
+        ),
+        "kgx_spmm_gemm",
+    )
+
+
+@spmm_gemm_acc_.register_fake
+def _spmm_gemm_acc_fake(out, x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias):
+    return None
+
+
 def fused_transform_supported(f_in: int, f_out: int) -> bool:
     """Shapes kgx_spmm_gemm implements (aggregate-then-transform is also only
     worth it when F_in <= F_out)."""
@@ -275,13 +318,21 @@ def aggregate_transform(
     pre_gin: bool = False,
     gin_scale: float = 1.0,
     exact: bool = False,
+    out: torch.Tensor | None = None,
 ) -> torch.Tensor:
-    """out = bias + PRE(REDUCE_{e in row} x[col_e] * w_e) @ W in one fused launch."""
+    """out = bias + PRE(REDUCE_{e in row} x[col_e] * w_e) @ W in one fused launch
+    (out += ... in place when `out` is given)."""
     red = nat.REDUCE_IDS[reduce] if isinstance(reduce, str) else int(reduce)
     items, _, split, _, n_slots = g.work(exact)
     w = g.w if weighted else None
     if weighted and w is None:
         raise ValueError("graph was built without GCN normalisation weights")
+    if out is not None:  # accumulate into `out` (sum only: the caller splits a row's edges)
+        if pre_gin or red != nat.SUM:
+            raise ValueError("aggregate_transform(out=...) accumulates plain sums only")
+        _timed(lambda: torch.ops.kgx.spmm_gemm_acc_(out, x, g.rowptr, g.rows, items, split, g.col, w, n_slots, red,
+                                                   W, bias))
+        return out
     return _timed(lambda: torch.ops.kgx.spmm_gemm(
         x, g.rowptr, g.rows, items, split, g.col, w, n_slots, red, W, bias, bool(pre_gin), float(gin_scale)
     ))

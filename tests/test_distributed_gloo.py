@@ -43,6 +43,31 @@ class OracleBackend:
     def gather_rows(self, table, rows):
         return table[rows.long()]
 
+    def split_by_source(self, g, n_own):
+        rows = torch.repeat_interleave(torch.arange(g.n_dst), g.deg.long())
+        own = g.col.long() < n_own
+        parts = []
+        for m, base in ((own, 0), (~own, n_own)):
+            deg = torch.bincount(rows[m], minlength=g.n_dst).int()
+            rowptr = torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(deg.long(), 0)]).int()
+            parts.append(SimpleNamespace(rowptr=rowptr, col=(g.col[m].long() - base).int(), eid=g.eid[m], deg=deg,
+                                         n_dst=g.n_dst, kept=int(m.sum()), dinv=None, w=g.w[m],
+                                         device=torch.device("cpu")))
+        return parts[0], parts[1]
+
+    def supports_fused(self, f_in, f_out):
+        return True
+
+    def aggregate_transform(self, g, x, W, bias=None, out=None):
+        """sum_e w_e x[col_e] in CSR order, then @ W (+ bias); out += ... if given."""
+        y = torch.matmul(self.aggregate(g, x, "sum", weighted=True), W)
+        if bias is not None:
+            y = K.add(y, bias)
+        if out is None:
+            return y
+        out += y
+        return out
+
     def aggregate(self, g, table, reduce="sum", weighted=False, epilogue=nat.EPI_NONE, bias=None, **_):
         rows = torch.repeat_interleave(torch.arange(g.n_dst), g.deg.long())
         msg = table[g.col.long()]
@@ -105,7 +130,15 @@ def _worker(rank, world, port, q):
         gcn = sg.backend.aggregate(sg.graph, table, "sum", weighted=True, epilogue=nat.EPI_BIAS,
                                    bias=torch.from_numpy(b))
         mx = sg.propagate(torch.from_numpy(x[lo:hi]), "max")
-        q.put((rank, gcn.numpy(), mx.numpy(), sg.n_halo, sum(sg.send_counts)))
+        # the GCN layer's default (overlapped, own-then-halo) path
+        layer = kd.ShardedGCNConv(F_OUT, sg)
+        layer._build_device = torch.device("cpu")  # host-logic test with the oracle backend
+        layer.build((hi - lo, F_IN))
+        with torch.no_grad():
+            layer.kernel.copy_(torch.from_numpy(W))
+            layer.bias.copy_(torch.from_numpy(b))
+        y = layer(torch.from_numpy(x[lo:hi])).detach()
+        q.put((rank, gcn.numpy(), mx.numpy(), sg.n_halo, sum(sg.send_counts), y.numpy()))
     finally:
         dist.destroy_process_group()
 
@@ -123,8 +156,8 @@ def test_sharded_equals_unsharded_bitwise(world):
         p.start()
     results = {}
     for _ in range(world):
-        rank, gcn, mx, n_halo, n_send = q.get(timeout=90)
-        results[rank] = (gcn, mx, n_halo, n_send)
+        rank, gcn, mx, n_halo, n_send, y_split = q.get(timeout=90)
+        results[rank] = (gcn, mx, n_halo, n_send, y_split)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -140,3 +173,8 @@ def test_sharded_equals_unsharded_bitwise(world):
                       torch.from_numpy(b)).numpy()
     err = np.abs(gcn - y) / np.maximum(1, np.abs(y))
     assert err.max() <= 1e-5
+    # overlapped layer path: own-source part then halo part per row (re-associated sum)
+    y_split = np.concatenate([results[r][4] for r in range(world)])
+    err = np.abs(y_split - y) / np.maximum(1, np.abs(y))
+    assert err.max() <= 1e-5
+

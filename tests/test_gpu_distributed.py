@@ -68,9 +68,11 @@ def _run_rank(rank, hub, dev, x, out):
         m = sg.propagate(xl, "max")
         layer = kd.ShardedGCNConv(32, sg)
         y = layer(xl)
+        sg.exact = False  # default path: fused own-source part overlapped with the halo exchange
+        y2 = layer(xl)
         torch.cuda.synchronize()
         out[rank] = (s.cpu().numpy(), m.cpu().numpy(), y.detach().cpu().numpy(), layer.kernel.detach().cpu().numpy(),
-                     sg.n_halo)
+                     sg.n_halo, y2.detach().cpu().numpy())
     except BaseException as e:  # surface worker failures in the test thread
         out[rank] = e
         hub.barrier.abort()
@@ -107,3 +109,7 @@ def test_sharded_hip_equals_single_gpu(world, dev):
     got = np.concatenate([res[r][2] for r in range(world)])
     err = np.abs(got - ref) / np.maximum(1.0, np.abs(ref))
     assert err.max() <= 1e-5
+    got = np.concatenate([res[r][5] for r in range(world)])  # overlapped, split-sum path
+    err = np.abs(got - ref) / np.maximum(1.0, np.abs(ref))
+    assert err.max() <= 1e-5
+

@@ -332,3 +332,34 @@ def test_fused_aggregate_transform(dev, F_out, split_len):
     g = kops.aggregate_transform(csr, xd, Wd, "max", bias=None, pre_gin=True, gin_scale=1.5).cpu().numpy()
     h = (1.5 * T(x) + R.aggregate("max", T(x)[ei_l[0].long()], ei_l[1], N)).numpy().astype(np.float64)
     assert_dot_bound(g, h, W64, np.zeros_like(b64))
+
+
+@pytest.mark.parametrize("split_len", [0, 16])
+def test_fused_accumulate_own_halo_split(dev, split_len):
+    """split_by_source + kgx_spmm_gemm accumulate mode: the own-source part
+    (with bias) plus the other-source part accumulated in place equals the
+    one-pass fused GCN row within the dot-product bound (the split only
+    re-associates each row's sum)."""
+    N, E, F, F_out = 3000, 40000, 128, 64
+    s, d = rmat_edges(9, scale_for(N), N, 0, E)
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal((N, F)).astype(np.float32)
+    W = (rng.standard_normal((F, F_out)) * 0.1).astype(np.float32)
+    b = rng.standard_normal(F_out).astype(np.float32)
+    csr = build(np.stack([s, d]), N, dev, self_loops=True, gcn_norm=True, split_len=split_len)
+    xd, Wd, bd = T(x).to(dev), T(W).to(dev), T(b).to(dev)
+    n_own = N // 3
+    g_own, g_oth = G.split_by_source(csr, n_own)
+    assert g_own.kept + g_oth.kept == csr.kept
+    assert int(g_own.col.max()) < n_own and int(g_oth.col.min()) >= 0
+    torch.testing.assert_close(g_own.deg + g_oth.deg, csr.deg, rtol=0, atol=0)
+    out = kops.aggregate_transform(g_own, xd, Wd, "sum", weighted=True, bias=bd)
+    kops.aggregate_transform(g_oth, xd[n_own:].contiguous(), Wd, "sum", weighted=True, out=out)
+    one = kops.aggregate_transform(csr, xd, Wd, "sum", weighted=True, bias=bd).cpu().numpy()
+    rows = np.repeat(np.arange(N), csr.deg.cpu().numpy())
+    aggr = np.zeros((N, F))
+    np.add.at(aggr, rows, x[csr.col.cpu().numpy()].astype(np.float64) * csr.w.cpu().numpy()[:, None])
+    assert_dot_bound(out.cpu().numpy(), aggr, W.astype(np.float64), b.astype(np.float64), k_eps=2e-5)
+    assert_dot_bound(one, aggr, W.astype(np.float64), b.astype(np.float64), k_eps=2e-5)
+    with pytest.raises(ValueError):
+        kops.aggregate_transform(g_oth, xd[n_own:].contiguous(), Wd, "max", out=out)
