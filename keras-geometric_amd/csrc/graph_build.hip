@@ -183,17 +183,22 @@ __global__ void gcn_edge_norm_kernel(const int32_t* __restrict__ rowptr, const i
 // --------------------------------------------------------------------------
 // Schedule kernels
 // --------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t degree_bucket_key(int32_t d) {
-  // bucket b = floor(log2 d) + 1 (0 for d == 0); key 32 - b sorts descending.
-  const uint32_t b = d > 0 ? 32u - __clz(uint32_t(d)) : 0u;
-  return 32u - b;
+// Rows are scheduled in descending exact degree (stable: ascending row id
+// among equal degrees).  The fused kernel reduces 16 consecutive items in
+// lock-step, so equal-length neighbours matter: exact order measured 2.8 %
+// faster than log2 degree buckets at NS.  Degrees >= 2^24 tie (such rows are
+// split into chunks anyway).
+constexpr int kDegKeyBits = 24;
+__device__ __forceinline__ uint32_t degree_key(int32_t d) {
+  const uint32_t c = uint32_t(d) < (1u << kDegKeyBits) ? uint32_t(d) : (1u << kDegKeyBits) - 1u;
+  return ((1u << kDegKeyBits) - 1u) - c;
 }
 
 __global__ void sched_keys_kernel(const int32_t* __restrict__ rowptr, int64_t n_dst,
                                   uint32_t* __restrict__ keys, int32_t* __restrict__ iota) {
   const int64_t stride = int64_t(gridDim.x) * blockDim.x;
   for (int64_t r = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; r < n_dst; r += stride) {
-    keys[r] = degree_bucket_key(rowptr[r + 1] - rowptr[r]);
+    keys[r] = degree_key(rowptr[r + 1] - rowptr[r]);
     iota[r] = int32_t(r);
   }
 }
@@ -282,7 +287,7 @@ SchedLayout sched_layout(void* ws, int64_t n) {
   L.nslots = c.take<int32_t>(n);
   L.slot_off = c.take<int32_t>(n);
   L.st = c.take<SchedStatus>(1);
-  size_t sb = sort_temp_bytes(n, 6);
+  size_t sb = sort_temp_bytes(n, kDegKeyBits);
   size_t scb = 0;
   const int32_t* si = nullptr;
   int32_t* so = nullptr;
@@ -499,7 +504,7 @@ extern "C" int kgx_schedule_build(const int32_t* rowptr, int64_t n_dst, int32_t 
   KGX_CHECK_LAUNCH();
   size_t tb = L.tmp_bytes;
   KGX_CHECK_HIP(rocprim::radix_sort_pairs(L.tmp, tb, L.keys, L.keys_sorted, L.iota, rows, (unsigned)n_dst, 0,
-                                          6, stream, false));
+                                          kDegKeyBits, stream, false));
   hipLaunchKernelGGL(sched_count_kernel, dim3(g), dim3(kBlock), 0, stream, rowptr, rows, n_dst, split_len,
                      L.nchunks, L.nslots);
   KGX_CHECK_LAUNCH();

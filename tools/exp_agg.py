@@ -105,6 +105,12 @@ def ns_both(n=10_000_000, e=100_000_000, f=128):
     h = torch.randn(n, f, device=dev)
     W = torch.randn(f, f, device=dev) * (1.0 / f) ** 0.5
     g = G.build_csr(ei[0].contiguous(), ei[1].contiguous(), n, n, self_loops=True, gcn_norm=True)
+    if os.environ.get("KGX_EXP_SORT"):  # experiment: exact descending-degree item order (stable)
+        it = g.items
+        pre = int((it[:, 3] >= 0).sum())
+        rest = it[pre:]
+        order = torch.sort(rest[:, 2] - rest[:, 1], descending=True, stable=True).indices
+        g.items = torch.cat([it[:pre], rest[order]]).contiguous()
     ms = timeit(lambda: kops.aggregate(g, h, "sum", weighted=True), reps=20)
     msf = timeit(lambda: kops.aggregate_transform(g, h, W, "sum", weighted=True), reps=20)
     print(json.dumps({"lib": os.path.basename(os.environ.get("KGX_LIB", "libkgx.so")),
