@@ -164,13 +164,32 @@ int kgx_spmm(int reduce, int epilogue,
  * operands: f32-accurate); tolerance-equal to the reference, not bit-equal.
  * Shapes: F_in == 128, F_out a multiple of 16 <= 128, W [F_in, F_out] row-major.
  * reduce in {SUM, MEAN, MAX, MIN}; partials: n_slots * 128 floats.
+ * agg_out (optional, [n, ld_agg >= F_in]): also store PRE(REDUCE(...)), the
+ * rows before the transform — what the backward's dW = agg^T dOut needs.
  * ------------------------------------------------------------------------- */
 enum { KGX_FUSED_PRE_GIN = 1, KGX_FUSED_ACCUMULATE = 2 };
 int kgx_spmm_gemm(int reduce, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
                   const int32_t* items, int64_t n_items, const int32_t* split, int64_t n_split,
                   const int32_t* idx, const float* w, const float* x, int64_t ld_x, int64_t F_in,
                   const float* W, int64_t F_out, const float* bias, int flags, float gin_scale,
-                  float* out, int64_t ld_out, float* partials, kgx_stream_t stream);
+                  float* out, int64_t ld_out, float* partials, float* agg_out, int64_t ld_agg,
+                  kgx_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Backward of the segment max / min reduction (autograd of kgx_spmm MAX/MIN).
+ * torch's scatter_reduce amax/amin backward, under the reference's isinf
+ * guard (aggregators.py:99-112, 151-167): grad_out[i,f] is shared evenly by
+ * the edges of row i whose message equals the row's raw extreme; rows whose
+ * extreme is +-inf (empty rows included) or NaN pass nothing.
+ *   grad_table[idx[e], f] += grad_out[i, f] / ties   (float atomics)
+ * grad_table must be zero-initialised by the caller.  Sum / mean / weighted
+ * sums need no separate entry point: their backward is kgx_spmm over the
+ * transposed graph (a kgx_csr_build of the reversed edges).
+ * ------------------------------------------------------------------------- */
+int kgx_spmm_max_backward(int reduce, const int32_t* rowptr, int64_t n_rows, const int32_t* idx,
+                          const float* table, int64_t ld_table, int64_t F,
+                          const float* grad_out, int64_t ld_grad_out,
+                          float* grad_table, int64_t ld_grad_table, kgx_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Fused GATv2 attention aggregation (single pass, online segment softmax).

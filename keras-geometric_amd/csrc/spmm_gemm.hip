@@ -61,6 +61,8 @@ struct FusedArgs {
   float* out;
   int64_t ld_o;
   float* partials;  // [n_slots, 128]
+  float* agg_out;   // optional [n, 128]: the aggregated rows before the transform (kept for backward)
+  int64_t ld_agg;
   int pre_gin;      // apply gin_scale * x[row] + aggr before the transform
   int accumulate;   // out += result
   float gin_scale;
@@ -269,6 +271,7 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) r[k] = __fadd_rn(__fmul_rn(a.gin_scale, xv[k]), r[k]);
     }
+    if (full_row && a.agg_out) vstore<4>(a.agg_out + int64_t(row) * a.ld_agg + f, r);
 #if KGX_FUSED_BF16X3
     {
       bf16x4_t ph, pm, pl;
@@ -372,6 +375,7 @@ __global__ __launch_bounds__(256) void spmm_gemm_fixup_kernel(FusedArgs a) {
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) vrow[g][lane * 4 + k] = acc[k];
+      if (a.agg_out) vstore<4>(a.agg_out + int64_t(row) * a.ld_agg + lane * 4, acc);
     }
     __syncthreads();
     if (row >= 0) {
@@ -425,7 +429,8 @@ extern "C" int kgx_spmm_gemm(int reduce, const int32_t* rowptr, const int32_t* r
                              const int32_t* items, int64_t n_items, const int32_t* split, int64_t n_split,
                              const int32_t* idx, const float* w, const float* x, int64_t ld_x, int64_t F_in,
                              const float* W, int64_t F_out, const float* bias, int flags, float gin_scale,
-                             float* out, int64_t ld_out, float* partials, kgx_stream_t stream_) {
+                             float* out, int64_t ld_out, float* partials, float* agg_out, int64_t ld_agg,
+                             kgx_stream_t stream_) {
   hipStream_t stream = as_stream(stream_);
   KGX_REQUIRE(reduce >= KGX_SUM && reduce <= KGX_MIN, KGX_ERR_ARG, "kgx_spmm_gemm: reduce %d unsupported", reduce);
   KGX_REQUIRE(F_in == kFin, KGX_ERR_UNSUPPORTED, "kgx_spmm_gemm: F_in must be %d (got %lld)", kFin,
@@ -435,6 +440,8 @@ extern "C" int kgx_spmm_gemm(int reduce, const int32_t* rowptr, const int32_t* r
   KGX_REQUIRE(n_rows >= 0 && n_items >= 0 && n_split >= 0, KGX_ERR_ARG, "kgx_spmm_gemm: negative size");
   KGX_REQUIRE((flags & ~(KGX_FUSED_PRE_GIN | KGX_FUSED_ACCUMULATE)) == 0, KGX_ERR_ARG,
               "kgx_spmm_gemm: unknown flags 0x%x", flags);
+  KGX_REQUIRE(!agg_out || (ld_agg >= F_in && reinterpret_cast<uintptr_t>(agg_out) % 16 == 0 && ld_agg % 4 == 0),
+              KGX_ERR_ARG, "kgx_spmm_gemm: agg_out must be 16-byte aligned with ld >= F_in, ld %% 4 == 0");
   if (n_rows == 0) return KGX_OK;
   KGX_REQUIRE(rowptr && rows && idx && x && W && out, KGX_ERR_ARG, "kgx_spmm_gemm: null pointer");
   KGX_REQUIRE(ld_x % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0 && ld_out >= F_out, KGX_ERR_ARG,
@@ -459,6 +466,8 @@ extern "C" int kgx_spmm_gemm(int reduce, const int32_t* rowptr, const int32_t* r
   a.out = out;
   a.ld_o = ld_out;
   a.partials = partials;
+  a.agg_out = agg_out;
+  a.ld_agg = ld_agg;
   a.pre_gin = (flags & KGX_FUSED_PRE_GIN) != 0;
   a.accumulate = (flags & KGX_FUSED_ACCUMULATE) != 0;
   a.gin_scale = gin_scale;

@@ -56,7 +56,10 @@ _SIGNATURES = {
     "kgx_spmm_gemm": [
         _int, _i32p, _i32p, _i64, _i32p, _i64, _i32p, _i64,
         _i32p, _f32p, _f32p, _i64, _i64, _f32p, _i64, _f32p, _int, ctypes.c_float,
-        _f32p, _i64, _f32p, ctypes.c_void_p,
+        _f32p, _i64, _f32p, _f32p, _i64, ctypes.c_void_p,
+    ],
+    "kgx_spmm_max_backward": [
+        _int, _i32p, _i64, _i32p, _f32p, _i64, _i64, _f32p, _i64, _f32p, _i64, ctypes.c_void_p,
     ],
     "kgx_gatv2": [
         _i32p, _i32p, _i64, _i32p, _i64, _i32p, _i64,

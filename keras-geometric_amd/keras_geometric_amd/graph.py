@@ -171,6 +171,45 @@ def _build_schedule(g: CSRGraph, split_len: int) -> None:
     g.split = split[: max(g.n_split, 0)]
 
 
+def row_of_slot(g: CSRGraph) -> torch.Tensor:
+    """int32 [kept]: the destination row of every CSR slot (cached)."""
+    r = g.extras.get("row_of_slot")
+    if r is None:
+        if g.kept:
+            r = torch.repeat_interleave(torch.arange(g.n_dst, device=g.device, dtype=torch.int32),
+                                        g.deg.long(), output_size=g.kept)
+        else:
+            r = torch.empty(0, dtype=torch.int32, device=g.device)
+        g.extras["row_of_slot"] = r
+    return r
+
+
+def transpose(g: CSRGraph) -> CSRGraph:
+    """The reversed graph as a CSR over SOURCE rows (cached on `g`): row j lists
+    the edges leaving source j, in input-edge order (the order the reference's
+    autograd accumulates x_j's gradient in), `col` = the edge's destination row,
+    `w` = the same edge weight.  Built with the same stable kgx_csr_build, so
+    sum / mean / weighted-sum backward is one kgx_spmm over it."""
+    t = g.extras.get("T")
+    if t is not None:
+        return t
+    if g.kept:
+        order = torch.sort(g.eid, stable=True).indices  # slots in input-edge order
+        src_t = row_of_slot(g)[order].contiguous()  # reversed edge: dst row -> source
+        dst_t = g.col[order].contiguous()
+    else:
+        order = torch.empty(0, dtype=torch.int64, device=g.device)
+        src_t = dst_t = torch.empty(0, dtype=torch.int32, device=g.device)
+    t = build_csr(src_t, dst_t, g.n_dst, g.n_src)
+    slot = order[t.eid.long()] if t.kept else order  # forward CSR slot of every transposed slot
+    t.eid = g.eid[slot].contiguous() if t.kept else g.eid[:0]
+    if g.w is not None:
+        t.w = g.w[slot].contiguous()
+    t.extras["fwd_slot"] = slot
+    g.extras["T"] = t
+    return t
+
+
 def split_by_source(g: CSRGraph, n_own: int) -> tuple[CSRGraph, CSRGraph]:
     """Split every CSR row into its edges from sources < n_own ("own") and the
     rest ("other", sources re-based to col - n_own), each part in CSR order and
@@ -178,11 +217,7 @@ def split_by_source(g: CSRGraph, n_own: int) -> tuple[CSRGraph, CSRGraph]:
     on a row's own-source part while its halo rows are still in flight
     (distributed.py); sum(own) + sum(other) re-associates the row's sum, so the
     split path is tolerance-equal, not bit-equal, to the one-pass row."""
-    if g.n_dst and int(g.kept):
-        row_of = torch.repeat_interleave(torch.arange(g.n_dst, device=g.device, dtype=torch.int32),
-                                         g.deg.long(), output_size=g.kept)
-    else:
-        row_of = torch.empty(0, dtype=torch.int32, device=g.device)
+    row_of = row_of_slot(g)
     own = g.col < n_own
     parts = []
     for m, base, n_src in ((own, 0, n_own), (~own, n_own, g.n_src - n_own)):

@@ -108,6 +108,10 @@ class GINConv(MessagePassing):
             h = (1 + self.eps) * x if self.train_eps else (1 + self.eps_init) * x
             return self.mlp(h, training=training)
         g = graph_for(edge_index, ei, N, N, n_features=x.shape[1])
+        if self.train_eps and torch.is_grad_enabled() and self.eps.requires_grad:
+            # trainable eps: keep (1 + eps) in the autograd graph (gin_conv.py:216-225)
+            h = (1 + self.eps) * x + kops.aggregate(g, x.contiguous(), self.aggregator, exact=self.exact)
+            return self.mlp(h, training=training)
         h = kops.aggregate(g, x.contiguous(), self.aggregator, epilogue=nat.EPI_GIN, xroot=x.contiguous(),
                            gin_scale=self._scale(), exact=self.exact)
         return self.mlp(h, training=training)

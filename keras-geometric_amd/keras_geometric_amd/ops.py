@@ -75,6 +75,32 @@ def _spmm_fake(table, rowptr, rows, items, split, idx, w, n_slots, reduce, epilo
     return table.new_empty((rowptr.shape[0] - 1, table.shape[1]))
 
 
+def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale, save_agg):
+    x, w, W, bias = _f32c(x), _f32c(w), _f32c(W), _f32c(bias)
+    dev = nat.require_device(x, rowptr, rows, idx, w, W, bias, items, split)
+    n_dst = rowptr.numel() - 1
+    F_out = W.shape[1]
+    out = torch.empty((n_dst, F_out), dtype=torch.float32, device=dev)
+    agg = torch.empty((n_dst if save_agg else 0, x.shape[1]), dtype=torch.float32, device=dev)
+    if n_dst == 0:
+        return out, agg
+    n_items = 0 if items is None else items.shape[0]
+    n_split = 0 if split is None else split.shape[0]
+    partials = None
+    if items is not None and n_split > 0:
+        partials = torch.empty((n_slots, x.shape[1]), dtype=torch.float32, device=dev)
+    nat.check(
+        nat.lib().kgx_spmm_gemm(
+            reduce, nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, nat.ptr(split), n_split,
+            nat.ptr(idx), nat.ptr(w), nat.ptr(x), x.stride(0), x.shape[1], nat.ptr(W), F_out, nat.ptr(bias),
+            int(pre_gin), float(gin_scale), nat.ptr(out), out.stride(0), nat.ptr(partials),
+            nat.ptr(agg) if save_agg else None, agg.stride(0) if save_agg else 0, nat.stream(dev),
+        ),
+        "kgx_spmm_gemm",
+    )
+    return out, agg
+
+
 @torch.library.custom_op("kgx::spmm_gemm", mutates_args=())
 def spmm_gemm(
     x: torch.Tensor,
@@ -91,32 +117,39 @@ def spmm_gemm(
     pre_gin: bool,
     gin_scale: float,
 ) -> torch.Tensor:
-    x, w, W, bias = _f32c(x), _f32c(w), _f32c(W), _f32c(bias)
-    dev = nat.require_device(x, rowptr, rows, idx, w, W, bias, items, split)
-    n_dst = rowptr.numel() - 1
-    F_out = W.shape[1]
-    out = torch.empty((n_dst, F_out), dtype=torch.float32, device=dev)
-    if n_dst == 0:
-        return out
-    n_items = 0 if items is None else items.shape[0]
-    n_split = 0 if split is None else split.shape[0]
-    partials = None
-    if items is not None and n_split > 0:
-        partials = torch.empty((n_slots, x.shape[1]), dtype=torch.float32, device=dev)
-    nat.check(
-        nat.lib().kgx_spmm_gemm(
-            reduce, nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, nat.ptr(split), n_split,
-            nat.ptr(idx), nat.ptr(w), nat.ptr(x), x.stride(0), x.shape[1], nat.ptr(W), F_out, nat.ptr(bias),
-            int(pre_gin), float(gin_scale), nat.ptr(out), out.stride(0), nat.ptr(partials), nat.stream(dev),
-        ),
-        "kgx_spmm_gemm",
-    )
-    return out
+    return _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale,
+                           False)[0]
 
 
 @spmm_gemm.register_fake
 def _spmm_gemm_fake(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale):
     return x.new_empty((rowptr.shape[0] - 1, W.shape[1]))
+
+
+@torch.library.custom_op("kgx::spmm_gemm_save", mutates_args=())
+def spmm_gemm_save(
+    x: torch.Tensor,
+    rowptr: torch.Tensor,
+    rows: torch.Tensor,
+    items: Optional[torch.Tensor],
+    split: Optional[torch.Tensor],
+    idx: torch.Tensor,
+    w: Optional[torch.Tensor],
+    n_slots: int,
+    reduce: int,
+    W: torch.Tensor,
+    bias: Optional[torch.Tensor],
+    pre_gin: bool,
+    gin_scale: float,
+) -> tuple[torch.Tensor, torch.Tensor]:
+    """kgx::spmm_gemm that also returns the aggregated rows before the transform."""
+    return _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale, True)
+
+
+@spmm_gemm_save.register_fake
+def _spmm_gemm_save_fake(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale):
+    n = rowptr.shape[0] - 1
+    return x.new_empty((n, W.shape[1])), x.new_empty((n, x.shape[1]))
 
 
 @torch.library.custom_op("kgx::spmm_gemm_acc_", mutates_args=("out",))
@@ -151,7 +184,7 @@ def spmm_gemm_acc_(
         nat.lib().kgx_spmm_gemm(
             reduce, nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, nat.ptr(split), n_split,
             nat.ptr(idx), nat.ptr(w), nat.ptr(x), x.stride(0), x.shape[1], nat.ptr(W), W.shape[1], nat.ptr(bias),
-            nat.FUSED_ACCUMULATE, 1.0, nat.ptr(out), out.stride(0), nat.ptr(partials), nat.stream(dev),
+            nat.FUSED_ACCUMULATE, 1.0, nat.ptr(out), out.stride(0), nat.ptr(partials), None, 0, nat.stream(dev),
         ),
         "kgx_spmm_gemm",
     )
@@ -277,6 +310,89 @@ def _timed(fn):
     EVENT_SINK.append((start, end))
     return out
 
+def _reduce_id(reduce) -> int:
+    return nat.REDUCE_IDS[reduce] if isinstance(reduce, str) else int(reduce)
+
+
+def _needs_grad(*ts) -> bool:
+    return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts)
+
+
+def _aggregate_raw(g, table, red, weighted, by_edge, epilogue, bias, xroot, gin_scale, exact):
+    items, _, split, _, n_slots = g.work(exact or red == nat.STD)
+    idx = g.eid if by_edge else g.col
+    w = g.w if weighted else None
+    if weighted and w is None:
+        raise ValueError("graph was built without GCN normalisation weights")
+    return _timed(lambda: torch.ops.kgx.spmm(
+        table, g.rowptr, g.rows, items, split, idx, w, n_slots, red, epilogue, bias, xroot, float(gin_scale)
+    ))
+
+
+def _reduce_backward(g: CSRGraph, red: int, weighted: bool, by_edge: bool, table: torch.Tensor | None,
+                     grad_out: torch.Tensor, exact: bool, table_rows: int) -> torch.Tensor:
+    """d loss / d table of REDUCE_{e in row} table[idx_e] (* w_e), given d loss / d out.
+
+    sum / mean: the transposed aggregation (graph.transpose: each source row
+    gathers the gradient rows of its edges' destinations, in input-edge order);
+    max / min: kgx_spmm_max_backward (ties share evenly, +-inf rows pass
+    nothing — torch scatter_reduce amax/amin under the reference's isinf guard);
+    by_edge (message tensors): each message receives its row's gradient."""
+    from . import graph as G
+
+    grad_out = grad_out.contiguous()
+    if red == nat.STD:
+        raise NotImplementedError("kgx: backward of the std aggregation is not implemented")
+    if red in (nat.MAX, nat.MIN):
+        table = table.contiguous()
+        gt = torch.zeros_like(table)
+        idx = g.eid if by_edge else g.col
+        nat.check(
+            nat.lib().kgx_spmm_max_backward(
+                red, nat.ptr(g.rowptr), g.n_dst, nat.ptr(idx), nat.ptr(table), table.stride(0), table.shape[1],
+                nat.ptr(grad_out), grad_out.stride(0), nat.ptr(gt), gt.stride(0), nat.stream(table.device),
+            ),
+            "kgx_spmm_max_backward",
+        )
+        return gt
+    d = grad_out
+    if red == nat.MEAN:  # forward: sum / max(count_f32, 1e-8) (aggregators.py:56-85)
+        count = torch.clamp(g.deg, max=1 << 24).float()
+        d = (grad_out / torch.clamp(count, min=1e-8).unsqueeze(1)).contiguous()
+    if by_edge:
+        vals = d.index_select(0, G.row_of_slot(g).long())
+        if weighted:
+            vals = vals * g.w.unsqueeze(1)
+        gt = grad_out.new_zeros((table_rows, grad_out.shape[1]))
+        gt.index_copy_(0, g.eid.long(), vals)
+        return gt
+    t = G.transpose(g)
+    return _aggregate_raw(t, d, nat.SUM, weighted, False, nat.EPI_NONE, None, None, 1.0, exact)
+
+
+class _AggregateFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, table, bias, xroot, g, red, weighted, by_edge, epilogue, gin_scale, exact):
+        ctx.g, ctx.red, ctx.weighted, ctx.by_edge = g, red, weighted, by_edge
+        ctx.epilogue, ctx.gin_scale, ctx.exact = epilogue, gin_scale, exact
+        ctx.table_rows = table.shape[0]
+        ctx.save_for_backward(table if red in (nat.MAX, nat.MIN) else None)
+        return _aggregate_raw(g, table, red, weighted, by_edge, epilogue, bias, xroot, gin_scale, exact)
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        (table,) = ctx.saved_tensors
+        g_table = g_bias = g_xroot = None
+        if ctx.needs_input_grad[0]:
+            g_table = _reduce_backward(ctx.g, ctx.red, ctx.weighted, ctx.by_edge, table, grad_out, ctx.exact,
+                                       ctx.table_rows)
+        if ctx.needs_input_grad[1] and ctx.epilogue == nat.EPI_BIAS:
+            g_bias = grad_out.sum(0)
+        if ctx.needs_input_grad[2] and ctx.epilogue == nat.EPI_GIN:
+            g_xroot = grad_out * ctx.gin_scale
+        return g_table, g_bias, g_xroot, None, None, None, None, None, None, None
+
+
 def aggregate(
     g: CSRGraph,
     table: torch.Tensor,
@@ -295,16 +411,88 @@ def aggregate(
     by_edge=False gathers node rows through `col` (the fused propagate path);
     by_edge=True gathers rows of a per-edge message tensor through `eid`
     (the reference's Aggregator.aggregate(messages, target_idx, dim_size)).
+    Differentiable in table, bias and xroot (sum, mean, max, min).
     """
-    red = nat.REDUCE_IDS[reduce] if isinstance(reduce, str) else int(reduce)
-    items, _, split, _, n_slots = g.work(exact or red == nat.STD)
-    idx = g.eid if by_edge else g.col
+    red = _reduce_id(reduce)
+    if _needs_grad(table, bias, xroot):
+        return _AggregateFn.apply(table, bias, xroot, g, red, weighted, by_edge, epilogue, float(gin_scale), exact)
+    return _aggregate_raw(g, table, red, weighted, by_edge, epilogue, bias, xroot, gin_scale, exact)
+
+
+def _aggregate_transform_raw(g, x, W, red, weighted, bias, pre_gin, gin_scale, exact):
+    items, _, split, _, n_slots = g.work(exact)
     w = g.w if weighted else None
     if weighted and w is None:
         raise ValueError("graph was built without GCN normalisation weights")
-    return _timed(lambda: torch.ops.kgx.spmm(
-        table, g.rowptr, g.rows, items, split, idx, w, n_slots, red, epilogue, bias, xroot, float(gin_scale)
+    return _timed(lambda: torch.ops.kgx.spmm_gemm(
+        x, g.rowptr, g.rows, items, split, g.col, w, n_slots, red, W, bias, bool(pre_gin), float(gin_scale)
     ))
+
+
+def _gemm_tn_tall(P: torch.Tensor, D: torch.Tensor, chunks: int = 512) -> torch.Tensor:
+    """P^T @ D for tall-skinny P [K, m], D [K, n] (K = number of nodes): split-K
+    as a batched GEMM over row chunks plus one sum, so every CU gets work
+    (a single GEMM with M = N = 128 and K = 10M runs on a handful of tiles)."""
+    K = P.shape[0]
+    if K < 8 * chunks:
+        return P.t() @ D
+    kc = K // chunks
+    main = kc * chunks
+    out = torch.bmm(P[:main].view(chunks, kc, P.shape[1]).transpose(1, 2), D[:main].view(chunks, kc, D.shape[1]))
+    out = out.sum(0)
+    if main < K:
+        out = out + P[main:].t() @ D[main:]
+    return out
+
+
+class _AggregateTransformFn(torch.autograd.Function):
+    """out = bias + PRE(A x) W.  Backward: P = PRE(A x) is recomputed (one
+    aggregation launch) rather than kept from the forward; dW = P^T dOut,
+    db = sum dOut, dx = A^T-backward(dOut W^T) (+ gin_scale dOut W^T)."""
+
+    @staticmethod
+    def forward(ctx, x, W, bias, g, red, weighted, pre_gin, gin_scale, exact):
+        ctx.g, ctx.red, ctx.weighted, ctx.pre_gin, ctx.gin_scale, ctx.exact = g, red, weighted, pre_gin, gin_scale, exact
+        items, _, split, _, n_slots = g.work(exact)
+        w = g.w if weighted else None
+        if ctx.needs_input_grad[1]:  # keep P = PRE(A x) for dW (one extra row store instead of a recompute)
+            out, P = _timed(lambda: torch.ops.kgx.spmm_gemm_save(
+                x, g.rowptr, g.rows, items, split, g.col, w, n_slots, red, W, bias, bool(pre_gin), float(gin_scale)))
+        else:
+            out = _aggregate_transform_raw(g, x, W, red, weighted, bias, pre_gin, gin_scale, exact)
+            P = None
+        ctx.save_for_backward(x if red in (nat.MAX, nat.MIN) else None, W, P)
+        ctx.x_rows = x.shape[0]
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        from . import graph as G
+
+        x, W, P = ctx.saved_tensors
+        grad_out = grad_out.contiguous()
+        g_x = g_W = g_b = None
+        if ctx.needs_input_grad[1]:
+            g_W = _gemm_tn_tall(P, grad_out)
+        if ctx.needs_input_grad[2]:
+            g_b = grad_out.sum(0)
+        if ctx.needs_input_grad[0]:
+            f_out, f_in = W.shape[1], W.shape[0]
+            if ctx.red in (nat.SUM, nat.MEAN) and not ctx.pre_gin and fused_transform_supported(f_out, f_in):
+                # dx = A^T (dOut W^T) = (A^T dOut) W^T: the same fused kernel on the transposed graph
+                d = grad_out
+                if ctx.red == nat.MEAN:
+                    count = torch.clamp(ctx.g.deg, max=1 << 24).float()
+                    d = (grad_out / torch.clamp(count, min=1e-8).unsqueeze(1)).contiguous()
+                t = G.transpose(ctx.g)
+                g_x = _aggregate_transform_raw(t, d, W.t().contiguous(), nat.SUM, ctx.weighted, None, False, 1.0,
+                                               ctx.exact)
+            else:
+                dP = grad_out @ W.t()
+                g_x = _reduce_backward(ctx.g, ctx.red, ctx.weighted, False, x, dP, ctx.exact, ctx.x_rows)
+                if ctx.pre_gin:
+                    g_x = g_x + dP * ctx.gin_scale
+        return g_x, g_W, g_b, None, None, None, None, None, None
 
 
 def aggregate_transform(
@@ -321,21 +509,21 @@ def aggregate_transform(
     out: torch.Tensor | None = None,
 ) -> torch.Tensor:
     """out = bias + PRE(REDUCE_{e in row} x[col_e] * w_e) @ W in one fused launch
-    (out += ... in place when `out` is given)."""
-    red = nat.REDUCE_IDS[reduce] if isinstance(reduce, str) else int(reduce)
-    items, _, split, _, n_slots = g.work(exact)
-    w = g.w if weighted else None
-    if weighted and w is None:
-        raise ValueError("graph was built without GCN normalisation weights")
+    (out += ... in place when `out` is given).  Differentiable in x, W, bias."""
+    red = _reduce_id(reduce)
     if out is not None:  # accumulate into `out` (sum only: the caller splits a row's edges)
         if pre_gin or red != nat.SUM:
             raise ValueError("aggregate_transform(out=...) accumulates plain sums only")
+        if _needs_grad(x, W, bias, out):
+            raise NotImplementedError("aggregate_transform(out=...) is a forward-only (no_grad) path")
+        items, _, split, _, n_slots = g.work(exact)
+        w = g.w if weighted else None
         _timed(lambda: torch.ops.kgx.spmm_gemm_acc_(out, x, g.rowptr, g.rows, items, split, g.col, w, n_slots, red,
                                                    W, bias))
         return out
-    return _timed(lambda: torch.ops.kgx.spmm_gemm(
-        x, g.rowptr, g.rows, items, split, g.col, w, n_slots, red, W, bias, bool(pre_gin), float(gin_scale)
-    ))
+    if _needs_grad(x, W, bias):
+        return _AggregateTransformFn.apply(x, W, bias, g, red, weighted, pre_gin, float(gin_scale), exact)
+    return _aggregate_transform_raw(g, x, W, red, weighted, bias, pre_gin, gin_scale, exact)
 
 
 def gatv2_aggregate(

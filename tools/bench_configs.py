@@ -103,6 +103,29 @@ def c5(dev):
                 edges_per_s=g.kept / ms * 1e3, alg_GBps=b / agg / 1e6)
 
 
+def ns_train(dev):
+    """NS GCNConv forward + backward (d/dx, d/dW, d/db): one training step's
+    propagate work (fused forward, recompute of A x for dW, dOut W^T GEMM,
+    transposed aggregation for dx)."""
+    n, e, f = 10_000_000, 100_000_000, 128
+    ei = synthetic.rmat_edge_index(n, e, seed=0, device=dev)
+    x = torch.randn(n, f, device=dev, requires_grad=True)
+    layer = kgx.GCNConv(f)
+    layer([x, ei])
+    g = graph(layer)
+    gout = torch.randn(n, f, device=dev)
+    kgx.graph.transpose(g)  # built once per graph, like the forward CSR
+
+    def step():
+        x.grad = None
+        layer.zero_grad(set_to_none=True)
+        layer([x, ei]).backward(gout)
+
+    ms, agg, per = run(step, steps=5)
+    return dict(config="NS GCNConv fwd+bwd 10M/100M F128", step_ms=ms, aggregation_kernels_ms=agg,
+                launches_per_step=per, e_agg=g.kept, edges_per_s=g.kept / ms * 1e3)
+
+
 def c1(dev):
     n, e, fin = 2708, 10556, 1433
     ei = synthetic.rmat_edge_index(n, e, seed=0, device=dev)
@@ -119,7 +142,7 @@ def c1(dev):
 
 if __name__ == "__main__":
     dev = torch.device("cuda", 0)
-    names = sys.argv[1:] or ["c1", "c2", "c3", "c4", "c5"]
+    names = sys.argv[1:] or ["c1", "c2", "c3", "c4", "c5", "ns_train"]
     for name in names:
         r = globals()[name](dev)
         print(json.dumps(r), flush=True)
