@@ -211,6 +211,23 @@ int kgx_gatv2(const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
               float* partials, kgx_stream_t stream);
 
 /* ---------------------------------------------------------------------------
+ * Backward of kgx_gatv2 (autograd of GATv2Conv's propagate, gatv2_conv.py:
+ * 241-352): given G = d loss / d out, writes d h_src (pulled over the
+ * TRANSPOSED graph: t_rowptr over sources, t_col = destination row, t_slot =
+ * forward CSR slot of every transposed slot), d h_dst, and ADDS d att
+ * (grad_att must be zeroed by the caller).  alpha_ws / ds_ws: E' * heads
+ * floats of workspace (per-edge attention and score gradients).  The bias
+ * gradient is a column sum the caller takes.  Whole rows, no hub split.
+ * ------------------------------------------------------------------------- */
+int kgx_gatv2_backward(const int32_t* rowptr, const int32_t* rows, int64_t n_rows, const int32_t* col,
+                       const float* h_src, const float* h_dst, int64_t ld_h, const float* att,
+                       int heads, int channels, float negative_slope,
+                       const float* grad_out, int64_t ld_grad,
+                       const int32_t* t_rowptr, int64_t n_src, const int32_t* t_col, const int32_t* t_slot,
+                       float* grad_h_src, float* grad_h_dst, int64_t ld_grad_h, float* grad_att,
+                       float* alpha_ws, float* ds_ws, kgx_stream_t stream);
+
+/* ---------------------------------------------------------------------------
  * Row gather out[i,:] = table[rows[i], :] — packs halo rows for the multi-GPU
  * exchange (no reference counterpart; the reference is single-device) and
  * scatters per-edge values back to input edge order.

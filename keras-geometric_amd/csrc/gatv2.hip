@@ -308,3 +308,269 @@ extern "C" int kgx_gatv2(const int32_t* rowptr, const int32_t* rows, int64_t n_r
     default: return launch<16>(a, stream);
   }
 }
+
+// ===========================================================================
+// Backward (kgx_gatv2_backward).  Forward per destination row i, head h:
+//   z_e = h_dst[i] + h_src[j_e];  s_e = sum_c att[c] lrelu(z_e[c]);
+//   alpha_e = exp(s_e - m) / (sum_e' exp(s_e' - m) + 1e-10);
+//   out_i = sum_e alpha_e h_src[j_e]  (+ bias)
+// With G = d loss / d out (the max shift m carries a ~1e-10-relative term
+// through the 1e-10 guard, ignored):
+//   dalpha_e = <G_i, h_src[j_e]>_head;  ds_e = alpha_e (dalpha_e - sum_e' alpha_e' dalpha_e')
+//   dz_e[c]  = ds_e att[c] lrelu'(z_e[c])          (lrelu'(0) = slope, as torch)
+//   d att[c] = sum_e ds_e lrelu(z_e[c]);  d h_dst[i] = sum_e dz_e
+//   d h_src[j] = sum_{e: j_e = j} (alpha_e G_i + dz_e)
+// Kernel A walks the destination CSR (three passes over a row's edges:
+// softmax statistics; the row sum of alpha * dalpha; then alpha, dalpha, ds,
+// dz and the row's d h_dst / d att), storing alpha and ds per (edge, head).  Kernel B
+// walks the TRANSPOSED CSR and pulls d h_src (no atomics).  Rows are taken
+// whole (no hub split) -- this is the training path, not the north star.
+// ===========================================================================
+
+namespace kgx {
+namespace {
+
+struct GatBwdArgs {
+  const int32_t* rowptr;
+  const int32_t* rows;
+  int64_t n_rows;
+  const int32_t* col;
+  const float* h_src;
+  const float* h_dst;
+  int64_t ld_h;
+  const float* att;
+  int H, C;
+  float slope;
+  const float* grad;
+  int64_t ld_g;
+  float* alpha;  // [E', H] CSR slot order
+  float* ds;     // [E', H]
+  float* grad_h_dst;
+  int64_t ld_gd;
+  float* grad_att;  // [H*C], atomically accumulated
+  // transposed graph (kernel B)
+  const int32_t* t_rowptr;
+  int64_t t_n_rows;
+  const int32_t* t_col;   // destination row of each transposed slot
+  const int32_t* t_slot;  // forward CSR slot of each transposed slot
+  float* grad_h_src;
+  int64_t ld_gs;
+  int G, lgG, LH, lgLH;
+};
+
+template <int K>
+__global__ __launch_bounds__(kBlock) void gatv2_bwd_rows_kernel(GatBwdArgs a) {
+  const int G = a.G;
+  const int lane = threadIdx.x & (G - 1);
+  const int head = lane >> a.lgLH;
+  const int sub = lane & (a.LH - 1);
+  const bool valid = head < a.H && sub * K < a.C;
+  const int f = head * a.C + sub * K;
+  const int64_t ngroups = (int64_t(gridDim.x) * kBlock) >> a.lgG;
+  float att[K], gatt[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    att[k] = 0.0f;
+    gatt[k] = 0.0f;
+  }
+  if (valid) vload<K>(att, a.att + f);
+  auto lrelu = [&](float g) { return g > 0.0f ? g : g * a.slope; };
+  auto score = [&](const float (&hd)[K], const float (&hs)[K]) {
+    float p = 0.0f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) p += lrelu(hd[k] + hs[k]) * att[k];
+    return head_reduce<K>(p, a.LH);
+  };
+  for (int64_t it = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> a.lgG; it < a.n_rows; it += ngroups) {
+    const int32_t row = a.rows ? a.rows[it] : int32_t(it);
+    const int32_t beg = a.rowptr[row], end = a.rowptr[row + 1];
+    float hd[K], gr[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) hd[k] = gr[k] = 0.0f;
+    if (valid) {
+      vload<K>(hd, a.h_dst + int64_t(row) * a.ld_h + f);
+      vload<K>(gr, a.grad + int64_t(row) * a.ld_g + f);
+    }
+    // pass 1: softmax statistics (as the forward: running max, fp64 sum)
+    float m = -__builtin_inff();
+    double l = 0.0;
+    for (int32_t e = beg; e < end; ++e) {
+      float hs[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) hs[k] = 0.0f;
+      if (valid) vload<K>(hs, a.h_src + int64_t(a.col[e]) * a.ld_h + f);
+      const float s = score(hd, hs);
+      const float mn = fmaxf(m, s);
+      l = l * double(expf(m - mn)) + double(expf(s - mn));
+      m = mn;
+    }
+    const double den = l + 1e-10;
+    // pass 2: alpha, dalpha and sum alpha*dalpha
+    double tsum = 0.0;
+    for (int32_t e = beg; e < end; ++e) {
+      float hs[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) hs[k] = 0.0f;
+      if (valid) vload<K>(hs, a.h_src + int64_t(a.col[e]) * a.ld_h + f);
+      const float s = score(hd, hs);
+      const float al = float(double(expf(s - m)) / den);
+      float p = 0.0f;
+#pragma unroll
+      for (int k = 0; k < K; ++k) p += gr[k] * hs[k];
+      const float da = head_reduce<K>(p, a.LH);
+      tsum += double(al) * double(da);
+    }
+    // pass 3: ds, dz -> d h_dst, d att
+    float gd[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) gd[k] = 0.0f;
+    for (int32_t e = beg; e < end; ++e) {
+      float hs[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) hs[k] = 0.0f;
+      if (valid) vload<K>(hs, a.h_src + int64_t(a.col[e]) * a.ld_h + f);
+      const float al = float(double(expf(score(hd, hs) - m)) / den);
+      float p = 0.0f;
+#pragma unroll
+      for (int k = 0; k < K; ++k) p += gr[k] * hs[k];
+      const float da = head_reduce<K>(p, a.LH);
+      const float dsv = float(double(al) * (double(da) - tsum));
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const float g = hd[k] + hs[k];
+        gd[k] += dsv * att[k] * (g > 0.0f ? 1.0f : a.slope);
+        gatt[k] += dsv * lrelu(g);
+      }
+      if (valid && sub == 0) {
+        a.alpha[int64_t(e) * a.H + head] = al;
+        a.ds[int64_t(e) * a.H + head] = dsv;
+      }
+    }
+    if (valid) vstore<K>(a.grad_h_dst + int64_t(row) * a.ld_gd + f, gd);
+  }
+  if (valid) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) atomicAdd(a.grad_att + f + k, gatt[k]);
+  }
+}
+
+template <int K>
+__global__ __launch_bounds__(kBlock) void gatv2_bwd_src_kernel(GatBwdArgs a) {
+  const int G = a.G;
+  const int lane = threadIdx.x & (G - 1);
+  const int head = lane >> a.lgLH;
+  const int sub = lane & (a.LH - 1);
+  const bool valid = head < a.H && sub * K < a.C;
+  const int f = head * a.C + sub * K;
+  const int64_t ngroups = (int64_t(gridDim.x) * kBlock) >> a.lgG;
+  if (!valid) return;  // no cross-lane work in this kernel
+  float att[K];
+  vload<K>(att, a.att + f);
+  for (int64_t j = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> a.lgG; j < a.t_n_rows; j += ngroups) {
+    float hs[K], acc[K];
+    vload<K>(hs, a.h_src + j * a.ld_h + f);
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = 0.0f;
+    const int32_t beg = a.t_rowptr[j], end = a.t_rowptr[j + 1];
+    for (int32_t e = beg; e < end; ++e) {
+      const int64_t i = a.t_col[e];
+      const int64_t s = a.t_slot[e];
+      const float al = a.alpha[s * a.H + head];
+      const float dsv = a.ds[s * a.H + head];
+      float gr[K], hd[K];
+      vload<K>(gr, a.grad + i * a.ld_g + f);
+      vload<K>(hd, a.h_dst + i * a.ld_h + f);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const float g = hd[k] + hs[k];
+        acc[k] += al * gr[k] + dsv * att[k] * (g > 0.0f ? 1.0f : a.slope);
+      }
+    }
+    vstore<K>(a.grad_h_src + j * a.ld_gs + f, acc);
+  }
+}
+
+template <int K>
+int launch_bwd(const GatBwdArgs& a, hipStream_t s) {
+  if (a.n_rows > 0) {
+    auto k = gatv2_bwd_rows_kernel<K>;
+    hipLaunchKernelGGL(k, dim3(resident_grid(k, a.n_rows, a.G)), dim3(kBlock), 0, s, a);
+    KGX_CHECK_LAUNCH();
+  }
+  if (a.t_n_rows > 0) {
+    auto k = gatv2_bwd_src_kernel<K>;
+    hipLaunchKernelGGL(k, dim3(resident_grid(k, a.t_n_rows, a.G)), dim3(kBlock), 0, s, a);
+    KGX_CHECK_LAUNCH();
+  }
+  return KGX_OK;
+}
+
+}  // namespace
+}  // namespace kgx
+
+extern "C" int kgx_gatv2_backward(const int32_t* rowptr, const int32_t* rows, int64_t n_rows, const int32_t* col,
+                                  const float* h_src, const float* h_dst, int64_t ld_h, const float* att, int heads,
+                                  int channels, float negative_slope, const float* grad_out, int64_t ld_grad,
+                                  const int32_t* t_rowptr, int64_t n_src, const int32_t* t_col,
+                                  const int32_t* t_slot, float* grad_h_src, float* grad_h_dst,
+                                  int64_t ld_grad_h, float* grad_att, float* alpha_ws, float* ds_ws,
+                                  kgx_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  KGX_REQUIRE(heads > 0 && channels > 0 && n_rows >= 0 && n_src >= 0, KGX_ERR_ARG, "kgx_gatv2_backward: bad sizes");
+  const int64_t HC = int64_t(heads) * channels;
+  KGX_REQUIRE(rowptr && col && h_src && h_dst && att && grad_out && t_rowptr && grad_h_src && grad_h_dst &&
+                  grad_att && alpha_ws && ds_ws,
+              KGX_ERR_ARG, "kgx_gatv2_backward: null pointer");
+  KGX_REQUIRE(ld_h >= HC && ld_grad >= HC && ld_grad_h >= HC, KGX_ERR_ARG,
+              "kgx_gatv2_backward: leading dimension < heads*channels");
+  // K channels per lane: the smallest K (dividing C, with aligned vector
+  // accesses) that fits one row's heads into a 64-lane group
+  auto al = [](const void* p, int b) { return p == nullptr || reinterpret_cast<uintptr_t>(p) % b == 0; };
+  int K = 0;
+  for (int k = 1; k <= 16 && !K; k <<= 1) {
+    const int va = 4 * (k < 4 ? k : 4);  // byte alignment vload<k> needs
+    if (channels % k || ld_h % (va / 4) || ld_grad % (va / 4) || ld_grad_h % (va / 4)) continue;
+    if (!al(h_src, va) || !al(h_dst, va) || !al(att, va) || !al(grad_out, va) || !al(grad_h_src, va) ||
+        !al(grad_h_dst, va))
+      continue;
+    if (heads * next_pow2(channels / k) <= 64) K = k;
+  }
+  KGX_REQUIRE(K > 0, KGX_ERR_UNSUPPORTED,
+              "kgx_gatv2_backward: heads=%d x channels=%d does not fit 64 lanes per row", heads, channels);
+  GatBwdArgs a{};
+  a.rowptr = rowptr;
+  a.rows = rows;
+  a.n_rows = n_rows;
+  a.col = col;
+  a.h_src = h_src;
+  a.h_dst = h_dst;
+  a.ld_h = ld_h;
+  a.att = att;
+  a.H = heads;
+  a.C = channels;
+  a.slope = negative_slope;
+  a.grad = grad_out;
+  a.ld_g = ld_grad;
+  a.alpha = alpha_ws;
+  a.ds = ds_ws;
+  a.grad_h_dst = grad_h_dst;
+  a.ld_gd = ld_grad_h;
+  a.grad_att = grad_att;
+  a.t_rowptr = t_rowptr;
+  a.t_n_rows = n_src;
+  a.t_col = t_col;
+  a.t_slot = t_slot;
+  a.grad_h_src = grad_h_src;
+  a.ld_gs = ld_grad_h;
+  a.LH = next_pow2(channels / K);
+  a.lgLH = log2i(a.LH);
+  a.G = next_pow2(heads * a.LH);
+  a.lgG = log2i(a.G);
+  switch (K) {
+    case 1: return launch_bwd<1>(a, stream);
+    case 2: return launch_bwd<2>(a, stream);
+    case 4: return launch_bwd<4>(a, stream);
+    case 8: return launch_bwd<8>(a, stream);
+    default: return launch_bwd<16>(a, stream);
+  }
+}

@@ -526,6 +526,55 @@ def aggregate_transform(
     return _aggregate_transform_raw(g, x, W, red, weighted, bias, pre_gin, gin_scale, exact)
 
 
+def _gatv2_raw(g, h_src, h_dst, att, heads, channels, negative_slope, bias, exact):
+    items, _, split, _, n_slots = g.work(exact)
+    return _timed(lambda: torch.ops.kgx.gatv2(
+        h_src, h_dst, g.rowptr, g.rows, items, split, g.col, att.reshape(-1), heads, channels,
+        float(negative_slope), bias, n_slots,
+    ))
+
+
+class _GATv2Fn(torch.autograd.Function):
+    """Autograd of the fused GATv2 aggregation: kgx_gatv2_backward (softmax
+    backward over the destination CSR, d h_src pulled over the transposed CSR)."""
+
+    @staticmethod
+    def forward(ctx, h_src, h_dst, att, bias, g, heads, channels, negative_slope, exact):
+        ctx.g, ctx.heads, ctx.channels, ctx.slope = g, heads, channels, float(negative_slope)
+        ctx.same = h_src is h_dst
+        ctx.save_for_backward(h_src, h_dst, att)
+        return _gatv2_raw(g, h_src, h_dst, att, heads, channels, negative_slope, bias, exact)
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        from . import graph as G
+
+        h_src, h_dst, att = ctx.saved_tensors
+        g, H, C = ctx.g, ctx.heads, ctx.channels
+        grad_out = grad_out.contiguous()
+        h_src, h_dst = h_src.contiguous(), h_dst.contiguous()
+        att_flat = att.reshape(-1).contiguous()
+        t = G.transpose(g)
+        dev = grad_out.device
+        g_src = torch.empty((g.n_src, H * C), dtype=torch.float32, device=dev)
+        g_dst = torch.empty((g.n_dst, H * C), dtype=torch.float32, device=dev)
+        g_att = torch.zeros(H * C, dtype=torch.float32, device=dev)
+        alpha = torch.empty((max(g.kept, 1), H), dtype=torch.float32, device=dev)
+        ds = torch.empty_like(alpha)
+        slot = t.extras["fwd_slot"].to(torch.int32)
+        nat.check(
+            nat.lib().kgx_gatv2_backward(
+                nat.ptr(g.rowptr), nat.ptr(g.rows), g.n_dst, nat.ptr(g.col), nat.ptr(h_src), nat.ptr(h_dst),
+                h_src.stride(0), nat.ptr(att_flat), H, C, ctx.slope, nat.ptr(grad_out), grad_out.stride(0),
+                nat.ptr(t.rowptr), g.n_src, nat.ptr(t.col), nat.ptr(slot), nat.ptr(g_src), nat.ptr(g_dst),
+                g_src.stride(0), nat.ptr(g_att), nat.ptr(alpha), nat.ptr(ds), nat.stream(dev),
+            ),
+            "kgx_gatv2_backward",
+        )
+        g_bias = grad_out.sum(0) if ctx.needs_input_grad[3] else None
+        return g_src, g_dst, g_att.view(att.shape), g_bias, None, None, None, None, None
+
+
 def gatv2_aggregate(
     g: CSRGraph,
     h_src: torch.Tensor,
@@ -537,8 +586,7 @@ def gatv2_aggregate(
     bias: torch.Tensor | None = None,
     exact: bool = False,
 ) -> torch.Tensor:
-    items, _, split, _, n_slots = g.work(exact)
-    return _timed(lambda: torch.ops.kgx.gatv2(
-        h_src, h_dst, g.rowptr, g.rows, items, split, g.col, att.reshape(-1), heads, channels,
-        float(negative_slope), bias, n_slots,
-    ))
+    """Fused GATv2 attention aggregation; differentiable in h_src, h_dst, att, bias."""
+    if _needs_grad(h_src, h_dst, att, bias):
+        return _GATv2Fn.apply(h_src, h_dst, att, bias, g, heads, channels, negative_slope, exact)
+    return _gatv2_raw(g, h_src, h_dst, att, heads, channels, negative_slope, bias, exact)

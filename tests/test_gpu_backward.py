@@ -222,3 +222,33 @@ def test_std_backward_raises(dev):
     y = kops.aggregate(g, xd, "std")
     with pytest.raises(NotImplementedError):
         y.sum().backward()
+
+
+@pytest.mark.parametrize("heads,C,concat", [(8, 16, True), (2, 5, True), (4, 8, False)])
+def test_gatv2_layer_backward(dev, heads, C, concat):
+    """GATv2Conv: d/dx, d/d kernel, d/d att, d/d bias through kgx_gatv2_backward
+    vs autograd through the reference forward (segment softmax included)."""
+    from keras_geometric_amd.layers import GATv2Conv
+
+    N, Fi = 900, 24
+    ei = _graph(N, 8000, seed=24)
+    x = _x(N, Fi, 25)
+    out_dim = heads * C if concat else C
+    gout = _x(N, out_dim, 26)
+    layer = GATv2Conv(C, heads=heads, concat=concat, exact=True)
+    xd = T(x).to(dev).requires_grad_(True)
+    layer([xd, T(ei).to(dev)])
+    with torch.no_grad():  # non-trivial bias
+        layer.bias.copy_(T(_x(1, out_dim, 27)[0]))
+    kern, att, bias = (t.detach().cpu() for t in (layer.linear_transform.kernel, layer.att, layer.bias))
+    y = layer([xd, T(ei).to(dev)])
+    y.backward(T(gout).to(dev))
+    xr = T(x).requires_grad_(True)
+    kr, ar, br = (t.clone().requires_grad_(True) for t in (kern, att, bias))
+    yr = R.gatv2_forward(xr, T(ei), kr, ar, br, heads=heads, concat=concat)
+    yr.backward(T(gout))
+    assert_tol(y, yr)
+    assert_tol(xd.grad, xr.grad)
+    assert_tol(layer.att.grad, ar.grad, tol=1e-5 * np.sqrt(N))
+    assert_tol(layer.bias.grad, br.grad, tol=1e-5 * np.sqrt(N))
+    assert_tol(layer.linear_transform.kernel.grad, kr.grad, tol=1e-5 * np.sqrt(N))

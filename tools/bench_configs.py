@@ -126,6 +126,27 @@ def ns_train(dev):
                 launches_per_step=per, e_agg=g.kept, edges_per_s=g.kept / ms * 1e3)
 
 
+def c3_train(dev):
+    """C3 GATv2 forward + backward (d/dx, d/dW, d/d att, d/d bias)."""
+    n, e, H, C, fin = 1_000_000, 10_000_000, 8, 16, 128
+    ei = synthetic.rmat_edge_index(n, e, seed=0, device=dev)
+    x = torch.randn(n, fin, device=dev, requires_grad=True)
+    layer = kgx.GATv2Conv(C, heads=H)
+    layer([x, ei])
+    g = graph(layer)
+    gout = torch.randn(n, H * C, device=dev)
+    kgx.graph.transpose(g)
+
+    def step():
+        x.grad = None
+        layer.zero_grad(set_to_none=True)
+        layer([x, ei]).backward(gout)
+
+    ms, agg, per = run(step, steps=5)
+    return dict(config="C3 GATv2 fwd+bwd 1M/10M H8xC16", step_ms=ms, forward_kernel_ms=agg, e_agg=g.kept,
+                edges_per_s=g.kept / ms * 1e3)
+
+
 def c1(dev):
     n, e, fin = 2708, 10556, 1433
     ei = synthetic.rmat_edge_index(n, e, seed=0, device=dev)
@@ -142,7 +163,7 @@ def c1(dev):
 
 if __name__ == "__main__":
     dev = torch.device("cuda", 0)
-    names = sys.argv[1:] or ["c1", "c2", "c3", "c4", "c5", "ns_train"]
+    names = sys.argv[1:] or ["c1", "c2", "c3", "c4", "c5", "ns_train", "c3_train"]
     for name in names:
         r = globals()[name](dev)
         print(json.dumps(r), flush=True)
