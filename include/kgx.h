@@ -201,6 +201,8 @@ int kgx_spmm_max_backward(int reduce, const int32_t* rowptr, int64_t n_rows, con
  *   _final_update (gatv2_conv.py:241-266, 268-311, 313-335, 337-352).
  * h_src/h_dst: [n, heads*channels] row-major with leading dimension ld_h.
  * partials: n_slots * (heads*channels + 2*heads) floats when items are split.
+ * stats (optional, [n, 2*heads]): per row and head the softmax max and
+ * denominator (sum + 1e-10), kept for kgx_gatv2_backward.
  * ------------------------------------------------------------------------- */
 int kgx_gatv2(const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
               const int32_t* items, int64_t n_items,
@@ -208,24 +210,32 @@ int kgx_gatv2(const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
               const int32_t* col, const float* h_src, const float* h_dst, int64_t ld_h,
               const float* att, int heads, int channels, float negative_slope,
               float* out, int64_t ld_out, const float* bias,
-              float* partials, kgx_stream_t stream);
+              float* partials, float* stats, kgx_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Backward of kgx_gatv2 (autograd of GATv2Conv's propagate, gatv2_conv.py:
- * 241-352): given G = d loss / d out, writes d h_src (pulled over the
- * TRANSPOSED graph: t_rowptr over sources, t_col = destination row, t_slot =
- * forward CSR slot of every transposed slot), d h_dst, and ADDS d att
- * (grad_att must be zeroed by the caller).  alpha_ws / ds_ws: E' * heads
- * floats of workspace (per-edge attention and score gradients).  The bias
- * gradient is a column sum the caller takes.  Whole rows, no hub split.
+ * 241-352).  Needs the forward's output `out` (bias included when bias is
+ * given) and its per-row softmax `stats` ([n, 2*heads]: max, denominator;
+ * kgx_gatv2's optional last output).  Given G = d loss / d out, writes
+ * d h_dst (destination CSR + its schedule; split rows via partials), d h_src
+ * (pulled over the TRANSPOSED graph: t_rowptr/t_rows/t_items/t_split over
+ * sources, t_col = destination row, t_slot = forward CSR slot of each
+ * transposed slot), and ADDS d att (grad_att zeroed by the caller).
+ * alpha_ws / ds_ws: E' * heads floats of workspace; partials:
+ * max(n_slots, t_n_slots) * heads*channels floats.  The bias gradient is a
+ * column sum the caller takes.
  * ------------------------------------------------------------------------- */
-int kgx_gatv2_backward(const int32_t* rowptr, const int32_t* rows, int64_t n_rows, const int32_t* col,
-                       const float* h_src, const float* h_dst, int64_t ld_h, const float* att,
-                       int heads, int channels, float negative_slope,
+int kgx_gatv2_backward(const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
+                       const int32_t* items, int64_t n_items, const int32_t* split, int64_t n_split,
+                       const int32_t* col, const float* h_src, const float* h_dst, int64_t ld_h,
+                       const float* att, int heads, int channels, float negative_slope,
+                       const float* out, int64_t ld_out, const float* bias, const float* stats,
                        const float* grad_out, int64_t ld_grad,
-                       const int32_t* t_rowptr, int64_t n_src, const int32_t* t_col, const int32_t* t_slot,
+                       const int32_t* t_rowptr, const int32_t* t_rows, int64_t n_src,
+                       const int32_t* t_items, int64_t t_n_items, const int32_t* t_split, int64_t t_n_split,
+                       const int32_t* t_col, const int32_t* t_slot,
                        float* grad_h_src, float* grad_h_dst, int64_t ld_grad_h, float* grad_att,
-                       float* alpha_ws, float* ds_ws, kgx_stream_t stream);
+                       float* alpha_ws, float* ds_ws, float* partials, kgx_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Row gather out[i,:] = table[rows[i], :] — packs halo rows for the multi-GPU

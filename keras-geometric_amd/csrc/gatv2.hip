@@ -42,6 +42,7 @@ struct GatArgs {
   int64_t ld_o;
   const float* bias;
   float* partials;  // per slot: [H*C acc | H m | H l]
+  float* stats;     // optional [n, 2H]: per row and head, the softmax max m and denominator l + 1e-10
   int G, lgG, LH, lgLH;
 };
 
@@ -156,6 +157,10 @@ __global__ __launch_bounds__(kBlock) void gatv2_kernel(GatArgs a) {
       }
     } else {
       const double den = l + 1e-10;
+      if (a.stats && sub == 0) {
+        a.stats[int64_t(row) * 2 * a.H + head] = m;
+        a.stats[int64_t(row) * 2 * a.H + a.H + head] = float(den);
+      }
       float r[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) r[k] = float(acc[k] / den);
@@ -200,6 +205,10 @@ __global__ __launch_bounds__(kBlock) void gatv2_fixup_kernel(GatArgs a) {
       for (int k = 0; k < K; ++k) acc[k] += double(v[k]) * sc;
     }
     const double den = L + 1e-10;
+    if (a.stats && sub == 0) {
+      a.stats[int64_t(row) * 2 * a.H + head] = M;
+      a.stats[int64_t(row) * 2 * a.H + a.H + head] = float(den);
+    }
     float r[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) r[k] = float(acc[k] / den);
@@ -240,7 +249,7 @@ extern "C" int kgx_gatv2(const int32_t* rowptr, const int32_t* rows, int64_t n_r
                          int64_t n_items, const int32_t* split, int64_t n_split, const int32_t* col,
                          const float* h_src, const float* h_dst, int64_t ld_h, const float* att, int heads,
                          int channels, float negative_slope, float* out, int64_t ld_out, const float* bias,
-                         float* partials, kgx_stream_t stream_) {
+                         float* partials, float* stats, kgx_stream_t stream_) {
   hipStream_t stream = as_stream(stream_);
   KGX_REQUIRE(heads > 0 && channels > 0 && n_rows >= 0 && n_items >= 0 && n_split >= 0, KGX_ERR_ARG,
               "kgx_gatv2: bad sizes");
@@ -296,6 +305,7 @@ extern "C" int kgx_gatv2(const int32_t* rowptr, const int32_t* rows, int64_t n_r
   a.ld_o = ld_out;
   a.bias = bias;
   a.partials = partials;
+  a.stats = stats;
   a.LH = next_pow2((channels + K - 1) / K);
   a.lgLH = log2i(a.LH);
   a.G = next_pow2(heads * a.LH);
@@ -316,24 +326,31 @@ extern "C" int kgx_gatv2(const int32_t* rowptr, const int32_t* rows, int64_t n_r
 //   out_i = sum_e alpha_e h_src[j_e]  (+ bias)
 // With G = d loss / d out (the max shift m carries a ~1e-10-relative term
 // through the 1e-10 guard, ignored):
-//   dalpha_e = <G_i, h_src[j_e]>_head;  ds_e = alpha_e (dalpha_e - sum_e' alpha_e' dalpha_e')
+//   dalpha_e = <G_i, h_src[j_e]>_h;  ds_e = alpha_e (dalpha_e - D_i)
+//   D_i      = sum_e alpha_e dalpha_e = <G_i, out_i - bias>_h   (no pass over edges)
 //   dz_e[c]  = ds_e att[c] lrelu'(z_e[c])          (lrelu'(0) = slope, as torch)
 //   d att[c] = sum_e ds_e lrelu(z_e[c]);  d h_dst[i] = sum_e dz_e
 //   d h_src[j] = sum_{e: j_e = j} (alpha_e G_i + dz_e)
-// Kernel A walks the destination CSR (three passes over a row's edges:
-// softmax statistics; the row sum of alpha * dalpha; then alpha, dalpha, ds,
-// dz and the row's d h_dst / d att), storing alpha and ds per (edge, head).  Kernel B
-// walks the TRANSPOSED CSR and pulls d h_src (no atomics).  Rows are taken
-// whole (no hub split) -- this is the training path, not the north star.
+// The forward keeps (m, denominator) per row and head (kgx_gatv2 `stats`), so
+// kernel A is ONE pass over a row's edges, and needs only row constants: hub
+// rows are split into the forward's chunks (partial d h_dst rows + fix-up).
+// Kernel A stores alpha and ds per (edge, head); kernel B walks the
+// TRANSPOSED CSR (its own split schedule) and pulls d h_src -- no atomics
+// except the H*C-float d att.
 // ===========================================================================
 
 namespace kgx {
 namespace {
 
 struct GatBwdArgs {
+  // destination CSR + its schedule
   const int32_t* rowptr;
   const int32_t* rows;
   int64_t n_rows;
+  const int4* items;
+  int64_t n_items;
+  const int4* split;
+  int64_t n_split;
   const int32_t* col;
   const float* h_src;
   const float* h_dst;
@@ -341,6 +358,10 @@ struct GatBwdArgs {
   const float* att;
   int H, C;
   float slope;
+  const float* out;  // forward output (bias included if bias != null)
+  int64_t ld_out;
+  const float* bias;
+  const float* stats;  // [n, 2H] from the forward
   const float* grad;
   int64_t ld_g;
   float* alpha;  // [E', H] CSR slot order
@@ -348,9 +369,15 @@ struct GatBwdArgs {
   float* grad_h_dst;
   int64_t ld_gd;
   float* grad_att;  // [H*C], atomically accumulated
-  // transposed graph (kernel B)
+  float* partials;  // [max(n_slots, t_n_slots), H*C]
+  // transposed graph + its schedule (kernel B)
   const int32_t* t_rowptr;
+  const int32_t* t_rows;
   int64_t t_n_rows;
+  const int4* t_items;
+  int64_t t_n_items;
+  const int4* t_split;
+  int64_t t_n_split;
   const int32_t* t_col;   // destination row of each transposed slot
   const int32_t* t_slot;  // forward CSR slot of each transposed slot
   float* grad_h_src;
@@ -359,94 +386,108 @@ struct GatBwdArgs {
 };
 
 template <int K>
+constexpr int bwd_unroll() {
+  return K <= 4 ? 8 : 4;
+}
+
+__device__ __forceinline__ void work_item(const int4* items, const int32_t* rows, const int32_t* rowptr, int64_t it,
+                                          int32_t& row, int32_t& beg, int32_t& end, int32_t& slot) {
+  if (items) {
+    const int4 v = items[it];
+    row = v.x;
+    beg = v.y;
+    end = v.z;
+    slot = v.w;
+  } else {
+    row = rows[it];
+    beg = rowptr[row];
+    end = rowptr[row + 1];
+    slot = -1;
+  }
+}
+
+template <int K>
 __global__ __launch_bounds__(kBlock) void gatv2_bwd_rows_kernel(GatBwdArgs a) {
+  constexpr int U = bwd_unroll<K>();
   const int G = a.G;
   const int lane = threadIdx.x & (G - 1);
   const int head = lane >> a.lgLH;
   const int sub = lane & (a.LH - 1);
   const bool valid = head < a.H && sub * K < a.C;
-  const int f = head * a.C + sub * K;
+  const int f = valid ? head * a.C + sub * K : 0;  // padding lanes read a valid address and use nothing
+  const int HC = a.H * a.C;
   const int64_t ngroups = (int64_t(gridDim.x) * kBlock) >> a.lgG;
+  const int64_t n_work = a.items ? a.n_items : a.n_rows;
   float att[K], gatt[K];
+  vload<K>(att, a.att + f);
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    att[k] = 0.0f;
     gatt[k] = 0.0f;
+    if (!valid) att[k] = 0.0f;
   }
-  if (valid) vload<K>(att, a.att + f);
   auto lrelu = [&](float g) { return g > 0.0f ? g : g * a.slope; };
-  auto score = [&](const float (&hd)[K], const float (&hs)[K]) {
-    float p = 0.0f;
+  for (int64_t it = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> a.lgG; it < n_work; it += ngroups) {
+    int32_t row, beg, end, slot;
+    work_item(a.items, a.rows, a.rowptr, it, row, beg, end, slot);
+    float hd[K], gr[K], o[K];
+    vload<K>(hd, a.h_dst + int64_t(row) * a.ld_h + f);
+    vload<K>(gr, a.grad + int64_t(row) * a.ld_g + f);
+    vload<K>(o, a.out + int64_t(row) * a.ld_out + f);
+    if (a.bias) {
+      float b[K];
+      vload<K>(b, a.bias + f);
 #pragma unroll
-    for (int k = 0; k < K; ++k) p += lrelu(hd[k] + hs[k]) * att[k];
-    return head_reduce<K>(p, a.LH);
-  };
-  for (int64_t it = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> a.lgG; it < a.n_rows; it += ngroups) {
-    const int32_t row = a.rows ? a.rows[it] : int32_t(it);
-    const int32_t beg = a.rowptr[row], end = a.rowptr[row + 1];
-    float hd[K], gr[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) hd[k] = gr[k] = 0.0f;
-    if (valid) {
-      vload<K>(hd, a.h_dst + int64_t(row) * a.ld_h + f);
-      vload<K>(gr, a.grad + int64_t(row) * a.ld_g + f);
+      for (int k = 0; k < K; ++k) o[k] -= b[k];
     }
-    // pass 1: softmax statistics (as the forward: running max, fp64 sum)
-    float m = -__builtin_inff();
-    double l = 0.0;
-    for (int32_t e = beg; e < end; ++e) {
-      float hs[K];
+    if (!valid) {
 #pragma unroll
-      for (int k = 0; k < K; ++k) hs[k] = 0.0f;
-      if (valid) vload<K>(hs, a.h_src + int64_t(a.col[e]) * a.ld_h + f);
-      const float s = score(hd, hs);
-      const float mn = fmaxf(m, s);
-      l = l * double(expf(m - mn)) + double(expf(s - mn));
-      m = mn;
+      for (int k = 0; k < K; ++k) gr[k] = 0.0f;
     }
-    const double den = l + 1e-10;
-    // pass 2: alpha, dalpha and sum alpha*dalpha
-    double tsum = 0.0;
-    for (int32_t e = beg; e < end; ++e) {
-      float hs[K];
+    float dp = 0.0f;
 #pragma unroll
-      for (int k = 0; k < K; ++k) hs[k] = 0.0f;
-      if (valid) vload<K>(hs, a.h_src + int64_t(a.col[e]) * a.ld_h + f);
-      const float s = score(hd, hs);
-      const float al = float(double(expf(s - m)) / den);
-      float p = 0.0f;
-#pragma unroll
-      for (int k = 0; k < K; ++k) p += gr[k] * hs[k];
-      const float da = head_reduce<K>(p, a.LH);
-      tsum += double(al) * double(da);
-    }
-    // pass 3: ds, dz -> d h_dst, d att
+    for (int k = 0; k < K; ++k) dp += gr[k] * o[k];
+    const float D = head_reduce<K>(dp, a.LH);
+    const float m = a.stats[int64_t(row) * 2 * a.H + (valid ? head : 0)];
+    const float den = a.stats[int64_t(row) * 2 * a.H + a.H + (valid ? head : 0)];
     float gd[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) gd[k] = 0.0f;
-    for (int32_t e = beg; e < end; ++e) {
-      float hs[K];
+    for (int32_t e = beg; e < end; e += U) {
+      float hs[U][K];
 #pragma unroll
-      for (int k = 0; k < K; ++k) hs[k] = 0.0f;
-      if (valid) vload<K>(hs, a.h_src + int64_t(a.col[e]) * a.ld_h + f);
-      const float al = float(double(expf(score(hd, hs) - m)) / den);
-      float p = 0.0f;
-#pragma unroll
-      for (int k = 0; k < K; ++k) p += gr[k] * hs[k];
-      const float da = head_reduce<K>(p, a.LH);
-      const float dsv = float(double(al) * (double(da) - tsum));
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const float g = hd[k] + hs[k];
-        gd[k] += dsv * att[k] * (g > 0.0f ? 1.0f : a.slope);
-        gatt[k] += dsv * lrelu(g);
+      for (int u = 0; u < U; ++u) {
+        const int32_t ee = e + u < end ? e + u : end - 1;
+        vload<K>(hs[u], a.h_src + int64_t(a.col[ee]) * a.ld_h + f);
       }
-      if (valid && sub == 0) {
-        a.alpha[int64_t(e) * a.H + head] = al;
-        a.ds[int64_t(e) * a.H + head] = dsv;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        float ps = 0.0f, pa = 0.0f;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          ps += lrelu(hd[k] + hs[u][k]) * att[k];
+          pa += gr[k] * hs[u][k];
+        }
+        const float sc = head_reduce<K>(ps, a.LH);
+        const float da = head_reduce<K>(pa, a.LH);
+        if (e + u < end) {
+          const float al = __fdiv_rn(expf(sc - m), den);
+          const float dsv = al * (da - D);
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            const float g = hd[k] + hs[u][k];
+            gd[k] += dsv * att[k] * (g > 0.0f ? 1.0f : a.slope);
+            gatt[k] += dsv * lrelu(g);
+          }
+          if (valid && sub == 0) {
+            a.alpha[int64_t(e + u) * a.H + head] = al;
+            a.ds[int64_t(e + u) * a.H + head] = dsv;
+          }
+        }
       }
     }
-    if (valid) vstore<K>(a.grad_h_dst + int64_t(row) * a.ld_gd + f, gd);
+    if (!valid) continue;
+    if (slot >= 0) vstore<K>(a.partials + int64_t(slot) * HC + f, gd);
+    else vstore<K>(a.grad_h_dst + int64_t(row) * a.ld_gd + f, gd);
   }
   if (valid) {
 #pragma unroll
@@ -456,50 +497,95 @@ __global__ __launch_bounds__(kBlock) void gatv2_bwd_rows_kernel(GatBwdArgs a) {
 
 template <int K>
 __global__ __launch_bounds__(kBlock) void gatv2_bwd_src_kernel(GatBwdArgs a) {
+  constexpr int U = bwd_unroll<K>();
   const int G = a.G;
   const int lane = threadIdx.x & (G - 1);
   const int head = lane >> a.lgLH;
   const int sub = lane & (a.LH - 1);
   const bool valid = head < a.H && sub * K < a.C;
-  const int f = head * a.C + sub * K;
+  const int HC = a.H * a.C;
   const int64_t ngroups = (int64_t(gridDim.x) * kBlock) >> a.lgG;
+  const int64_t n_work = a.t_items ? a.t_n_items : a.t_n_rows;
   if (!valid) return;  // no cross-lane work in this kernel
+  const int f = head * a.C + sub * K;
   float att[K];
   vload<K>(att, a.att + f);
-  for (int64_t j = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> a.lgG; j < a.t_n_rows; j += ngroups) {
+  for (int64_t it = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> a.lgG; it < n_work; it += ngroups) {
+    int32_t j, beg, end, slot;
+    work_item(a.t_items, a.t_rows, a.t_rowptr, it, j, beg, end, slot);
     float hs[K], acc[K];
-    vload<K>(hs, a.h_src + j * a.ld_h + f);
+    vload<K>(hs, a.h_src + int64_t(j) * a.ld_h + f);
 #pragma unroll
     for (int k = 0; k < K; ++k) acc[k] = 0.0f;
-    const int32_t beg = a.t_rowptr[j], end = a.t_rowptr[j + 1];
-    for (int32_t e = beg; e < end; ++e) {
-      const int64_t i = a.t_col[e];
-      const int64_t s = a.t_slot[e];
-      const float al = a.alpha[s * a.H + head];
-      const float dsv = a.ds[s * a.H + head];
-      float gr[K], hd[K];
-      vload<K>(gr, a.grad + i * a.ld_g + f);
-      vload<K>(hd, a.h_dst + i * a.ld_h + f);
+    for (int32_t e = beg; e < end; e += U) {
+      float gr[U][K], hd[U][K], al[U], dsv[U];
 #pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const float g = hd[k] + hs[k];
-        acc[k] += al * gr[k] + dsv * att[k] * (g > 0.0f ? 1.0f : a.slope);
+      for (int u = 0; u < U; ++u) {
+        const int32_t ee = e + u < end ? e + u : end - 1;
+        const int64_t i = a.t_col[ee];
+        const int64_t s = a.t_slot[ee];
+        al[u] = a.alpha[s * a.H + head];
+        dsv[u] = a.ds[s * a.H + head];
+        vload<K>(gr[u], a.grad + i * a.ld_g + f);
+        vload<K>(hd[u], a.h_dst + i * a.ld_h + f);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (e + u < end) {
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            const float g = hd[u][k] + hs[k];
+            acc[k] += al[u] * gr[u][k] + dsv[u] * att[k] * (g > 0.0f ? 1.0f : a.slope);
+          }
+        }
       }
     }
-    vstore<K>(a.grad_h_src + j * a.ld_gs + f, acc);
+    if (slot >= 0) vstore<K>(a.partials + int64_t(slot) * HC + f, acc);
+    else vstore<K>(a.grad_h_src + int64_t(j) * a.ld_gs + f, acc);
+  }
+}
+
+// Sum the chunk partials of split rows in chunk order into out rows.
+template <int K>
+__global__ __launch_bounds__(kBlock) void gatv2_bwd_fixup_kernel(const int4* __restrict__ split, int64_t n_split,
+                                                                 const float* __restrict__ partials, int HC,
+                                                                 float* __restrict__ out, int64_t ld_out, int G,
+                                                                 int lgG) {
+  const int lane = threadIdx.x & (G - 1);
+  const int64_t ngroups = (int64_t(gridDim.x) * kBlock) >> lgG;
+  for (int64_t it = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> lgG; it < n_split; it += ngroups) {
+    const int4 sp = split[it];
+    for (int f = lane; f < HC; f += G) {
+      float acc = 0.0f;
+      for (int32_t c = 0; c < sp.z; ++c) acc += partials[int64_t(sp.y + c) * HC + f];
+      out[int64_t(sp.x) * ld_out + f] = acc;
+    }
   }
 }
 
 template <int K>
 int launch_bwd(const GatBwdArgs& a, hipStream_t s) {
-  if (a.n_rows > 0) {
+  const int HC = a.H * a.C;
+  const int64_t work = a.items ? a.n_items : a.n_rows;
+  if (work > 0) {
     auto k = gatv2_bwd_rows_kernel<K>;
-    hipLaunchKernelGGL(k, dim3(resident_grid(k, a.n_rows, a.G)), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(k, dim3(resident_grid(k, work, a.G)), dim3(kBlock), 0, s, a);
     KGX_CHECK_LAUNCH();
   }
-  if (a.t_n_rows > 0) {
+  if (a.items && a.n_split > 0) {
+    hipLaunchKernelGGL(gatv2_bwd_fixup_kernel<K>, dim3(grid_for(a.n_split * 64, 4096)), dim3(kBlock), 0, s, a.split,
+                       a.n_split, a.partials, HC, a.grad_h_dst, a.ld_gd, 64, 6);
+    KGX_CHECK_LAUNCH();
+  }
+  const int64_t t_work = a.t_items ? a.t_n_items : a.t_n_rows;
+  if (t_work > 0) {
     auto k = gatv2_bwd_src_kernel<K>;
-    hipLaunchKernelGGL(k, dim3(resident_grid(k, a.t_n_rows, a.G)), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(k, dim3(resident_grid(k, t_work, a.G)), dim3(kBlock), 0, s, a);
+    KGX_CHECK_LAUNCH();
+  }
+  if (a.t_items && a.t_n_split > 0) {
+    hipLaunchKernelGGL(gatv2_bwd_fixup_kernel<K>, dim3(grid_for(a.t_n_split * 64, 4096)), dim3(kBlock), 0, s,
+                       a.t_split, a.t_n_split, a.partials, HC, a.grad_h_src, a.ld_gs, 64, 6);
     KGX_CHECK_LAUNCH();
   }
   return KGX_OK;
@@ -508,30 +594,37 @@ int launch_bwd(const GatBwdArgs& a, hipStream_t s) {
 }  // namespace
 }  // namespace kgx
 
-extern "C" int kgx_gatv2_backward(const int32_t* rowptr, const int32_t* rows, int64_t n_rows, const int32_t* col,
+extern "C" int kgx_gatv2_backward(const int32_t* rowptr, const int32_t* rows, int64_t n_rows, const int32_t* items,
+                                  int64_t n_items, const int32_t* split, int64_t n_split, const int32_t* col,
                                   const float* h_src, const float* h_dst, int64_t ld_h, const float* att, int heads,
-                                  int channels, float negative_slope, const float* grad_out, int64_t ld_grad,
-                                  const int32_t* t_rowptr, int64_t n_src, const int32_t* t_col,
-                                  const int32_t* t_slot, float* grad_h_src, float* grad_h_dst,
-                                  int64_t ld_grad_h, float* grad_att, float* alpha_ws, float* ds_ws,
-                                  kgx_stream_t stream_) {
+                                  int channels, float negative_slope, const float* out, int64_t ld_out,
+                                  const float* bias, const float* stats, const float* grad_out, int64_t ld_grad,
+                                  const int32_t* t_rowptr, const int32_t* t_rows, int64_t n_src,
+                                  const int32_t* t_items, int64_t t_n_items, const int32_t* t_split,
+                                  int64_t t_n_split, const int32_t* t_col, const int32_t* t_slot,
+                                  float* grad_h_src, float* grad_h_dst, int64_t ld_grad_h, float* grad_att,
+                                  float* alpha_ws, float* ds_ws, float* partials, kgx_stream_t stream_) {
   hipStream_t stream = as_stream(stream_);
-  KGX_REQUIRE(heads > 0 && channels > 0 && n_rows >= 0 && n_src >= 0, KGX_ERR_ARG, "kgx_gatv2_backward: bad sizes");
+  KGX_REQUIRE(heads > 0 && channels > 0 && n_rows >= 0 && n_src >= 0 && n_items >= 0 && n_split >= 0 &&
+                  t_n_items >= 0 && t_n_split >= 0,
+              KGX_ERR_ARG, "kgx_gatv2_backward: bad sizes");
   const int64_t HC = int64_t(heads) * channels;
-  KGX_REQUIRE(rowptr && col && h_src && h_dst && att && grad_out && t_rowptr && grad_h_src && grad_h_dst &&
-                  grad_att && alpha_ws && ds_ws,
+  KGX_REQUIRE(rowptr && rows && col && h_src && h_dst && att && out && stats && grad_out && t_rowptr && t_rows &&
+                  t_col && t_slot && grad_h_src && grad_h_dst && grad_att && alpha_ws && ds_ws,
               KGX_ERR_ARG, "kgx_gatv2_backward: null pointer");
-  KGX_REQUIRE(ld_h >= HC && ld_grad >= HC && ld_grad_h >= HC, KGX_ERR_ARG,
+  KGX_REQUIRE(ld_h >= HC && ld_grad >= HC && ld_grad_h >= HC && ld_out >= HC, KGX_ERR_ARG,
               "kgx_gatv2_backward: leading dimension < heads*channels");
+  KGX_REQUIRE(((!items || n_split == 0) && (!t_items || t_n_split == 0)) || partials, KGX_ERR_ARG,
+              "kgx_gatv2_backward: split rows need partials");
   // K channels per lane: the smallest K (dividing C, with aligned vector
   // accesses) that fits one row's heads into a 64-lane group
   auto al = [](const void* p, int b) { return p == nullptr || reinterpret_cast<uintptr_t>(p) % b == 0; };
   int K = 0;
   for (int k = 1; k <= 16 && !K; k <<= 1) {
     const int va = 4 * (k < 4 ? k : 4);  // byte alignment vload<k> needs
-    if (channels % k || ld_h % (va / 4) || ld_grad % (va / 4) || ld_grad_h % (va / 4)) continue;
+    if (channels % k || ld_h % (va / 4) || ld_grad % (va / 4) || ld_grad_h % (va / 4) || ld_out % (va / 4)) continue;
     if (!al(h_src, va) || !al(h_dst, va) || !al(att, va) || !al(grad_out, va) || !al(grad_h_src, va) ||
-        !al(grad_h_dst, va))
+        !al(grad_h_dst, va) || !al(out, va) || !al(bias, va) || !al(partials, va))
       continue;
     if (heads * next_pow2(channels / k) <= 64) K = k;
   }
@@ -541,6 +634,10 @@ extern "C" int kgx_gatv2_backward(const int32_t* rowptr, const int32_t* rows, in
   a.rowptr = rowptr;
   a.rows = rows;
   a.n_rows = n_rows;
+  a.items = items ? reinterpret_cast<const int4*>(items) : nullptr;
+  a.n_items = items ? n_items : 0;
+  a.split = reinterpret_cast<const int4*>(split);
+  a.n_split = items ? n_split : 0;
   a.col = col;
   a.h_src = h_src;
   a.h_dst = h_dst;
@@ -549,6 +646,10 @@ extern "C" int kgx_gatv2_backward(const int32_t* rowptr, const int32_t* rows, in
   a.H = heads;
   a.C = channels;
   a.slope = negative_slope;
+  a.out = out;
+  a.ld_out = ld_out;
+  a.bias = bias;
+  a.stats = stats;
   a.grad = grad_out;
   a.ld_g = ld_grad;
   a.alpha = alpha_ws;
@@ -556,8 +657,14 @@ extern "C" int kgx_gatv2_backward(const int32_t* rowptr, const int32_t* rows, in
   a.grad_h_dst = grad_h_dst;
   a.ld_gd = ld_grad_h;
   a.grad_att = grad_att;
+  a.partials = partials;
   a.t_rowptr = t_rowptr;
+  a.t_rows = t_rows;
   a.t_n_rows = n_src;
+  a.t_items = t_items ? reinterpret_cast<const int4*>(t_items) : nullptr;
+  a.t_n_items = t_items ? t_n_items : 0;
+  a.t_split = reinterpret_cast<const int4*>(t_split);
+  a.t_n_split = t_items ? t_n_split : 0;
   a.t_col = t_col;
   a.t_slot = t_slot;
   a.grad_h_src = grad_h_src;

@@ -62,13 +62,15 @@ _SIGNATURES = {
         _int, _i32p, _i64, _i32p, _f32p, _i64, _i64, _f32p, _i64, _f32p, _i64, ctypes.c_void_p,
     ],
     "kgx_gatv2_backward": [
-        _i32p, _i32p, _i64, _i32p, _f32p, _f32p, _i64, _f32p, _int, _int, ctypes.c_float, _f32p, _i64,
-        _i32p, _i64, _i32p, _i32p, _f32p, _f32p, _i64, _f32p, _f32p, _f32p, ctypes.c_void_p,
+        _i32p, _i32p, _i64, _i32p, _i64, _i32p, _i64, _i32p, _f32p, _f32p, _i64, _f32p, _int, _int,
+        ctypes.c_float, _f32p, _i64, _f32p, _f32p, _f32p, _i64,
+        _i32p, _i32p, _i64, _i32p, _i64, _i32p, _i64, _i32p, _i32p,
+        _f32p, _f32p, _i64, _f32p, _f32p, _f32p, _f32p, ctypes.c_void_p,
     ],
     "kgx_gatv2": [
         _i32p, _i32p, _i64, _i32p, _i64, _i32p, _i64,
         _i32p, _f32p, _f32p, _i64, _f32p, _int, _int, ctypes.c_float,
-        _f32p, _i64, _f32p, _f32p, ctypes.c_void_p,
+        _f32p, _i64, _f32p, _f32p, _f32p, ctypes.c_void_p,
     ],
     "kgx_gather_rows": [_f32p, _i64, _i32p, _i64, _i64, _f32p, _i64, ctypes.c_void_p],
     "kgx_scatter_f32": [_f32p, _i32p, _i64, _f32p, ctypes.c_void_p],

@@ -205,6 +205,61 @@ def fused_transform_supported(f_in: int, f_out: int) -> bool:
     return f_in == 128 and f_out % 16 == 0 and 0 < f_out <= 128 and f_in <= f_out
 
 
+def _gatv2_impl(h_src, h_dst, rowptr, rows, items, split, col, att, heads, channels, negative_slope, bias,
+                n_slots, save_stats):
+    h_src, h_dst, att, bias = _f32c(h_src), _f32c(h_dst), _f32c(att), _f32c(bias)
+    dev = nat.require_device(h_src, h_dst, rowptr, rows, col, att, bias, items, split)
+    n_dst = rowptr.numel() - 1
+    HC = heads * channels
+    out = torch.empty((n_dst, HC), dtype=torch.float32, device=dev)
+    stats = torch.empty((n_dst if save_stats else 0, 2 * heads), dtype=torch.float32, device=dev)
+    if n_dst == 0:
+        return out, stats
+    n_items = 0 if items is None else items.shape[0]
+    n_split = 0 if split is None else split.shape[0]
+    partials = None
+    if items is not None and n_split > 0:
+        partials = torch.empty((n_slots, HC + 2 * heads), dtype=torch.float32, device=dev)
+    nat.check(
+        nat.lib().kgx_gatv2(
+            nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, nat.ptr(split), n_split,
+            nat.ptr(col), nat.ptr(h_src), nat.ptr(h_dst), h_src.stride(0), nat.ptr(att), heads, channels,
+            float(negative_slope), nat.ptr(out), out.stride(0), nat.ptr(bias), nat.ptr(partials),
+            nat.ptr(stats) if save_stats else None, nat.stream(dev),
+        ),
+        "kgx_gatv2",
+    )
+    return out, stats
+
+
+@torch.library.custom_op("kgx::gatv2_save", mutates_args=())
+def gatv2_save(
+    h_src: torch.Tensor,
+    h_dst: torch.Tensor,
+    rowptr: torch.Tensor,
+    rows: torch.Tensor,
+    items: Optional[torch.Tensor],
+    split: Optional[torch.Tensor],
+    col: torch.Tensor,
+    att: torch.Tensor,
+    heads: int,
+    channels: int,
+    negative_slope: float,
+    bias: Optional[torch.Tensor],
+    n_slots: int,
+) -> tuple[torch.Tensor, torch.Tensor]:
+    """kgx::gatv2 that also returns the per-row softmax statistics [n, 2*heads]."""
+    return _gatv2_impl(h_src, h_dst, rowptr, rows, items, split, col, att, heads, channels, negative_slope, bias,
+                       n_slots, True)
+
+
+@gatv2_save.register_fake
+def _gatv2_save_fake(h_src, h_dst, rowptr, rows, items, split, col, att, heads, channels, negative_slope, bias,
+                     n_slots):
+    n = rowptr.shape[0] - 1
+    return h_src.new_empty((n, heads * channels)), h_src.new_empty((n, 2 * heads))
+
+
 @torch.library.custom_op("kgx::gatv2", mutates_args=())
 def gatv2(
     h_src: torch.Tensor,
@@ -221,28 +276,8 @@ def gatv2(
     bias: Optional[torch.Tensor],
     n_slots: int,
 ) -> torch.Tensor:
-    h_src, h_dst, att, bias = _f32c(h_src), _f32c(h_dst), _f32c(att), _f32c(bias)
-    dev = nat.require_device(h_src, h_dst, rowptr, rows, col, att, bias, items, split)
-    n_dst = rowptr.numel() - 1
-    HC = heads * channels
-    out = torch.empty((n_dst, HC), dtype=torch.float32, device=dev)
-    if n_dst == 0:
-        return out
-    n_items = 0 if items is None else items.shape[0]
-    n_split = 0 if split is None else split.shape[0]
-    partials = None
-    if items is not None and n_split > 0:
-        partials = torch.empty((n_slots, HC + 2 * heads), dtype=torch.float32, device=dev)
-    nat.check(
-        nat.lib().kgx_gatv2(
-            nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, nat.ptr(split), n_split,
-            nat.ptr(col), nat.ptr(h_src), nat.ptr(h_dst), h_src.stride(0), nat.ptr(att), heads, channels,
-            float(negative_slope), nat.ptr(out), out.stride(0), nat.ptr(bias), nat.ptr(partials),
-            nat.stream(dev),
-        ),
-        "kgx_gatv2",
-    )
-    return out
+    return _gatv2_impl(h_src, h_dst, rowptr, rows, items, split, col, att, heads, channels, negative_slope, bias,
+                       n_slots, False)[0]
 
 
 @gatv2.register_fake
@@ -535,39 +570,57 @@ def _gatv2_raw(g, h_src, h_dst, att, heads, channels, negative_slope, bias, exac
 
 
 class _GATv2Fn(torch.autograd.Function):
-    """Autograd of the fused GATv2 aggregation: kgx_gatv2_backward (softmax
-    backward over the destination CSR, d h_src pulled over the transposed CSR)."""
+    """Autograd of the fused GATv2 aggregation: the forward keeps its output
+    and per-row softmax statistics; kgx_gatv2_backward does one pass over the
+    destination CSR (d h_dst, d att, per-edge alpha / ds) and pulls d h_src
+    over the transposed CSR, both with hub rows split into chunks."""
 
     @staticmethod
     def forward(ctx, h_src, h_dst, att, bias, g, heads, channels, negative_slope, exact):
-        ctx.g, ctx.heads, ctx.channels, ctx.slope = g, heads, channels, float(negative_slope)
-        ctx.same = h_src is h_dst
-        ctx.save_for_backward(h_src, h_dst, att)
-        return _gatv2_raw(g, h_src, h_dst, att, heads, channels, negative_slope, bias, exact)
+        ctx.g, ctx.heads, ctx.channels, ctx.slope, ctx.exact = g, heads, channels, float(negative_slope), exact
+        items, _, split, _, n_slots = g.work(exact)
+        out, stats = _timed(lambda: torch.ops.kgx.gatv2_save(
+            h_src, h_dst, g.rowptr, g.rows, items, split, g.col, att.reshape(-1), heads, channels,
+            float(negative_slope), bias, n_slots,
+        ))
+        ctx.save_for_backward(h_src, h_dst, att, bias, out, stats)
+        return out
 
     @staticmethod
     def backward(ctx, grad_out):
         from . import graph as G
 
-        h_src, h_dst, att = ctx.saved_tensors
+        h_src, h_dst, att, bias, out, stats = ctx.saved_tensors
         g, H, C = ctx.g, ctx.heads, ctx.channels
         grad_out = grad_out.contiguous()
         h_src, h_dst = h_src.contiguous(), h_dst.contiguous()
         att_flat = att.reshape(-1).contiguous()
         t = G.transpose(g)
+        items, _, split, _, n_slots = g.work(ctx.exact)
+        t_items, _, t_split, _, t_slots = t.work(ctx.exact)
         dev = grad_out.device
         g_src = torch.empty((g.n_src, H * C), dtype=torch.float32, device=dev)
         g_dst = torch.empty((g.n_dst, H * C), dtype=torch.float32, device=dev)
         g_att = torch.zeros(H * C, dtype=torch.float32, device=dev)
         alpha = torch.empty((max(g.kept, 1), H), dtype=torch.float32, device=dev)
         ds = torch.empty_like(alpha)
-        slot = t.extras["fwd_slot"].to(torch.int32)
+        partials = torch.empty((max(n_slots, t_slots, 1), H * C), dtype=torch.float32, device=dev)
+        slot = t.extras.get("fwd_slot32")
+        if slot is None:
+            slot = t.extras["fwd_slot"].to(torch.int32)
+            t.extras["fwd_slot32"] = slot
+        n_items = 0 if items is None else items.shape[0]
+        n_split = 0 if split is None else split.shape[0]
+        t_n_items = 0 if t_items is None else t_items.shape[0]
+        t_n_split = 0 if t_split is None else t_split.shape[0]
         nat.check(
             nat.lib().kgx_gatv2_backward(
-                nat.ptr(g.rowptr), nat.ptr(g.rows), g.n_dst, nat.ptr(g.col), nat.ptr(h_src), nat.ptr(h_dst),
-                h_src.stride(0), nat.ptr(att_flat), H, C, ctx.slope, nat.ptr(grad_out), grad_out.stride(0),
-                nat.ptr(t.rowptr), g.n_src, nat.ptr(t.col), nat.ptr(slot), nat.ptr(g_src), nat.ptr(g_dst),
-                g_src.stride(0), nat.ptr(g_att), nat.ptr(alpha), nat.ptr(ds), nat.stream(dev),
+                nat.ptr(g.rowptr), nat.ptr(g.rows), g.n_dst, nat.ptr(items), n_items, nat.ptr(split), n_split,
+                nat.ptr(g.col), nat.ptr(h_src), nat.ptr(h_dst), h_src.stride(0), nat.ptr(att_flat), H, C,
+                ctx.slope, nat.ptr(out), out.stride(0), nat.ptr(bias), nat.ptr(stats), nat.ptr(grad_out),
+                grad_out.stride(0), nat.ptr(t.rowptr), nat.ptr(t.rows), g.n_src, nat.ptr(t_items), t_n_items,
+                nat.ptr(t_split), t_n_split, nat.ptr(t.col), nat.ptr(slot), nat.ptr(g_src), nat.ptr(g_dst),
+                g_src.stride(0), nat.ptr(g_att), nat.ptr(alpha), nat.ptr(ds), nat.ptr(partials), nat.stream(dev),
             ),
             "kgx_gatv2_backward",
         )

@@ -60,8 +60,10 @@ def test_argument_validation_without_device(lib):
     # unsupported GAT shape (too many lanes per row) is reported, not launched
     rc = lib.kgx_gatv2(ctypes.c_void_p(16), ctypes.c_void_p(16), 1, None, 0, None, 0, ctypes.c_void_p(16),
                        ctypes.c_void_p(16), ctypes.c_void_p(16), 64 * 33, ctypes.c_void_p(16), 64, 33, 0.2,
-                       ctypes.c_void_p(16), 64 * 33, None, None, None)
+                       ctypes.c_void_p(16), 64 * 33, None, None, None, None)
     assert rc == 4
+    # backward of max/min only; fused accumulate flag validation
+    assert lib.kgx_spmm_max_backward(0, None, 0, None, None, 0, 0, None, 0, None, 0, None) == 1
     # rmat argument checks
     assert lib.kgx_rmat_edges(0, 4, 100, 1, 1, 1, 0, 10, None, None, None) == 1
 
