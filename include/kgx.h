@@ -45,8 +45,11 @@ enum kgx_reduce { KGX_SUM = 0, KGX_MEAN = 1, KGX_MAX = 2, KGX_MIN = 3, KGX_STD =
 
 /* Fused epilogues applied after the reduction of a destination row.
  *   BIAS: out = aggr + bias[f]              (GCNConv.update, gcn_conv.py:266-272)
- *   GIN : out = gin_scale * x[row,f] + aggr (GINConv.update, gin_conv.py:216-222) */
-enum kgx_epilogue { KGX_EPI_NONE = 0, KGX_EPI_BIAS = 1, KGX_EPI_GIN = 2 };
+ *   GIN : out = gin_scale * x[row,f] + aggr (GINConv.update, gin_conv.py:216-222)
+ *   RAW : MAX / MIN without the aggregators' isinf -> 0 guard: plain
+ *         keras.ops.segment_max semantics (empty segment -> -inf), as
+ *         BatchGlobalPooling uses it (global_pooling.py:228-249)            */
+enum kgx_epilogue { KGX_EPI_NONE = 0, KGX_EPI_BIAS = 1, KGX_EPI_GIN = 2, KGX_EPI_RAW = 3 };
 
 /* Graph-preparation flags. */
 enum kgx_csr_flags {
@@ -182,11 +185,14 @@ int kgx_spmm_gemm(int reduce, const int32_t* rowptr, const int32_t* rows, int64_
  * the edges of row i whose message equals the row's raw extreme; rows whose
  * extreme is +-inf (empty rows included) or NaN pass nothing.
  *   grad_table[idx[e], f] += grad_out[i, f] / ties   (float atomics)
+ * raw != 0 (KGX_EPI_RAW forward): no guard -- a +-inf extreme shares its
+ * gradient with its tied edges, and a -inf extreme also with the -inf init
+ * (torch's include_self count).
  * grad_table must be zero-initialised by the caller.  Sum / mean / weighted
  * sums need no separate entry point: their backward is kgx_spmm over the
  * transposed graph (a kgx_csr_build of the reversed edges).
  * ------------------------------------------------------------------------- */
-int kgx_spmm_max_backward(int reduce, const int32_t* rowptr, int64_t n_rows, const int32_t* idx,
+int kgx_spmm_max_backward(int reduce, int raw, const int32_t* rowptr, int64_t n_rows, const int32_t* idx,
                           const float* table, int64_t ld_table, int64_t F,
                           const float* grad_out, int64_t ld_grad_out,
                           float* grad_table, int64_t ld_grad_table, kgx_stream_t stream);

@@ -73,6 +73,12 @@ struct Reducer {
     if constexpr (RED == KGX_MAX || RED == KGX_MIN) return amax_update(acc, v);
     return __fadd_rn(acc, v);
   }
+  // KGX_EPI_RAW: max / min as plain segment_max (no isinf guard)
+  static __device__ __forceinline__ float finish_raw(float acc, int32_t deg) {
+    if constexpr (RED == KGX_MAX) return acc;
+    if constexpr (RED == KGX_MIN) return -acc;
+    return finish(acc, deg);
+  }
   static __device__ __forceinline__ float finish(float acc, int32_t deg) {
     if constexpr (RED == KGX_MEAN) return __fdiv_rn(acc, fmaxf(ref_count_f32(deg), 1e-8f));
     if constexpr (RED == KGX_MAX) return is_inf(acc) ? 0.0f : acc;
@@ -195,7 +201,8 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
       } else {
         float r[VEC];
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) r[k] = R::finish(acc[t][k], end - beg);
+        for (int k = 0; k < VEC; ++k)
+          r[k] = a.epi == KGX_EPI_RAW ? R::finish_raw(acc[t][k], end - beg) : R::finish(acc[t][k], end - beg);
         epilogue<VEC>(a, row, fo[t], r);
         if (a.hints & 2) vstore_nt<VEC>(a.out + int64_t(row) * a.ld_o + fo[t], r);
         else vstore<VEC>(a.out + int64_t(row) * a.ld_o + fo[t], r);
@@ -228,7 +235,7 @@ __global__ __launch_bounds__(kBlock) void spmm_fixup_kernel(SpmmArgs a) {
         for (int k = 0; k < VEC; ++k) acc[k] = R::combine(acc[k], p[k]);
       }
 #pragma unroll
-      for (int k = 0; k < VEC; ++k) acc[k] = R::finish(acc[k], deg);
+      for (int k = 0; k < VEC; ++k) acc[k] = a.epi == KGX_EPI_RAW ? R::finish_raw(acc[k], deg) : R::finish(acc[k], deg);
       epilogue<VEC>(a, row, f, acc);
       vstore<VEC>(a.out + int64_t(row) * a.ld_o + f, acc);
     }
@@ -349,7 +356,7 @@ extern "C" int kgx_spmm(int reduce, int epilogue, const int32_t* rowptr, const i
                         float gin_scale, float* partials, kgx_stream_t stream_) {
   hipStream_t stream = as_stream(stream_);
   KGX_REQUIRE(reduce >= KGX_SUM && reduce <= KGX_STD, KGX_ERR_ARG, "kgx_spmm: unknown reduce %d", reduce);
-  KGX_REQUIRE(epilogue >= KGX_EPI_NONE && epilogue <= KGX_EPI_GIN, KGX_ERR_ARG, "kgx_spmm: unknown epilogue %d",
+  KGX_REQUIRE(epilogue >= KGX_EPI_NONE && epilogue <= KGX_EPI_RAW, KGX_ERR_ARG, "kgx_spmm: unknown epilogue %d",
               epilogue);
   KGX_REQUIRE(F >= 0 && n_rows >= 0 && n_items >= 0 && n_split >= 0, KGX_ERR_ARG, "kgx_spmm: negative size");
   if (F == 0 || n_rows == 0) return KGX_OK;

@@ -21,7 +21,7 @@ namespace kgx {
 namespace {
 
 template <int RED>
-__global__ __launch_bounds__(kBlock) void max_backward_kernel(const int32_t* __restrict__ rowptr, int64_t n_rows,
+__global__ __launch_bounds__(kBlock) void max_backward_kernel(int raw, const int32_t* __restrict__ rowptr, int64_t n_rows,
                                                               const int32_t* __restrict__ idx,
                                                               const float* __restrict__ table, int64_t ld_t,
                                                               int64_t F, const float* __restrict__ grad_out,
@@ -40,9 +40,10 @@ __global__ __launch_bounds__(kBlock) void max_backward_kernel(const int32_t* __r
       m = amax_update(m, RED == KGX_MIN ? -v : v);
     }
     if (RED == KGX_MIN) m = -m;
-    if (__builtin_isinf(m) || m != m) continue;  // isinf guard / NaN: no gradient
-    // pass 2: ties
-    int32_t cnt = 0;
+    if (m != m) continue;                         // NaN: no edge equals the result
+    if (!raw && __builtin_isinf(m)) continue;     // the aggregators' isinf guard passes nothing
+    // pass 2: ties (raw: the -inf init of the scatter counts as one more tie)
+    int32_t cnt = (raw && m == (RED == KGX_MIN ? __builtin_inff() : -__builtin_inff())) ? 1 : 0;
     for (int32_t e = beg; e < end; ++e) cnt += table[int64_t(idx[e]) * ld_t + f] == m;
     if (cnt == 0) continue;
     // pass 3: share the gradient
@@ -59,7 +60,7 @@ __global__ __launch_bounds__(kBlock) void max_backward_kernel(const int32_t* __r
 
 using namespace kgx;
 
-extern "C" int kgx_spmm_max_backward(int reduce, const int32_t* rowptr, int64_t n_rows, const int32_t* idx,
+extern "C" int kgx_spmm_max_backward(int reduce, int raw, const int32_t* rowptr, int64_t n_rows, const int32_t* idx,
                                      const float* table, int64_t ld_table, int64_t F, const float* grad_out,
                                      int64_t ld_grad_out, float* grad_table, int64_t ld_grad_table,
                                      kgx_stream_t stream_) {
@@ -73,10 +74,10 @@ extern "C" int kgx_spmm_max_backward(int reduce, const int32_t* rowptr, int64_t 
               "kgx_spmm_max_backward: leading dimension < F");
   const unsigned grid = grid_for(n_rows * F, 16384);
   if (reduce == KGX_MAX)
-    hipLaunchKernelGGL(max_backward_kernel<KGX_MAX>, dim3(grid), dim3(kBlock), 0, stream, rowptr, n_rows, idx, table,
+    hipLaunchKernelGGL(max_backward_kernel<KGX_MAX>, dim3(grid), dim3(kBlock), 0, stream, raw, rowptr, n_rows, idx, table,
                        ld_table, F, grad_out, ld_grad_out, grad_table, ld_grad_table);
   else
-    hipLaunchKernelGGL(max_backward_kernel<KGX_MIN>, dim3(grid), dim3(kBlock), 0, stream, rowptr, n_rows, idx, table,
+    hipLaunchKernelGGL(max_backward_kernel<KGX_MIN>, dim3(grid), dim3(kBlock), 0, stream, raw, rowptr, n_rows, idx, table,
                        ld_table, F, grad_out, ld_grad_out, grad_table, ld_grad_table);
   KGX_CHECK_LAUNCH();
   return KGX_OK;

@@ -9,26 +9,32 @@ from . import _native, graph, ops
 from .graph import CSRGraph, build_csr, clear_cache
 from .layers import (
     AggregatorFactory,
+    BatchGlobalPooling,
     GATv2Conv,
     GCNConv,
     GINConv,
+    GlobalPooling,
     MessagePassing,
     SAGEConv,
     set_random_seed,
 )
-from .utils import add_self_loops, compute_gcn_normalization
+from .utils import GraphData, add_self_loops, batch_graphs, compute_gcn_normalization
 
 __version__ = "0.1.0"
 
 __all__ = [
     "AggregatorFactory",
+    "BatchGlobalPooling",
     "CSRGraph",
     "GATv2Conv",
     "GCNConv",
     "GINConv",
+    "GlobalPooling",
+    "GraphData",
     "MessagePassing",
     "SAGEConv",
     "add_self_loops",
+    "batch_graphs",
     "build_csr",
     "clear_cache",
     "compute_gcn_normalization",

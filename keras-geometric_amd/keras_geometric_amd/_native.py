@@ -20,7 +20,7 @@ LIB_PATH = Path(os.environ.get("KGX_LIB", _PKG_ROOT / "lib" / "libkgx.so"))
 
 KGX_OK, KGX_ERR_ARG, KGX_ERR_HIP, KGX_ERR_INDEX, KGX_ERR_UNSUPPORTED = range(5)
 SUM, MEAN, MAX, MIN, STD = range(5)
-EPI_NONE, EPI_BIAS, EPI_GIN = range(3)
+EPI_NONE, EPI_BIAS, EPI_GIN, EPI_RAW = range(4)
 FUSED_PRE_GIN, FUSED_ACCUMULATE = 1, 2
 CSR_SELF_LOOPS, CSR_SEGMENT_ONLY, CSR_GCN_NORM = 1, 2, 4
 
@@ -59,7 +59,7 @@ _SIGNATURES = {
         _f32p, _i64, _f32p, _f32p, _i64, ctypes.c_void_p,
     ],
     "kgx_spmm_max_backward": [
-        _int, _i32p, _i64, _i32p, _f32p, _i64, _i64, _f32p, _i64, _f32p, _i64, ctypes.c_void_p,
+        _int, _int, _i32p, _i64, _i32p, _f32p, _i64, _i64, _f32p, _i64, _f32p, _i64, ctypes.c_void_p,
     ],
     "kgx_gatv2_backward": [
         _i32p, _i32p, _i64, _i32p, _i64, _i32p, _i64, _i32p, _f32p, _f32p, _i64, _f32p, _int, _int,

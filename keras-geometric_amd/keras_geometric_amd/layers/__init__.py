@@ -15,15 +15,18 @@ from .gatv2_conv import GATv2Conv
 from .gcn_conv import GCNConv
 from .gin_conv import GINConv
 from .message_passing import MessagePassing
+from .pooling import BatchGlobalPooling, GlobalPooling
 from .sage_conv import SAGEConv
 
 __all__ = [
     "Aggregator",
     "AggregatorFactory",
+    "BatchGlobalPooling",
     "Dense",
     "GATv2Conv",
     "GCNConv",
     "GINConv",
+    "GlobalPooling",
     "Layer",
     "MaxAggregator",
     "MeanAggregator",

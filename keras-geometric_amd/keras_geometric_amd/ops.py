@@ -365,7 +365,7 @@ def _aggregate_raw(g, table, red, weighted, by_edge, epilogue, bias, xroot, gin_
 
 
 def _reduce_backward(g: CSRGraph, red: int, weighted: bool, by_edge: bool, table: torch.Tensor | None,
-                     grad_out: torch.Tensor, exact: bool, table_rows: int) -> torch.Tensor:
+                     grad_out: torch.Tensor, exact: bool, table_rows: int, raw: bool = False) -> torch.Tensor:
     """d loss / d table of REDUCE_{e in row} table[idx_e] (* w_e), given d loss / d out.
 
     sum / mean: the transposed aggregation (graph.transpose: each source row
@@ -384,7 +384,7 @@ def _reduce_backward(g: CSRGraph, red: int, weighted: bool, by_edge: bool, table
         idx = g.eid if by_edge else g.col
         nat.check(
             nat.lib().kgx_spmm_max_backward(
-                red, nat.ptr(g.rowptr), g.n_dst, nat.ptr(idx), nat.ptr(table), table.stride(0), table.shape[1],
+                red, int(raw), nat.ptr(g.rowptr), g.n_dst, nat.ptr(idx), nat.ptr(table), table.stride(0), table.shape[1],
                 nat.ptr(grad_out), grad_out.stride(0), nat.ptr(gt), gt.stride(0), nat.stream(table.device),
             ),
             "kgx_spmm_max_backward",
@@ -420,7 +420,7 @@ class _AggregateFn(torch.autograd.Function):
         g_table = g_bias = g_xroot = None
         if ctx.needs_input_grad[0]:
             g_table = _reduce_backward(ctx.g, ctx.red, ctx.weighted, ctx.by_edge, table, grad_out, ctx.exact,
-                                       ctx.table_rows)
+                                       ctx.table_rows, raw=ctx.epilogue == nat.EPI_RAW)
         if ctx.needs_input_grad[1] and ctx.epilogue == nat.EPI_BIAS:
             g_bias = grad_out.sum(0)
         if ctx.needs_input_grad[2] and ctx.epilogue == nat.EPI_GIN:

@@ -251,6 +251,60 @@ def gatv2_forward(x, edge_index, kernel, att, bias=None, heads=1, concat=True, n
 
 
 # ---------------------------------------------------------------------------
+# layers/pooling/global_pooling.py, utils/data_utils.py
+# ---------------------------------------------------------------------------
+
+
+def global_pooling(x, pooling: str = "mean") -> torch.Tensor:
+    """GlobalPooling.call (global_pooling.py:66-92): ops.mean/max/sum over axis 0, keepdims."""
+    x = K.convert(x)
+    if pooling == "mean":
+        return torch.mean(x, dim=0, keepdim=True)
+    if pooling == "max":
+        return torch.amax(x, dim=0, keepdim=True)
+    return torch.sum(x, dim=0, keepdim=True)
+
+
+def batch_global_pooling(x, batch, pooling: str = "mean") -> torch.Tensor:
+    """BatchGlobalPooling.call (global_pooling.py:214-251)."""
+    x = K.convert(x)
+    batch = K.cast(batch, torch.int32)
+    num_graphs = int(torch.max(batch)) + 1  # :231
+    if pooling == "mean":  # :235-247
+        pooled_sum = K.segment_sum(x, batch, num_graphs)
+        ones = torch.ones_like(batch, dtype=x.dtype)
+        counts = K.segment_sum(ones, batch, num_graphs)
+        counts = torch.maximum(counts, torch.tensor(1.0, dtype=x.dtype))
+        return pooled_sum / torch.unsqueeze(counts, 1)
+    if pooling == "max":  # :249-250, no isinf guard
+        return K.segment_max(x, batch, num_graphs)
+    return K.segment_sum(x, batch, num_graphs)  # :252-253
+
+
+def batch_graphs(graphs):
+    """batch_graphs (data_utils.py:139-272) on numpy dicts {x, edge_index, [edge_attr], [y]}:
+    returns dict with x, edge_index (shifted by node offsets), batch, edge_attr, y."""
+    xs = [np.asarray(g["x"]) for g in graphs]
+    total = sum(x.shape[0] for x in xs)
+    out = {"x": np.concatenate(xs, 0), "batch": np.zeros(total, np.int32)}
+    eis, off = [], 0
+    for i, g in enumerate(graphs):
+        n = xs[i].shape[0]
+        out["batch"][off:off + n] = i  # :219-223
+        ei = np.asarray(g["edge_index"])
+        if ei.shape[1]:
+            eis.append(ei + off)  # :226-230
+        off += n
+    out["edge_index"] = np.concatenate(eis, 1) if eis else np.zeros((2, 0), np.int32)
+    if all(g.get("edge_attr") is not None for g in graphs):
+        out["edge_attr"] = np.concatenate([g["edge_attr"] for g in graphs], 0)
+    if all(g.get("y") is not None for g in graphs):
+        ys = [np.asarray(g["y"]) for g in graphs]
+        out["y"] = np.stack(ys, 0) if ys[0].ndim == 1 else np.concatenate(ys, 0)  # :245-252
+    return out
+
+
+# ---------------------------------------------------------------------------
 # stable CSR by destination (integer parity of kgx_csr_build)
 # ---------------------------------------------------------------------------
 

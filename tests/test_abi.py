@@ -63,7 +63,7 @@ def test_argument_validation_without_device(lib):
                        ctypes.c_void_p(16), 64 * 33, None, None, None, None)
     assert rc == 4
     # backward of max/min only; fused accumulate flag validation
-    assert lib.kgx_spmm_max_backward(0, None, 0, None, None, 0, 0, None, 0, None, 0, None) == 1
+    assert lib.kgx_spmm_max_backward(0, 0, None, 0, None, None, 0, 0, None, 0, None, 0, None) == 1
     # rmat argument checks
     assert lib.kgx_rmat_edges(0, 4, 100, 1, 1, 1, 0, 10, None, None, None) == 1
 

@@ -147,6 +147,23 @@ def c3_train(dev):
                 edges_per_s=g.kept / ms * 1e3)
 
 
+def pool(dev):
+    """BatchGlobalPooling (sum / mean / max) over 10M nodes, F 128, 100k graphs:
+    a segment reduction whose rows are contiguous -- a streaming read of x."""
+    from keras_geometric_amd.layers import BatchGlobalPooling
+
+    n, f, G = 10_000_000, 128, 100_000
+    x = torch.randn(n, f, device=dev)
+    batch = torch.sort(torch.randint(0, G, (n,), device=dev, dtype=torch.int32)).values
+    out = {}
+    for p in ("sum", "mean", "max"):
+        layer = BatchGlobalPooling(pooling=p)
+        layer([x, batch])
+        ms, agg, _ = run(lambda: layer([x, batch]), steps=10)
+        out[p] = dict(layer_ms=ms, kernel_ms=agg, GBps=(4 * n * f + 4 * n + 4 * G * f) / agg / 1e6)
+    return dict(config="BatchGlobalPooling 10M nodes F128 100k graphs", **out)
+
+
 def c1(dev):
     n, e, fin = 2708, 10556, 1433
     ei = synthetic.rmat_edge_index(n, e, seed=0, device=dev)
@@ -163,7 +180,7 @@ def c1(dev):
 
 if __name__ == "__main__":
     dev = torch.device("cuda", 0)
-    names = sys.argv[1:] or ["c1", "c2", "c3", "c4", "c5", "ns_train", "c3_train"]
+    names = sys.argv[1:] or ["c1", "c2", "c3", "c4", "c5", "ns_train", "c3_train", "pool"]
     for name in names:
         r = globals()[name](dev)
         print(json.dumps(r), flush=True)
