@@ -140,6 +140,12 @@ def main() -> None:
         t0 = time.perf_counter()
         layer([x, ei])  # build: weights + CSR + schedule (cached)
         torch.cuda.synchronize()
+        first_call_ms = (time.perf_counter() - t0) * 1e3
+        # steady-state graph preparation (CSR + schedule), timed warm: once per graph, not per step
+        t0 = time.perf_counter()
+        kgx.graph.build_csr(ei[0].contiguous(), ei[1].contiguous(), n_local, n_local, self_loops=True,
+                            gcn_norm=True, n_features=f_out)
+        torch.cuda.synchronize()
         graph_build_ms = (time.perf_counter() - t0) * 1e3
         g = next(iter(kgx.graph._CACHE.values()))[1]
         e_agg, n_rows, max_deg = g.kept, g.n_dst, g.max_degree
@@ -156,7 +162,7 @@ def main() -> None:
         layer = kd.ShardedGCNConv(f_out, sg)
         layer(x)
         torch.cuda.synchronize()
-        graph_build_ms = (time.perf_counter() - t0) * 1e3
+        graph_build_ms = first_call_ms = (time.perf_counter() - t0) * 1e3  # incl. shard generation + halo plan
         e_agg, n_rows, max_deg = sg.graph.kept, sg.n_local, sg.graph.max_degree
         step = lambda: layer(x)  # noqa: E731
         shard_info = {"halo_rows_per_rank": sg.n_halo, "halo_MB_per_layer": sg.n_halo * f_in * 4 / 1e6}
@@ -236,6 +242,7 @@ def main() -> None:
         "aggregation_ms": kern_ms,
         "aggregation_launches_per_step": launches,
         "graph_build_ms": graph_build_ms,
+        "first_call_ms": first_call_ms,
         "roofline": {
             "bound": "hbm",
             "achieved": achieved,

@@ -164,6 +164,38 @@ def pool(dev):
     return dict(config="BatchGlobalPooling 10M nodes F128 100k graphs", **out)
 
 
+def io(dev):
+    """Persistent graph file: NS graph (10M/100M, GCN CSR + schedule) loaded
+    from an NPZ vs rebuilt from edge_index (x is 1 feature wide to keep the
+    file to the graph)."""
+    import os
+    import tempfile
+
+    from keras_geometric_amd.utils import load_graphs, save_graphs
+
+    n, e = 10_000_000, 100_000_000
+    ei = synthetic.rmat_edge_index(n, e, seed=0, device=dev)
+    gd = kgx.GraphData(x=torch.zeros(n, 1, device=dev), edge_index=ei)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    G = kgx.graph.build_csr(ei[0].contiguous(), ei[1].contiguous(), n, n, self_loops=True, gcn_norm=True)
+    torch.cuda.synchronize()
+    build_s = time.perf_counter() - t0
+    del G
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as d:
+        path = os.path.join(d, "ns.npz")
+        save_graphs(path, [gd], with_csr=True, self_loops=True, gcn_norm=True, n_features=128)
+        size = os.path.getsize(path)
+        kgx.clear_cache()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        loaded, _ = load_graphs(path)
+        torch.cuda.synchronize()
+        load_s = time.perf_counter() - t0
+    return dict(config="NS graph CSR: build vs load", build_s=build_s, load_s=load_s, file_GB=size / 1e9,
+                kept=loaded[0].csr.kept)
+
+
 def c1(dev):
     n, e, fin = 2708, 10556, 1433
     ei = synthetic.rmat_edge_index(n, e, seed=0, device=dev)
@@ -180,7 +212,7 @@ def c1(dev):
 
 if __name__ == "__main__":
     dev = torch.device("cuda", 0)
-    names = sys.argv[1:] or ["c1", "c2", "c3", "c4", "c5", "ns_train", "c3_train", "pool"]
+    names = sys.argv[1:] or ["c1", "c2", "c3", "c4", "c5", "ns_train", "c3_train", "pool", "io"]
     for name in names:
         r = globals()[name](dev)
         print(json.dumps(r), flush=True)
