@@ -142,6 +142,8 @@ int kgx_schedule_build(const int32_t* rowptr, int64_t n_dst, int32_t split_len,
  *   sequentially in CSR order (EXACT: bit-identical to the reference's
  *   sequential scatter_add / scatter_reduce for identical messages).
  * KGX_STD ignores items (always EXACT, two sequential passes per row).
+ * drop_key (optional, SUM only): per-slot keys of the message dropout mask
+ * (see kgx_dropout_mask); the message is (table[idx] * mask) * w.
  * ------------------------------------------------------------------------- */
 int kgx_spmm(int reduce, int epilogue,
              const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
@@ -151,7 +153,18 @@ int kgx_spmm(int reduce, int epilogue,
              const float* table, int64_t ld_table, int64_t F,
              float* out, int64_t ld_out,
              const float* bias, const float* xroot, int64_t ld_x, float gin_scale,
+             const int32_t* drop_key, float drop_p, uint64_t drop_seed,
              float* partials, kgx_stream_t stream);
+
+/* Message dropout mask (training; GCNConv.message dropout, gcn_conv.py:237-242;
+ * GATv2 attention dropout, gatv2_conv.py:252-253): element (key, f) is kept
+ * with probability 1 - p and scaled by 1/(1-p).  The mask is a pure function
+ * of (seed, key = input edge id, f), so a layer's forward (kgx_spmm with
+ * drop_key = the CSR's input edge ids), its backward over the transposed
+ * graph and tests agree.  kgx_dropout_mask writes the multiplier (0 or
+ * 1/(1-p)) of n keys x F columns, row-major. */
+int kgx_dropout_mask(uint64_t seed, float p, const int32_t* keys, int64_t n, int64_t F, float* out,
+                     kgx_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Fused aggregate -> dense transform (+ bias), one launch (plus a fix-up for
@@ -209,6 +222,9 @@ int kgx_spmm_max_backward(int reduce, int raw, const int32_t* rowptr, int64_t n_
  * partials: n_slots * (heads*channels + 2*heads) floats when items are split.
  * stats (optional, [n, 2*heads]): per row and head the softmax max and
  * denominator (sum + 1e-10), kept for kgx_gatv2_backward.
+ * drop_key (optional): attention dropout (training, gatv2_conv.py:252-253):
+ * alpha of (slot e, head h) is multiplied by the kgx_dropout_mask value of
+ * (seed, drop_key[e], h); the denominator is not.
  * ------------------------------------------------------------------------- */
 int kgx_gatv2(const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
               const int32_t* items, int64_t n_items,
@@ -216,7 +232,8 @@ int kgx_gatv2(const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
               const int32_t* col, const float* h_src, const float* h_dst, int64_t ld_h,
               const float* att, int heads, int channels, float negative_slope,
               float* out, int64_t ld_out, const float* bias,
-              float* partials, float* stats, kgx_stream_t stream);
+              float* partials, float* stats,
+              const int32_t* drop_key, float drop_p, uint64_t drop_seed, kgx_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Backward of kgx_gatv2 (autograd of GATv2Conv's propagate, gatv2_conv.py:
@@ -241,7 +258,8 @@ int kgx_gatv2_backward(const int32_t* rowptr, const int32_t* rows, int64_t n_row
                        const int32_t* t_items, int64_t t_n_items, const int32_t* t_split, int64_t t_n_split,
                        const int32_t* t_col, const int32_t* t_slot,
                        float* grad_h_src, float* grad_h_dst, int64_t ld_grad_h, float* grad_att,
-                       float* alpha_ws, float* ds_ws, float* partials, kgx_stream_t stream);
+                       float* alpha_ws, float* ds_ws, float* partials,
+                       const int32_t* drop_key, float drop_p, uint64_t drop_seed, kgx_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Row gather out[i,:] = table[rows[i], :] — packs halo rows for the multi-GPU

@@ -43,6 +43,11 @@ struct GatArgs {
   const float* bias;
   float* partials;  // per slot: [H*C acc | H m | H l]
   float* stats;     // optional [n, 2H]: per row and head, the softmax max m and denominator l + 1e-10
+  // attention dropout (training): alpha_e *= keep(seed, drop_key[e], head) / (1 - p)
+  const int32_t* drop_key;
+  uint64_t drop_seed;
+  uint32_t drop_thresh;
+  float drop_scale;
   int G, lgG, LH, lgLH;
 };
 
@@ -54,7 +59,11 @@ __device__ __forceinline__ float head_reduce(float p, int LH) {
 
 template <int K>
 __global__ __launch_bounds__(kBlock) void gatv2_kernel(GatArgs a) {
+#ifdef KGX_GAT_U
+  constexpr int U = KGX_GAT_U;
+#else
   constexpr int U = K <= 4 ? 8 : (K == 8 ? 4 : 2);
+#endif
   const int G = a.G;
   const int lane = threadIdx.x & (G - 1);
   const int head = lane >> a.lgLH;
@@ -102,16 +111,21 @@ __global__ __launch_bounds__(kBlock) void gatv2_kernel(GatArgs a) {
       int32_t c[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) c[u] = a.col[u < n ? e + u : end - 1];
+      float dm[U];  // attention dropout multiplier per edge (this lane's head)
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        dm[u] = a.drop_key ? drop_scale(a.drop_seed, uint32_t(a.drop_key[u < n ? e + u : end - 1]), uint32_t(head),
+                                        a.drop_thresh, a.drop_scale)
+                           : 1.0f;
+      // unconditional loads from clamped addresses (padding lanes read column 0
+      // of the row; edges past the end re-read the last one), masked on use
       float hs[U][K];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (valid && u < n) {
-          vload<K>(hs[u], a.h_src + int64_t(c[u]) * a.ld_h + f);
-        } else {
+      for (int u = 0; u < U; ++u) vload<K>(hs[u], a.h_src + int64_t(c[u]) * a.ld_h + (valid ? f : 0));
 #pragma unroll
-          for (int k = 0; k < K; ++k) hs[u][k] = 0.0f;
-        }
-      }
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int k = 0; k < K; ++k) hs[u][k] = valid ? hs[u][k] : 0.0f;
       float s[U];
       float mc = -__builtin_inff();
 #pragma unroll
@@ -136,9 +150,10 @@ __global__ __launch_bounds__(kBlock) void gatv2_kernel(GatArgs a) {
       for (int u = 0; u < U; ++u) {
         if (u < n) {
           const double pu = double(expf(s[u] - m_new));
-          l += pu;
+          l += pu;  // the denominator sees every edge; dropout masks the normalised alpha
+          const double pd = pu * double(dm[u]);
 #pragma unroll
-          for (int k = 0; k < K; ++k) acc[k] = fma(pu, double(hs[u][k]), acc[k]);
+          for (int k = 0; k < K; ++k) acc[k] = fma(pd, double(hs[u][k]), acc[k]);
         }
       }
       m = m_new;
@@ -249,7 +264,8 @@ extern "C" int kgx_gatv2(const int32_t* rowptr, const int32_t* rows, int64_t n_r
                          int64_t n_items, const int32_t* split, int64_t n_split, const int32_t* col,
                          const float* h_src, const float* h_dst, int64_t ld_h, const float* att, int heads,
                          int channels, float negative_slope, float* out, int64_t ld_out, const float* bias,
-                         float* partials, float* stats, kgx_stream_t stream_) {
+                         float* partials, float* stats, const int32_t* drop_key, float drop_p,
+                         uint64_t drop_seed, kgx_stream_t stream_) {
   hipStream_t stream = as_stream(stream_);
   KGX_REQUIRE(heads > 0 && channels > 0 && n_rows >= 0 && n_items >= 0 && n_split >= 0, KGX_ERR_ARG,
               "kgx_gatv2: bad sizes");
@@ -306,6 +322,13 @@ extern "C" int kgx_gatv2(const int32_t* rowptr, const int32_t* rows, int64_t n_r
   a.bias = bias;
   a.partials = partials;
   a.stats = stats;
+  KGX_REQUIRE(drop_p >= 0.0f && drop_p < 1.0f, KGX_ERR_ARG, "kgx_gatv2: dropout p must be in [0, 1)");
+  if (drop_key && drop_p > 0.0f) {
+    a.drop_key = drop_key;
+    a.drop_seed = drop_seed;
+    a.drop_thresh = uint32_t(double(drop_p) * 4294967296.0);
+    a.drop_scale = 1.0f / (1.0f - drop_p);
+  }
   a.LH = next_pow2((channels + K - 1) / K);
   a.lgLH = log2i(a.LH);
   a.G = next_pow2(heads * a.LH);
@@ -362,6 +385,10 @@ struct GatBwdArgs {
   int64_t ld_out;
   const float* bias;
   const float* stats;  // [n, 2H] from the forward
+  const int32_t* drop_key;  // attention dropout keys per CSR slot (or null)
+  uint64_t drop_seed;
+  uint32_t drop_thresh;
+  float drop_scale;
   const float* grad;
   int64_t ld_g;
   float* alpha;  // [E', H] CSR slot order
@@ -471,7 +498,11 @@ __global__ __launch_bounds__(kBlock) void gatv2_bwd_rows_kernel(GatBwdArgs a) {
         const float da = head_reduce<K>(pa, a.LH);
         if (e + u < end) {
           const float al = __fdiv_rn(expf(sc - m), den);
-          const float dsv = al * (da - D);
+          // dropout: out = sum alpha*d*h, so d alpha = d * <G, h>; D = <G, out - b> already includes d
+          const float dmu = a.drop_key ? drop_scale(a.drop_seed, uint32_t(a.drop_key[e + u]), uint32_t(head),
+                                                    a.drop_thresh, a.drop_scale)
+                                       : 1.0f;
+          const float dsv = al * (dmu * da - D);
 #pragma unroll
           for (int k = 0; k < K; ++k) {
             const float g = hd[k] + hs[u][k];
@@ -479,7 +510,7 @@ __global__ __launch_bounds__(kBlock) void gatv2_bwd_rows_kernel(GatBwdArgs a) {
             gatt[k] += dsv * lrelu(g);
           }
           if (valid && sub == 0) {
-            a.alpha[int64_t(e + u) * a.H + head] = al;
+            a.alpha[int64_t(e + u) * a.H + head] = al * dmu;  // the message weight kernel B pulls with
             a.ds[int64_t(e + u) * a.H + head] = dsv;
           }
         }
@@ -603,7 +634,8 @@ extern "C" int kgx_gatv2_backward(const int32_t* rowptr, const int32_t* rows, in
                                   const int32_t* t_items, int64_t t_n_items, const int32_t* t_split,
                                   int64_t t_n_split, const int32_t* t_col, const int32_t* t_slot,
                                   float* grad_h_src, float* grad_h_dst, int64_t ld_grad_h, float* grad_att,
-                                  float* alpha_ws, float* ds_ws, float* partials, kgx_stream_t stream_) {
+                                  float* alpha_ws, float* ds_ws, float* partials, const int32_t* drop_key,
+                                  float drop_p, uint64_t drop_seed, kgx_stream_t stream_) {
   hipStream_t stream = as_stream(stream_);
   KGX_REQUIRE(heads > 0 && channels > 0 && n_rows >= 0 && n_src >= 0 && n_items >= 0 && n_split >= 0 &&
                   t_n_items >= 0 && t_n_split >= 0,
@@ -650,6 +682,13 @@ extern "C" int kgx_gatv2_backward(const int32_t* rowptr, const int32_t* rows, in
   a.ld_out = ld_out;
   a.bias = bias;
   a.stats = stats;
+  KGX_REQUIRE(drop_p >= 0.0f && drop_p < 1.0f, KGX_ERR_ARG, "kgx_gatv2_backward: dropout p must be in [0, 1)");
+  if (drop_key && drop_p > 0.0f) {
+    a.drop_key = drop_key;
+    a.drop_seed = drop_seed;
+    a.drop_thresh = uint32_t(double(drop_p) * 4294967296.0);
+    a.drop_scale = 1.0f / (1.0f - drop_p);
+  }
   a.grad = grad_out;
   a.ld_g = ld_grad;
   a.alpha = alpha_ws;

@@ -83,6 +83,21 @@ __device__ __forceinline__ float amax_update(float acc, float v) {
 
 __device__ __forceinline__ bool is_inf(float v) { return __builtin_isinf(v); }
 
+// Counter-based dropout mask: element (key, f) is kept iff the high 32 bits of
+// splitmix64(seed ^ (key << 32 | f) * golden) are >= thresh = p * 2^32.  A
+// function of (seed, edge id, feature) only, so the forward, its backward over
+// the transposed graph and the test oracle (kgx_dropout_mask) agree.
+__host__ __device__ __forceinline__ uint32_t drop_hash(uint64_t seed, uint32_t key, uint32_t f) {
+  uint64_t z = seed ^ ((uint64_t(key) << 32 | f) * 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return uint32_t(z >> 32);
+}
+__device__ __forceinline__ float drop_scale(uint64_t seed, uint32_t key, uint32_t f, uint32_t thresh, float keep_scale) {
+  return drop_hash(seed, key, f) >= thresh ? keep_scale : 0.0f;
+}
+
 // IEEE round-to-nearest sqrt.  NOTE: on gfx950 `__fsqrt_rn` lowers to a bare
 // v_sqrt_f32 (~1 ulp); plain sqrtf under hipcc's default
 // -fhip-fp32-correctly-rounded-divide-sqrt expands to v_sqrt + an fma-based

@@ -53,6 +53,12 @@ struct SpmmArgs {
   int G;
   int lgG;
   int hints;  // bit0: nt loads of idx/w, bit1: nt stores of out (experiment knob, KGX_SPMM_HINTS)
+  // message dropout (training): message *= keep(seed, drop_key[e], column) / (1 - p)
+  const int32_t* drop_key;
+  uint64_t drop_seed;
+  uint32_t drop_thresh;
+  float drop_scale;
+  int f_base;  // first column of this launch (column slicing of wide F)
 };
 
 template <int RED>
@@ -110,13 +116,18 @@ __device__ __forceinline__ void epilogue(const SpmmArgs& a, int32_t row, int f, 
 // to end-1, whose row is already being fetched), then an in-order fold where
 // clamped edges contribute the reduction's identity.  No load sits under a
 // lane-dependent branch, so hipcc keeps all U gathers in flight.
-template <int U, int VEC, int NT, int RED, bool WEIGHTED>
+template <int U, int VEC, int NT, int RED, bool WEIGHTED, bool DROP = false>
 __device__ __forceinline__ void edge_block(const SpmmArgs& a, int32_t e, int32_t end, const int (&fl)[NT],
                                            float (&acc)[NT][VEC]) {
   using R = Reducer<RED>;
   const int n = end - e;
   int32_t c[U];
   float wt[U];
+  uint32_t dk[U];
+  if constexpr (DROP) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) dk[u] = uint32_t(a.drop_key[u < n ? e + u : end - 1]);
+  }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int32_t ee = u < n ? e + u : end - 1;
@@ -139,12 +150,16 @@ __device__ __forceinline__ void edge_block(const SpmmArgs& a, int32_t e, int32_t
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
-        const float m = WEIGHTED ? __fmul_rn(v[u][t][k], wt[u]) : v[u][t][k];
+        float m = v[u][t][k];
+        if constexpr (DROP)  // reference order: dropout(x_j W), then * norm (gcn_conv.py:237-248)
+          m = __fmul_rn(m, drop_scale(a.drop_seed, dk[u], uint32_t(a.f_base + fl[t] + k), a.drop_thresh,
+                                      a.drop_scale));
+        if constexpr (WEIGHTED) m = __fmul_rn(m, wt[u]);
         acc[t][k] = R::combine(acc[t][k], u < n ? R::msg(m) : R::init());
       }
 }
 
-template <int VEC, int NT, int RED, bool WEIGHTED>
+template <int VEC, int NT, int RED, bool WEIGHTED, bool DROP = false>
 __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
   using R = Reducer<RED>;
   constexpr int U = NT >= 4 ? 2 : (NT == 2 ? 4 : 8);
@@ -188,10 +203,10 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
       for (int k = 0; k < VEC; ++k) acc[t][k] = R::init();
 
     int32_t e = beg;
-    for (; e + U <= end; e += U) edge_block<U, VEC, NT, RED, WEIGHTED>(a, e, end, fl, acc);
+    for (; e + U <= end; e += U) edge_block<U, VEC, NT, RED, WEIGHTED, DROP>(a, e, end, fl, acc);
     // tail in half-width blocks: at most TU-1 clamped (redundant, cache-hit) loads
     constexpr int TU = U > 1 ? U / 2 : 1;
-    for (; e < end; e += TU) edge_block<TU, VEC, NT, RED, WEIGHTED>(a, e, end, fl, acc);
+    for (; e < end; e += TU) edge_block<TU, VEC, NT, RED, WEIGHTED, DROP>(a, e, end, fl, acc);
 
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -297,6 +312,9 @@ int launch_main(const SpmmArgs& a, hipStream_t s) {
   const int64_t work = a.items ? a.n_items : a.n_rows;
   if (work > 0) {
     auto k = spmm_kernel<VEC, NT, RED, W>;
+    if constexpr (RED == KGX_SUM) {
+      if (a.drop_key) k = spmm_kernel<VEC, NT, RED, W, true>;
+    }
     hipLaunchKernelGGL(k, dim3(resident_grid(k, work, a.G)), dim3(kBlock), 0, s, a);
     KGX_CHECK_LAUNCH();
   }
@@ -353,7 +371,8 @@ extern "C" int kgx_spmm(int reduce, int epilogue, const int32_t* rowptr, const i
                         const int32_t* items, int64_t n_items, const int32_t* split, int64_t n_split,
                         const int32_t* idx, const float* w, const float* table, int64_t ld_table, int64_t F,
                         float* out, int64_t ld_out, const float* bias, const float* xroot, int64_t ld_x,
-                        float gin_scale, float* partials, kgx_stream_t stream_) {
+                        float gin_scale, const int32_t* drop_key, float drop_p, uint64_t drop_seed,
+                        float* partials, kgx_stream_t stream_) {
   hipStream_t stream = as_stream(stream_);
   KGX_REQUIRE(reduce >= KGX_SUM && reduce <= KGX_STD, KGX_ERR_ARG, "kgx_spmm: unknown reduce %d", reduce);
   KGX_REQUIRE(epilogue >= KGX_EPI_NONE && epilogue <= KGX_EPI_RAW, KGX_ERR_ARG, "kgx_spmm: unknown epilogue %d",
@@ -364,6 +383,9 @@ extern "C" int kgx_spmm(int reduce, int epilogue, const int32_t* rowptr, const i
   KGX_REQUIRE(rowptr && rows && idx && table, KGX_ERR_ARG, "kgx_spmm: null CSR / table pointer");
   KGX_REQUIRE(epilogue != KGX_EPI_BIAS || bias, KGX_ERR_ARG, "kgx_spmm: EPI_BIAS needs bias");
   KGX_REQUIRE(epilogue != KGX_EPI_GIN || (xroot && ld_x >= F), KGX_ERR_ARG, "kgx_spmm: EPI_GIN needs xroot");
+  KGX_REQUIRE(!drop_key || (reduce == KGX_SUM && drop_p >= 0.0f && drop_p < 1.0f), KGX_ERR_ARG,
+              "kgx_spmm: message dropout needs reduce SUM and 0 <= p < 1 (got reduce %d, p %g)", reduce,
+              double(drop_p));
   const bool use_items = items != nullptr && reduce != KGX_STD;
   KGX_REQUIRE(!use_items || n_split == 0 || (split && partials), KGX_ERR_ARG,
               "kgx_spmm: split rows need split list and partials");
@@ -389,6 +411,12 @@ extern "C" int kgx_spmm(int reduce, int epilogue, const int32_t* rowptr, const i
     return h ? atoi(h) : 0;
   }();
   a.hints = hints;
+  if (drop_key && drop_p > 0.0f) {
+    a.drop_key = drop_key;
+    a.drop_seed = drop_seed;
+    a.drop_thresh = uint32_t(double(drop_p) * 4294967296.0);
+    a.drop_scale = 1.0f / (1.0f - drop_p);
+  }
 
   // widest vector the shapes and pointers allow
   auto ok = [&](int v) {
@@ -417,6 +445,7 @@ extern "C" int kgx_spmm(int reduce, int epilogue, const int32_t* rowptr, const i
     s.bias = bias ? bias + c0 : nullptr;
     s.xroot = xroot ? xroot + c0 : nullptr;
     s.partials = partials ? partials + c0 : nullptr;
+    s.f_base = int(c0);
     int rc;
     if (VEC == 4) rc = dispatch_nt<4>(nt, reduce, s, stream);
     else if (VEC == 2) rc = dispatch_nt<2>(nt, reduce, s, stream);

@@ -82,3 +82,35 @@ extern "C" int kgx_spmm_max_backward(int reduce, int raw, const int32_t* rowptr,
   KGX_CHECK_LAUNCH();
   return KGX_OK;
 }
+
+namespace kgx {
+namespace {
+
+__global__ __launch_bounds__(kBlock) void dropout_mask_kernel(uint64_t seed, uint32_t thresh, float keep_scale,
+                                                              const int32_t* __restrict__ keys, int64_t n,
+                                                              int64_t F, float* __restrict__ out) {
+  const int64_t total = n * F;
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  for (int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; t < total; t += stride) {
+    const int64_t i = t / F;
+    out[t] = drop_scale(seed, uint32_t(keys[i]), uint32_t(t - i * F), thresh, keep_scale);
+  }
+}
+
+}  // namespace
+}  // namespace kgx
+
+extern "C" int kgx_dropout_mask(uint64_t seed, float p, const int32_t* keys, int64_t n, int64_t F, float* out,
+                                kgx_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  KGX_REQUIRE(n >= 0 && F >= 0 && p >= 0.0f && p < 1.0f, KGX_ERR_ARG, "kgx_dropout_mask: bad arguments");
+  if (n == 0 || F == 0) return KGX_OK;
+  KGX_REQUIRE(keys && out, KGX_ERR_ARG, "kgx_dropout_mask: null pointer");
+  const uint32_t thresh = p > 0.0f ? uint32_t(double(p) * 4294967296.0) : 0u;
+  const float scale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
+  hipLaunchKernelGGL(dropout_mask_kernel, dim3(grid_for(n * F, 16384)), dim3(kBlock), 0, stream, seed, thresh, scale,
+                     keys, n, F, out);
+  KGX_CHECK_LAUNCH();
+  return KGX_OK;
+}
+

@@ -51,8 +51,9 @@ _SIGNATURES = {
     "kgx_spmm": [
         _int, _int, _i32p, _i32p, _i64, _i32p, _i64, _i32p, _i64,
         _i32p, _f32p, _f32p, _i64, _i64, _f32p, _i64,
-        _f32p, _f32p, _i64, ctypes.c_float, _f32p, ctypes.c_void_p,
+        _f32p, _f32p, _i64, ctypes.c_float, _i32p, ctypes.c_float, ctypes.c_uint64, _f32p, ctypes.c_void_p,
     ],
+    "kgx_dropout_mask": [ctypes.c_uint64, ctypes.c_float, _i32p, _i64, _i64, _f32p, ctypes.c_void_p],
     "kgx_spmm_gemm": [
         _int, _i32p, _i32p, _i64, _i32p, _i64, _i32p, _i64,
         _i32p, _f32p, _f32p, _i64, _i64, _f32p, _i64, _f32p, _int, ctypes.c_float,
@@ -65,12 +66,12 @@ _SIGNATURES = {
         _i32p, _i32p, _i64, _i32p, _i64, _i32p, _i64, _i32p, _f32p, _f32p, _i64, _f32p, _int, _int,
         ctypes.c_float, _f32p, _i64, _f32p, _f32p, _f32p, _i64,
         _i32p, _i32p, _i64, _i32p, _i64, _i32p, _i64, _i32p, _i32p,
-        _f32p, _f32p, _i64, _f32p, _f32p, _f32p, _f32p, ctypes.c_void_p,
+        _f32p, _f32p, _i64, _f32p, _f32p, _f32p, _f32p, _i32p, ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p,
     ],
     "kgx_gatv2": [
         _i32p, _i32p, _i64, _i32p, _i64, _i32p, _i64,
         _i32p, _f32p, _f32p, _i64, _f32p, _int, _int, ctypes.c_float,
-        _f32p, _i64, _f32p, _f32p, _f32p, ctypes.c_void_p,
+        _f32p, _i64, _f32p, _f32p, _f32p, _i32p, ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p,
     ],
     "kgx_gather_rows": [_f32p, _i64, _i32p, _i64, _i64, _f32p, _i64, ctypes.c_void_p],
     "kgx_scatter_f32": [_f32p, _i32p, _i64, _f32p, ctypes.c_void_p],

@@ -75,18 +75,13 @@ class GATv2Conv(MessagePassing):
             x, edge_index = inputs[0], inputs[1]
         else:
             raise ValueError(f"Expected inputs to be [x, edge_index], got {inputs}")
-        if training and self.dropout_rate > 0:
-            raise NotImplementedError(
-                "GATv2Conv attention dropout in training mode is not implemented by the kgx forward "
-                "engine (gatv2_conv.py:252-253); use dropout=0 or training=False."
-            )
         if isinstance(x, (list, tuple)):
             x_i = to_device_tensor(x[0], torch.float32)
             x_j = to_device_tensor(x[1], torch.float32, x_i.device)
         else:
             x_i = x_j = to_device_tensor(x, torch.float32)
         ei = edge_index_tensor(edge_index, x_i.device, allow_transpose=False)
-        return self._gatv2_propagate(x_i, x_j, ei, edge_index)
+        return self._gatv2_propagate(x_i, x_j, ei, edge_index, training=training)
 
     def propagate(self, x, edge_index, edge_attr=None, size=None, **kwargs):
         if isinstance(x, (list, tuple)):
@@ -97,7 +92,7 @@ class GATv2Conv(MessagePassing):
         ei = edge_index_tensor(edge_index, x_i.device, allow_transpose=False)
         return self._gatv2_propagate(x_i, x_j, ei, edge_index, self_loops=False)
 
-    def _gatv2_propagate(self, x_i, x_j, ei, edge_index_obj, self_loops: bool | None = None):
+    def _gatv2_propagate(self, x_i, x_j, ei, edge_index_obj, self_loops: bool | None = None, training=None):
         n, n_src = x_i.shape[0], x_j.shape[0]
         loops = self.add_self_loops_flag if self_loops is None else self_loops
         if loops and x_i is not x_j:
@@ -112,8 +107,11 @@ class GATv2Conv(MessagePassing):
         h_src = h_dst if x_j is x_i else self.linear_transform(x_j).contiguous()
         g = graph_for(edge_index_obj, ei, n_src, n, self_loops=loops, n_features=H * C)
         use_b = self.use_bias and self.bias is not None
+        drop = bool(training) and self.dropout_rate > 0  # attention dropout, gatv2_conv.py:252-253
         out = kops.gatv2_aggregate(g, h_src, h_dst, self.att, H, C, self.negative_slope,
-                                   bias=self.bias if (use_b and self.concat) else None, exact=self.exact)
+                                   bias=self.bias if (use_b and self.concat) else None, exact=self.exact,
+                                   dropout=self.dropout_rate if drop else 0.0,
+                                   seed=int(torch.randint(0, 2**62, (1,)).item()) if drop else 0)
         if not self.concat:
             out = out.view(n, H, C).mean(dim=1)
             if use_b:

@@ -4,10 +4,12 @@ Reference forward (gcn_conv.py:275-364): add self loops, norm_e =
 dinv[dst]*dinv[src], per-EDGE matmul x_j @ W (:233-235), * norm (:246),
 segment_sum (:79 forces "sum"), + bias (:266-272).
 
-kgx forward: H = x @ W once per NODE (GEMM, hipBLASLt on MFMA; per-edge and
-per-node products are the same dot products), then ONE fused kernel
-out_i = bias + sum_{e in CSR row i} H[col_e] * w_e with w_e the GCN norm in
-CSR order, accumulated sequentially in the reference's edge order.
+kgx forward (default): ONE fused kernel out = bias + (sum_e w_e x[col_e]) W
+(aggregate-then-transform, kgx_spmm_gemm).  EXACT mode / other shapes:
+H = x @ W once per NODE, then out_i = bias + sum_{e in CSR row i} H[col_e] * w_e
+in the reference's edge order.  Training with dropout_rate > 0: the same
+unfused order with every message element of H[col_e] dropped/scaled by a
+counter-based mask of (seed, edge, column) before the * norm (gcn_conv.py:237-242).
 """
 
 from __future__ import annotations
@@ -98,11 +100,7 @@ class GCNConv(MessagePassing):
         N = x.shape[0]
         if N == 0:
             return torch.zeros((0, self.output_dim), dtype=x.dtype, device=x.device)
-        if training and self.dropout_rate > 0:
-            raise NotImplementedError(
-                "GCNConv per-edge message dropout in training mode is not implemented by the kgx "
-                "forward engine (gcn_conv.py:238-242); use dropout_rate=0 or training=False."
-            )
+        drop = bool(training) and self.dropout_rate > 0  # gcn_conv.py:237-242
         n_edges = ei.shape[1] + (N if self.add_self_loops else 0)
         if n_edges == 0:  # gcn_conv.py:332-347
             out = torch.matmul(x, self.kernel)
@@ -110,6 +108,13 @@ class GCNConv(MessagePassing):
         g = graph_for(edge_index, ei, N, N, self_loops=self.add_self_loops, gcn_norm=self.normalize,
                       n_features=self.output_dim)
         use_b = self.use_bias and self.bias is not None
+        if drop:  # per-message dropout of x_j W: the unfused order (H = x W, then masked messages)
+            h = torch.matmul(x, self.kernel)
+            return kops.aggregate(
+                g, h, "sum", weighted=self.normalize,
+                epilogue=nat.EPI_BIAS if use_b else nat.EPI_NONE, bias=self.bias if use_b else None,
+                exact=self.exact, dropout=self.dropout_rate, seed=int(torch.randint(0, 2**62, (1,)).item()),
+            )
         if not self.exact and kops.fused_transform_supported(x.shape[1], self.output_dim):
             # aggregate-then-transform in one launch (W on f32 MFMA in the epilogue)
             return kops.aggregate_transform(g, x.contiguous(), self.kernel, "sum", weighted=self.normalize,

@@ -42,6 +42,9 @@ def spmm(
     bias: Optional[torch.Tensor],
     xroot: Optional[torch.Tensor],
     gin_scale: float,
+    drop_key: Optional[torch.Tensor] = None,
+    drop_p: float = 0.0,
+    drop_seed: int = 0,
 ) -> torch.Tensor:
     table = _f32c(table)
     w, bias, xroot = _f32c(w), _f32c(bias), _f32c(xroot)
@@ -63,6 +66,7 @@ def spmm(
             nat.ptr(idx), nat.ptr(w), nat.ptr(table), table.stride(0), F,
             nat.ptr(out), out.stride(0),
             nat.ptr(bias), nat.ptr(xroot), xroot.stride(0) if xroot is not None else 0, float(gin_scale),
+            nat.ptr(drop_key) if drop_p > 0 else None, float(drop_p), int(drop_seed) & (2**64 - 1),
             nat.ptr(partials), nat.stream(dev),
         ),
         "kgx_spmm",
@@ -71,7 +75,8 @@ def spmm(
 
 
 @spmm.register_fake
-def _spmm_fake(table, rowptr, rows, items, split, idx, w, n_slots, reduce, epilogue, bias, xroot, gin_scale):
+def _spmm_fake(table, rowptr, rows, items, split, idx, w, n_slots, reduce, epilogue, bias, xroot, gin_scale,
+               drop_key=None, drop_p=0.0, drop_seed=0):
     return table.new_empty((rowptr.shape[0] - 1, table.shape[1]))
 
 
@@ -206,7 +211,7 @@ def fused_transform_supported(f_in: int, f_out: int) -> bool:
 
 
 def _gatv2_impl(h_src, h_dst, rowptr, rows, items, split, col, att, heads, channels, negative_slope, bias,
-                n_slots, save_stats):
+                n_slots, save_stats, drop_key=None, drop_p=0.0, drop_seed=0):
     h_src, h_dst, att, bias = _f32c(h_src), _f32c(h_dst), _f32c(att), _f32c(bias)
     dev = nat.require_device(h_src, h_dst, rowptr, rows, col, att, bias, items, split)
     n_dst = rowptr.numel() - 1
@@ -225,7 +230,8 @@ def _gatv2_impl(h_src, h_dst, rowptr, rows, items, split, col, att, heads, chann
             nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, nat.ptr(split), n_split,
             nat.ptr(col), nat.ptr(h_src), nat.ptr(h_dst), h_src.stride(0), nat.ptr(att), heads, channels,
             float(negative_slope), nat.ptr(out), out.stride(0), nat.ptr(bias), nat.ptr(partials),
-            nat.ptr(stats) if save_stats else None, nat.stream(dev),
+            nat.ptr(stats) if save_stats else None, nat.ptr(drop_key) if drop_p > 0 else None, float(drop_p),
+            int(drop_seed) & (2**64 - 1), nat.stream(dev),
         ),
         "kgx_gatv2",
     )
@@ -247,15 +253,18 @@ def gatv2_save(
     negative_slope: float,
     bias: Optional[torch.Tensor],
     n_slots: int,
+    drop_key: Optional[torch.Tensor] = None,
+    drop_p: float = 0.0,
+    drop_seed: int = 0,
 ) -> tuple[torch.Tensor, torch.Tensor]:
     """kgx::gatv2 that also returns the per-row softmax statistics [n, 2*heads]."""
     return _gatv2_impl(h_src, h_dst, rowptr, rows, items, split, col, att, heads, channels, negative_slope, bias,
-                       n_slots, True)
+                       n_slots, True, drop_key, drop_p, drop_seed)
 
 
 @gatv2_save.register_fake
 def _gatv2_save_fake(h_src, h_dst, rowptr, rows, items, split, col, att, heads, channels, negative_slope, bias,
-                     n_slots):
+                     n_slots, drop_key=None, drop_p=0.0, drop_seed=0):
     n = rowptr.shape[0] - 1
     return h_src.new_empty((n, heads * channels)), h_src.new_empty((n, 2 * heads))
 
@@ -275,13 +284,17 @@ def gatv2(
     negative_slope: float,
     bias: Optional[torch.Tensor],
     n_slots: int,
+    drop_key: Optional[torch.Tensor] = None,
+    drop_p: float = 0.0,
+    drop_seed: int = 0,
 ) -> torch.Tensor:
     return _gatv2_impl(h_src, h_dst, rowptr, rows, items, split, col, att, heads, channels, negative_slope, bias,
-                       n_slots, False)[0]
+                       n_slots, False, drop_key, drop_p, drop_seed)[0]
 
 
 @gatv2.register_fake
-def _gatv2_fake(h_src, h_dst, rowptr, rows, items, split, col, att, heads, channels, negative_slope, bias, n_slots):
+def _gatv2_fake(h_src, h_dst, rowptr, rows, items, split, col, att, heads, channels, negative_slope, bias, n_slots,
+                drop_key=None, drop_p=0.0, drop_seed=0):
     return h_src.new_empty((rowptr.shape[0] - 1, heads * channels))
 
 
@@ -353,19 +366,24 @@ def _needs_grad(*ts) -> bool:
     return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts)
 
 
-def _aggregate_raw(g, table, red, weighted, by_edge, epilogue, bias, xroot, gin_scale, exact):
+def _aggregate_raw(g, table, red, weighted, by_edge, epilogue, bias, xroot, gin_scale, exact, drop_p=0.0,
+                   drop_seed=0):
     items, _, split, _, n_slots = g.work(exact or red == nat.STD)
     idx = g.eid if by_edge else g.col
     w = g.w if weighted else None
     if weighted and w is None:
         raise ValueError("graph was built without GCN normalisation weights")
+    if drop_p > 0 and red != nat.SUM:
+        raise ValueError("message dropout is implemented for sum aggregation (GCNConv) only")
     return _timed(lambda: torch.ops.kgx.spmm(
-        table, g.rowptr, g.rows, items, split, idx, w, n_slots, red, epilogue, bias, xroot, float(gin_scale)
+        table, g.rowptr, g.rows, items, split, idx, w, n_slots, red, epilogue, bias, xroot, float(gin_scale),
+        g.eid if drop_p > 0 else None, float(drop_p), int(drop_seed),
     ))
 
 
 def _reduce_backward(g: CSRGraph, red: int, weighted: bool, by_edge: bool, table: torch.Tensor | None,
-                     grad_out: torch.Tensor, exact: bool, table_rows: int, raw: bool = False) -> torch.Tensor:
+                     grad_out: torch.Tensor, exact: bool, table_rows: int, raw: bool = False, drop_p: float = 0.0,
+                     drop_seed: int = 0) -> torch.Tensor:
     """d loss / d table of REDUCE_{e in row} table[idx_e] (* w_e), given d loss / d out.
 
     sum / mean: the transposed aggregation (graph.transpose: each source row
@@ -401,18 +419,29 @@ def _reduce_backward(g: CSRGraph, red: int, weighted: bool, by_edge: bool, table
         gt = grad_out.new_zeros((table_rows, grad_out.shape[1]))
         gt.index_copy_(0, g.eid.long(), vals)
         return gt
-    t = G.transpose(g)
-    return _aggregate_raw(t, d, nat.SUM, weighted, False, nat.EPI_NONE, None, None, 1.0, exact)
+    t = G.transpose(g)  # t.eid = input edge ids: the same dropout mask keys as the forward
+    return _aggregate_raw(t, d, nat.SUM, weighted, False, nat.EPI_NONE, None, None, 1.0, exact, drop_p, drop_seed)
+
+
+def dropout_mask(seed: int, p: float, keys: torch.Tensor, F: int) -> torch.Tensor:
+    """The multipliers (0 or 1/(1-p)) kgx's message dropout applies: [len(keys), F]."""
+    keys = keys.to(torch.int32).contiguous()
+    out = torch.empty((keys.numel(), F), dtype=torch.float32, device=keys.device)
+    nat.check(nat.lib().kgx_dropout_mask(int(seed) & (2**64 - 1), float(p), nat.ptr(keys), keys.numel(), F,
+                                         nat.ptr(out), nat.stream(keys.device)), "kgx_dropout_mask")
+    return out
 
 
 class _AggregateFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, table, bias, xroot, g, red, weighted, by_edge, epilogue, gin_scale, exact):
+    def forward(ctx, table, bias, xroot, g, red, weighted, by_edge, epilogue, gin_scale, exact, drop_p, drop_seed):
         ctx.g, ctx.red, ctx.weighted, ctx.by_edge = g, red, weighted, by_edge
         ctx.epilogue, ctx.gin_scale, ctx.exact = epilogue, gin_scale, exact
+        ctx.drop_p, ctx.drop_seed = drop_p, drop_seed
         ctx.table_rows = table.shape[0]
         ctx.save_for_backward(table if red in (nat.MAX, nat.MIN) else None)
-        return _aggregate_raw(g, table, red, weighted, by_edge, epilogue, bias, xroot, gin_scale, exact)
+        return _aggregate_raw(g, table, red, weighted, by_edge, epilogue, bias, xroot, gin_scale, exact, drop_p,
+                              drop_seed)
 
     @staticmethod
     def backward(ctx, grad_out):
@@ -420,12 +449,13 @@ class _AggregateFn(torch.autograd.Function):
         g_table = g_bias = g_xroot = None
         if ctx.needs_input_grad[0]:
             g_table = _reduce_backward(ctx.g, ctx.red, ctx.weighted, ctx.by_edge, table, grad_out, ctx.exact,
-                                       ctx.table_rows, raw=ctx.epilogue == nat.EPI_RAW)
+                                       ctx.table_rows, raw=ctx.epilogue == nat.EPI_RAW, drop_p=ctx.drop_p,
+                                       drop_seed=ctx.drop_seed)
         if ctx.needs_input_grad[1] and ctx.epilogue == nat.EPI_BIAS:
             g_bias = grad_out.sum(0)
         if ctx.needs_input_grad[2] and ctx.epilogue == nat.EPI_GIN:
             g_xroot = grad_out * ctx.gin_scale
-        return g_table, g_bias, g_xroot, None, None, None, None, None, None, None
+        return g_table, g_bias, g_xroot, None, None, None, None, None, None, None, None, None
 
 
 def aggregate(
@@ -440,18 +470,27 @@ def aggregate(
     xroot: torch.Tensor | None = None,
     gin_scale: float = 1.0,
     exact: bool = False,
+    dropout: float = 0.0,
+    seed: int = 0,
 ) -> torch.Tensor:
     """out[i] = EPI(REDUCE_{e in row i} table[idx[e]] * (w[e] if weighted)).
 
     by_edge=False gathers node rows through `col` (the fused propagate path);
     by_edge=True gathers rows of a per-edge message tensor through `eid`
     (the reference's Aggregator.aggregate(messages, target_idx, dim_size)).
-    Differentiable in table, bias and xroot (sum, mean, max, min).
+    Differentiable in table, bias and xroot (sum, mean, max, min).  dropout > 0
+    (sum only): every message element is kept with probability 1 - dropout and
+    scaled by 1/(1 - dropout), the mask a function of (seed, input edge id,
+    column) -- GCNConv's training-time message dropout (gcn_conv.py:237-242).
     """
     red = _reduce_id(reduce)
+    if dropout and by_edge:
+        raise ValueError("message dropout applies to gathered node rows, not to message tensors")
     if _needs_grad(table, bias, xroot):
-        return _AggregateFn.apply(table, bias, xroot, g, red, weighted, by_edge, epilogue, float(gin_scale), exact)
-    return _aggregate_raw(g, table, red, weighted, by_edge, epilogue, bias, xroot, gin_scale, exact)
+        return _AggregateFn.apply(table, bias, xroot, g, red, weighted, by_edge, epilogue, float(gin_scale), exact,
+                                  float(dropout), int(seed))
+    return _aggregate_raw(g, table, red, weighted, by_edge, epilogue, bias, xroot, gin_scale, exact, float(dropout),
+                          int(seed))
 
 
 def _aggregate_transform_raw(g, x, W, red, weighted, bias, pre_gin, gin_scale, exact):
@@ -561,11 +600,11 @@ def aggregate_transform(
     return _aggregate_transform_raw(g, x, W, red, weighted, bias, pre_gin, gin_scale, exact)
 
 
-def _gatv2_raw(g, h_src, h_dst, att, heads, channels, negative_slope, bias, exact):
+def _gatv2_raw(g, h_src, h_dst, att, heads, channels, negative_slope, bias, exact, drop_p=0.0, drop_seed=0):
     items, _, split, _, n_slots = g.work(exact)
     return _timed(lambda: torch.ops.kgx.gatv2(
         h_src, h_dst, g.rowptr, g.rows, items, split, g.col, att.reshape(-1), heads, channels,
-        float(negative_slope), bias, n_slots,
+        float(negative_slope), bias, n_slots, g.eid if drop_p > 0 else None, float(drop_p), int(drop_seed),
     ))
 
 
@@ -576,12 +615,13 @@ class _GATv2Fn(torch.autograd.Function):
     over the transposed CSR, both with hub rows split into chunks."""
 
     @staticmethod
-    def forward(ctx, h_src, h_dst, att, bias, g, heads, channels, negative_slope, exact):
+    def forward(ctx, h_src, h_dst, att, bias, g, heads, channels, negative_slope, exact, drop_p, drop_seed):
         ctx.g, ctx.heads, ctx.channels, ctx.slope, ctx.exact = g, heads, channels, float(negative_slope), exact
+        ctx.drop_p, ctx.drop_seed = drop_p, drop_seed
         items, _, split, _, n_slots = g.work(exact)
         out, stats = _timed(lambda: torch.ops.kgx.gatv2_save(
             h_src, h_dst, g.rowptr, g.rows, items, split, g.col, att.reshape(-1), heads, channels,
-            float(negative_slope), bias, n_slots,
+            float(negative_slope), bias, n_slots, g.eid if drop_p > 0 else None, float(drop_p), int(drop_seed),
         ))
         ctx.save_for_backward(h_src, h_dst, att, bias, out, stats)
         return out
@@ -620,12 +660,14 @@ class _GATv2Fn(torch.autograd.Function):
                 ctx.slope, nat.ptr(out), out.stride(0), nat.ptr(bias), nat.ptr(stats), nat.ptr(grad_out),
                 grad_out.stride(0), nat.ptr(t.rowptr), nat.ptr(t.rows), g.n_src, nat.ptr(t_items), t_n_items,
                 nat.ptr(t_split), t_n_split, nat.ptr(t.col), nat.ptr(slot), nat.ptr(g_src), nat.ptr(g_dst),
-                g_src.stride(0), nat.ptr(g_att), nat.ptr(alpha), nat.ptr(ds), nat.ptr(partials), nat.stream(dev),
+                g_src.stride(0), nat.ptr(g_att), nat.ptr(alpha), nat.ptr(ds), nat.ptr(partials),
+                nat.ptr(g.eid) if ctx.drop_p > 0 else None, float(ctx.drop_p), int(ctx.drop_seed) & (2**64 - 1),
+                nat.stream(dev),
             ),
             "kgx_gatv2_backward",
         )
         g_bias = grad_out.sum(0) if ctx.needs_input_grad[3] else None
-        return g_src, g_dst, g_att.view(att.shape), g_bias, None, None, None, None, None
+        return g_src, g_dst, g_att.view(att.shape), g_bias, None, None, None, None, None, None, None
 
 
 def gatv2_aggregate(
@@ -638,8 +680,12 @@ def gatv2_aggregate(
     negative_slope: float,
     bias: torch.Tensor | None = None,
     exact: bool = False,
+    dropout: float = 0.0,
+    seed: int = 0,
 ) -> torch.Tensor:
-    """Fused GATv2 attention aggregation; differentiable in h_src, h_dst, att, bias."""
+    """Fused GATv2 attention aggregation; differentiable in h_src, h_dst, att, bias.
+    dropout > 0: attention dropout of alpha per (edge, head), mask of (seed, input edge id, head)."""
     if _needs_grad(h_src, h_dst, att, bias):
-        return _GATv2Fn.apply(h_src, h_dst, att, bias, g, heads, channels, negative_slope, exact)
-    return _gatv2_raw(g, h_src, h_dst, att, heads, channels, negative_slope, bias, exact)
+        return _GATv2Fn.apply(h_src, h_dst, att, bias, g, heads, channels, negative_slope, exact, float(dropout),
+                              int(seed))
+    return _gatv2_raw(g, h_src, h_dst, att, heads, channels, negative_slope, bias, exact, float(dropout), int(seed))

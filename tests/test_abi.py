@@ -42,7 +42,7 @@ def test_binding_covers_header(lib):
 def test_version_and_error_channel(lib):
     assert lib.kgx_version() == 1
     rc = lib.kgx_spmm(99, 0, None, None, 1, None, 0, None, 0, None, None, None, 1, 1, None, 1, None, None, 0,
-                      1.0, None, None)
+                      1.0, None, 0.0, 0, None, None)
     assert rc == 1  # KGX_ERR_ARG, no device touched
     assert b"unknown reduce" in lib.kgx_last_error()
 
@@ -60,8 +60,13 @@ def test_argument_validation_without_device(lib):
     # unsupported GAT shape (too many lanes per row) is reported, not launched
     rc = lib.kgx_gatv2(ctypes.c_void_p(16), ctypes.c_void_p(16), 1, None, 0, None, 0, ctypes.c_void_p(16),
                        ctypes.c_void_p(16), ctypes.c_void_p(16), 64 * 33, ctypes.c_void_p(16), 64, 33, 0.2,
-                       ctypes.c_void_p(16), 64 * 33, None, None, None, None)
+                       ctypes.c_void_p(16), 64 * 33, None, None, None, None, 0.0, 0, None)
     assert rc == 4
+    # message dropout only for sums, p in [0, 1)
+    rc = lib.kgx_spmm(2, 0, ctypes.c_void_p(16), ctypes.c_void_p(16), 1, None, 0, None, 0, ctypes.c_void_p(16), None,
+                      ctypes.c_void_p(16), 4, 4, ctypes.c_void_p(16), 4, None, None, 0, 1.0, ctypes.c_void_p(16), 0.5,
+                      1, None, None)
+    assert rc == 1 and b"dropout" in lib.kgx_last_error()
     # backward of max/min only; fused accumulate flag validation
     assert lib.kgx_spmm_max_backward(0, 0, None, 0, None, None, 0, 0, None, 0, None, 0, None) == 1
     # rmat argument checks

@@ -119,6 +119,21 @@ def ns_both(n=10_000_000, e=100_000_000, f=128):
                       "TBps_alg": round(b_alg(n, g.kept, f) / ms / 1e9, 3)}), flush=True)
 
 
+def gat_once(n=1_000_000, e=10_000_000, H=8, C=16):
+    """C3-shaped GATv2 aggregation timing with the library named by KGX_LIB."""
+    import os
+
+    dev = torch.device("cuda", 0)
+    ei = synthetic.rmat_edge_index(n, e, seed=0, device=dev)
+    g = G.build_csr(ei[0].contiguous(), ei[1].contiguous(), n, n, self_loops=True)
+    h = torch.randn(n, H * C, device=dev)
+    att = torch.randn(H * C, device=dev)
+    ms = timeit(lambda: kops.gatv2_aggregate(g, h, h, att, H, C, 0.2), reps=20)
+    b = 4 * (n + 1) + g.kept * (4 + 4 * H * C) + 8 * n * H * C
+    print(json.dumps({"lib": os.path.basename(os.environ.get("KGX_LIB", "libkgx.so")), "gat_ms": round(ms, 4),
+                      "TBps_alg": round(b / ms / 1e9, 3)}), flush=True)
+
+
 def ab(specs, rounds=2):
     """A/B over library variants / env knobs, each in its own process, interleaved.
     spec = "libname[:KEY=VAL,...]" with libname "main" or a lib/variants/libkgx_<name>.so.
@@ -135,7 +150,7 @@ def ab(specs, rounds=2):
             for item in filter(None, kv.split(",")):
                 k, _, v = item.partition("=")
                 env[k] = v
-            res = subprocess.run([sys.executable, __file__, "both"], env=env, timeout=300,
+            res = subprocess.run([sys.executable, __file__, os.environ.get("KGX_AB_WORK", "both")], env=env, timeout=300,
                                  capture_output=True, text=True)
             line = " | ".join(res.stdout.strip().splitlines()[-2:]) if res.stdout.strip() else res.stderr[-2000:]
             print(f"round{r} {spec}: {line}", flush=True)
@@ -147,4 +162,4 @@ if __name__ == "__main__":
     if sys.argv[1] == "ab":
         ab(sys.argv[2:])
     else:
-        {"sweep": sweep, "calib": calib, "ns": ns_once, "both": ns_both}[sys.argv[1]]()
+        {"sweep": sweep, "calib": calib, "ns": ns_once, "both": ns_both, "gat": gat_once}[sys.argv[1]]()
