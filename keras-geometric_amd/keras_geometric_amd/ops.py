@@ -395,7 +395,27 @@ def _reduce_backward(g: CSRGraph, red: int, weighted: bool, by_edge: bool, table
 
     grad_out = grad_out.contiguous()
     if red == nat.STD:
-        raise NotImplementedError("kgx: backward of the std aggregation is not implemented")
+        # std_i = sqrt(ssd_i / n_i) (0 where n_i <= 1), aggregators.py:182-228:
+        #   d std_i / d m_e = (m_e - mean_i) / (n_i std_i)   (the mean's own path sums to 0)
+        # so with A_i = g_i / (n_i std_i) (0 where n_i <= 1):
+        #   grad m_e = A_i (m_e - mean_i);  grad x_j = x_j * (A^T A)_j - (A^T (A * mean))_j
+        std = _aggregate_raw(g, table, nat.STD, False, by_edge, nat.EPI_NONE, None, None, 1.0, True)
+        mean = _aggregate_raw(g, table, nat.MEAN, False, by_edge, nat.EPI_NONE, None, None, 1.0, True)
+        # As torch autograd of the reference: the count <= 1 guard's where() sends 0 into
+        # sqrt'(0) = inf, so rows with one message (and zero-variance rows) yield NaN.
+        count = torch.clamp(g.deg, max=1 << 24).float().unsqueeze(1)
+        A = grad_out / (torch.clamp(count, min=1e-8) * std)
+        A = torch.where(count > 1, A, torch.full_like(A, float("nan")))
+        if by_edge:
+            rows = G.row_of_slot(g).long()
+            gt = grad_out.new_zeros((table_rows, grad_out.shape[1]))
+            gt.index_copy_(0, g.eid.long(), A.index_select(0, rows) * (table.index_select(0, g.eid.long())
+                                                                       - mean.index_select(0, rows)))
+            return gt
+        t = G.transpose(g)
+        sa = _aggregate_raw(t, A.contiguous(), nat.SUM, False, False, nat.EPI_NONE, None, None, 1.0, exact)
+        sb = _aggregate_raw(t, (A * mean).contiguous(), nat.SUM, False, False, nat.EPI_NONE, None, None, 1.0, exact)
+        return table * sa - sb
     if red in (nat.MAX, nat.MIN):
         table = table.contiguous()
         gt = torch.zeros_like(table)
@@ -439,7 +459,7 @@ class _AggregateFn(torch.autograd.Function):
         ctx.epilogue, ctx.gin_scale, ctx.exact = epilogue, gin_scale, exact
         ctx.drop_p, ctx.drop_seed = drop_p, drop_seed
         ctx.table_rows = table.shape[0]
-        ctx.save_for_backward(table if red in (nat.MAX, nat.MIN) else None)
+        ctx.save_for_backward(table if red in (nat.MAX, nat.MIN, nat.STD) else None)
         return _aggregate_raw(g, table, red, weighted, by_edge, epilogue, bias, xroot, gin_scale, exact, drop_p,
                               drop_seed)
 

@@ -214,14 +214,40 @@ def test_transpose_graph(dev):
     np.testing.assert_array_equal(t.deg.cpu().numpy(), np.bincount(src, minlength=N))
 
 
-def test_std_backward_raises(dev):
-    N = 300
-    ei = _graph(N, 2000, seed=22)
+def assert_tol_nan(a, b, tol=1e-5):
+    """NaN in the same places, then the tolerance elsewhere."""
+    a = a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else a
+    b = b.detach().cpu().numpy() if isinstance(b, torch.Tensor) else b
+    np.testing.assert_array_equal(np.isnan(a), np.isnan(b))
+    ok = ~np.isnan(b)
+    assert_tol(a[ok], b[ok], tol)
+
+
+@pytest.mark.parametrize("by_edge", [False, True])
+def test_std_backward(dev, by_edge):
+    """std aggregation (aggregators.py:182-228) gradient vs oracle autograd,
+    including the reference's NaNs: its count <= 1 guard is a where() after a
+    sqrt, so rows with one message send 0 * inf = NaN to that message."""
+    N, F = 600, 8
+    ei = _graph(N, 5000, seed=22)
+    gout = _x(N, F, 24)
+    if by_edge:
+        msg = _x(ei.shape[1], F, 23)
+        g = G.build_csr(T(ei[0]).to(dev), T(ei[1]).to(dev), N, N, segment_only=True)
+        md = T(msg).to(dev).requires_grad_(True)
+        kops.aggregate(g, md, "std", by_edge=True).backward(T(gout).to(dev))
+        mr = T(msg).requires_grad_(True)
+        R.aggregate("std", mr, T(ei[1]), N).backward(T(gout))
+        assert_tol_nan(md.grad, mr.grad, tol=1e-4)  # ill-conditioned where std is small
+        assert np.isnan(mr.grad.numpy()).any()  # the fixture exercises the single-message rows
+        return
+    x = _x(N, F, 23)
     g = G.build_csr(T(ei[0]).to(dev), T(ei[1]).to(dev), N, N)
-    xd = T(_x(N, 8, 23)).to(dev).requires_grad_(True)
-    y = kops.aggregate(g, xd, "std")
-    with pytest.raises(NotImplementedError):
-        y.sum().backward()
+    xd = T(x).to(dev).requires_grad_(True)
+    kops.aggregate(g, xd, "std").backward(T(gout).to(dev))
+    xr = T(x).requires_grad_(True)
+    R.propagate(xr, T(ei), "std").backward(T(gout))
+    assert_tol_nan(xd.grad, xr.grad, tol=1e-4)
 
 
 @pytest.mark.parametrize("heads,C,concat", [(8, 16, True), (2, 5, True), (4, 8, False)])
