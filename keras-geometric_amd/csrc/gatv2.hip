@@ -51,9 +51,22 @@ struct GatArgs {
   int G, lgG, LH, lgLH;
 };
 
+// Sum over the LH (power of two) lanes of a head, result in every lane.
+// Within 16 lanes the exchanges are DPP moves (VALU, no LDS round trip):
+// quad_perm xor 1 and xor 2, then row_half_mirror (lane i <-> 7-i) and
+// row_mirror (i <-> 15-i) pair each lane with one holding the other half's sum.
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
 template <int K>
 __device__ __forceinline__ float head_reduce(float p, int LH) {
-  for (int o = 1; o < LH; o <<= 1) p += __shfl_xor(p, o, 64);
+  if (LH > 1) p += dpp<0xB1>(p);   // quad_perm [1,0,3,2]
+  if (LH > 2) p += dpp<0x4E>(p);   // quad_perm [2,3,0,1]
+  if (LH > 4) p += dpp<0x141>(p);  // row_half_mirror
+  if (LH > 8) p += dpp<0x140>(p);  // row_mirror
+  if (LH > 16) p += __shfl_xor(p, 16, 64);
+  if (LH > 32) p += __shfl_xor(p, 32, 64);
   return p;
 }
 
