@@ -162,7 +162,12 @@ __device__ __forceinline__ void edge_block(const SpmmArgs& a, int32_t e, int32_t
 template <int VEC, int NT, int RED, bool WEIGHTED, bool DROP = false>
 __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
   using R = Reducer<RED>;
-  constexpr int U = NT >= 4 ? 2 : (NT == 2 ? 4 : 8);
+  // gathers in flight per group (NT = 1: 6 measured best at NS, 9.2-9.4 ms vs 9.5 at 8, 9.9 at 12)
+#ifdef KGX_SPMM_U
+  constexpr int U = NT >= 4 ? 2 : (NT == 2 ? 4 : KGX_SPMM_U);
+#else
+  constexpr int U = NT >= 4 ? 2 : (NT == 2 ? 4 : 6);
+#endif
   const int G = a.G;
   const int lane = threadIdx.x & (G - 1);
   const int64_t ngroups = (int64_t(gridDim.x) * kBlock) >> a.lgG;
