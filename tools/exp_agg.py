@@ -104,7 +104,8 @@ def ns_both(n=10_000_000, e=100_000_000, f=128):
     ei = synthetic.rmat_edge_index(n, e, seed=0, device=dev)
     h = torch.randn(n, f, device=dev)
     W = torch.randn(f, f, device=dev) * (1.0 / f) ** 0.5
-    g = G.build_csr(ei[0].contiguous(), ei[1].contiguous(), n, n, self_loops=True, gcn_norm=True)
+    split = int(os.environ.get("KGX_EXP_SPLIT", "0")) or None
+    g = G.build_csr(ei[0].contiguous(), ei[1].contiguous(), n, n, self_loops=True, gcn_norm=True, split_len=split)
     if os.environ.get("KGX_EXP_SORT"):  # experiment: exact descending-degree item order (stable)
         it = g.items
         pre = int((it[:, 3] >= 0).sum())
