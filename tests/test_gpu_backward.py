@@ -278,3 +278,53 @@ def test_gatv2_layer_backward(dev, heads, C, concat):
     assert_tol(layer.att.grad, ar.grad, tol=1e-5 * np.sqrt(N))
     assert_tol(layer.bias.grad, br.grad, tol=1e-5 * np.sqrt(N))
     assert_tol(layer.linear_transform.kernel.grad, kr.grad, tol=1e-5 * np.sqrt(N))
+
+
+@pytest.mark.parametrize("aggr", ["sum", "max"])
+def test_backward_bipartite_wide_noncontiguous(dev, aggr):
+    """Bipartite propagate (n_src != n_dst), F > 1024 (column-sliced launches)
+    and a non-contiguous feature view, through the transposed-graph / max
+    backward paths."""
+    from keras_geometric_amd.layers import MessagePassing
+
+    n_dst, n_src, F, E = 300, 700, 1100, 5000
+    rng = np.random.default_rng(31)
+    ei = np.stack([rng.integers(0, n_src, E), rng.integers(0, n_dst, E)]).astype(np.int32)
+    xs = rng.standard_normal((F, n_src)).astype(np.float32)  # stored transposed -> non-contiguous view
+    xd_dst = rng.standard_normal((n_dst, F)).astype(np.float32)
+    gout = rng.standard_normal((n_dst, F)).astype(np.float32)
+    src_t = T(xs).to(dev).requires_grad_(True)
+    mp = MessagePassing(aggregator=aggr, exact=True)
+    y = mp.propagate((T(xd_dst).to(dev), src_t.t()), T(ei).to(dev))
+    y.backward(T(gout).to(dev))
+    xr = T(xs).requires_grad_(True)
+    yr = R.propagate(None, T(ei), aggr, x_pair=(T(xd_dst), xr.t()))
+    yr.backward(T(gout))
+    assert_tol(y, yr)
+    assert_tol(src_t.grad, xr.grad)
+
+
+@pytest.mark.parametrize("loops,norm", [(False, True), (True, False), (False, False)])
+def test_gcn_backward_flags(dev, loops, norm):
+    N, F = 500, 128
+    ei = _graph(N, 4000, seed=32)
+    x, gout = _x(N, F, 33), _x(N, 64, 34)
+    # without the symmetric normalisation (or with the 1e6 dinv of zero-in-degree
+    # nodes when loops are off) the sums are large and cancel: bound-based check
+    layer = GCNConv(64, add_self_loops=loops, normalize=norm)
+    xd = T(x).to(dev).requires_grad_(True)
+    layer([xd, T(ei).to(dev)])
+    W, b = (t.detach().cpu() for t in layer.weights)
+    y = layer([xd, T(ei).to(dev)])
+    y.backward(T(gout).to(dev))
+    xr, Wr, br = T(x).requires_grad_(True), W.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = R.gcn_forward(xr, T(ei), Wr, br, loops, norm)
+    yr.backward(T(gout))
+    # error bound of a re-ordered fp32 sum: relative to the same computation on |terms|
+    # (the forward and both gradients are linear in x, W with non-negative norms)
+    xa, Wa, ba = (t.abs().clone().requires_grad_(True) for t in (T(x), W, b))
+    ya = R.gcn_forward(xa, T(ei), Wa, ba, loops, norm)
+    ya.backward(T(np.abs(gout)))
+    assert_tol_scaled(y, yr, ya)
+    assert_tol_scaled(xd.grad, xr.grad, xa.grad)
+    assert_tol_scaled(layer.kernel.grad, Wr.grad, Wa.grad)
