@@ -119,10 +119,23 @@ def main() -> None:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}; launch N>1 with torch.distributed.run")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # KGX_BENCH_REHEARSAL=1 (test only, one-GPU box): all ranks share cuda:0 and
+    # the exchange is staged through host memory over gloo -- exercises the N>1
+    # control flow and halo plumbing where RCCL cannot run (one GPU); never a
+    # measurement.
+    rehearsal = os.environ.get("KGX_BENCH_REHEARSAL", "0") == "1"
+    gpu = 0 if rehearsal else local_rank
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    comm = None
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearsal:
+            dist.init_process_group("gloo")
+            from keras_geometric_amd.distributed import HostStagedComm
+
+            comm = HostStagedComm()
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     import keras_geometric_amd as kgx
     from keras_geometric_amd import ops as kops
@@ -159,7 +172,7 @@ def main() -> None:
 
         log(f"world={world}: generating shards of R-MAT N={n_local * world} E={e_local * world}")
         t0 = time.perf_counter()
-        sg = kd.ShardedGraph.rmat(n_local * world, e_local * world, seed=args.seed, device=dev,
+        sg = kd.ShardedGraph.rmat(n_local * world, e_local * world, seed=args.seed, device=dev, comm=comm,
                                   self_loops=True, gcn_norm=True, exact=args.exact)
         x = torch.randn(sg.n_local, f_in, device=dev)
         layer = kd.ShardedGCNConv(f_out, sg)
@@ -196,10 +209,11 @@ def main() -> None:
     launches = len(events) // args.steps
 
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], device=dev, dtype=torch.float64)
+        rdev = torch.device("cpu") if rehearsal else dev
+        t = torch.tensor([elapsed, kern_ms], device=rdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
-        tot = torch.tensor([e_agg], device=dev, dtype=torch.float64)
+        tot = torch.tensor([e_agg], device=rdev, dtype=torch.float64)
         dist.all_reduce(tot)
         e_total = float(tot[0])
     else:
@@ -269,6 +283,8 @@ def main() -> None:
         result["cpu_baseline"] = cpu_baseline(dev, "")
     elif rank == 0:
         result["cpu_baseline"] = None
+    if rehearsal:
+        result["data"] += " [REHEARSAL: ranks share one GPU, host-staged gloo exchange -- not a measurement]"
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

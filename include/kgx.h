@@ -183,7 +183,9 @@ int kgx_dropout_mask(uint64_t seed, float p, const int32_t* keys, int64_t n, int
  * agg_out (optional, [n, ld_agg >= F_in]): also store PRE(REDUCE(...)), the
  * rows before the transform — what the backward's dW = agg^T dOut needs.
  * ------------------------------------------------------------------------- */
-enum { KGX_FUSED_PRE_GIN = 1, KGX_FUSED_ACCUMULATE = 2 };
+/* KGX_FUSED_SHARE_GPU: launch 7/8 of the resident grid, leaving block slots
+ * for kernels of a concurrent stream (the sharded layer's RCCL exchange). */
+enum { KGX_FUSED_PRE_GIN = 1, KGX_FUSED_ACCUMULATE = 2, KGX_FUSED_SHARE_GPU = 4 };
 int kgx_spmm_gemm(int reduce, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
                   const int32_t* items, int64_t n_items, const int32_t* split, int64_t n_split,
                   const int32_t* idx, const float* w, const float* x, int64_t ld_x, int64_t F_in,

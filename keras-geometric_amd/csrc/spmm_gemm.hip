@@ -65,6 +65,7 @@ struct FusedArgs {
   int64_t ld_agg;
   int pre_gin;      // apply gin_scale * x[row] + aggr before the transform
   int accumulate;   // out += result
+  int share_gpu;    // launch 7/8 of the resident grid
   float gin_scale;
   int debug;        // experiment knob (KGX_FUSED_DEBUG): 1 skip the MFMA phase, 2 skip stores
 };
@@ -407,7 +408,9 @@ int launch(const FusedArgs& a, hipStream_t s) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, 0) != hipSuccess || per_cu <= 0)
       per_cu = 2;
     const int64_t need = (work + kGroups - 1) / kGroups;
-    const int64_t cap = int64_t(per_cu) * cus;
+    // KGX_FUSED_SHARE_GPU: leave an eighth of the block slots free so a
+    // concurrent collective's kernels (RCCL halo all-to-all) are not starved
+    const int64_t cap = a.share_gpu ? int64_t(per_cu) * cus * 7 / 8 : int64_t(per_cu) * cus;
     hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kThreads), 0, s, a);
     KGX_CHECK_LAUNCH();
   }
@@ -438,7 +441,7 @@ extern "C" int kgx_spmm_gemm(int reduce, const int32_t* rowptr, const int32_t* r
   KGX_REQUIRE(F_out > 0 && F_out <= 128 && F_out % 16 == 0, KGX_ERR_UNSUPPORTED,
               "kgx_spmm_gemm: F_out must be a multiple of 16 <= 128 (got %lld)", (long long)F_out);
   KGX_REQUIRE(n_rows >= 0 && n_items >= 0 && n_split >= 0, KGX_ERR_ARG, "kgx_spmm_gemm: negative size");
-  KGX_REQUIRE((flags & ~(KGX_FUSED_PRE_GIN | KGX_FUSED_ACCUMULATE)) == 0, KGX_ERR_ARG,
+  KGX_REQUIRE((flags & ~(KGX_FUSED_PRE_GIN | KGX_FUSED_ACCUMULATE | KGX_FUSED_SHARE_GPU)) == 0, KGX_ERR_ARG,
               "kgx_spmm_gemm: unknown flags 0x%x", flags);
   KGX_REQUIRE(!agg_out || (ld_agg >= F_in && reinterpret_cast<uintptr_t>(agg_out) % 16 == 0 && ld_agg % 4 == 0),
               KGX_ERR_ARG, "kgx_spmm_gemm: agg_out must be 16-byte aligned with ld >= F_in, ld %% 4 == 0");
@@ -470,6 +473,7 @@ extern "C" int kgx_spmm_gemm(int reduce, const int32_t* rowptr, const int32_t* r
   a.ld_agg = ld_agg;
   a.pre_gin = (flags & KGX_FUSED_PRE_GIN) != 0;
   a.accumulate = (flags & KGX_FUSED_ACCUMULATE) != 0;
+  a.share_gpu = (flags & KGX_FUSED_SHARE_GPU) != 0;
   a.gin_scale = gin_scale;
   static const int dbg = [] {
     const char* h = getenv("KGX_FUSED_DEBUG");

@@ -105,6 +105,26 @@ class TorchComm:
         dist.broadcast(t, src=src, group=self.group)
 
 
+class HostStagedComm(TorchComm):
+    """Exchange staged through host memory over a gloo group: for rehearsing the
+    multi-rank path where RCCL cannot run (ranks sharing one GPU).  Not a
+    product path -- bench.py only uses it under KGX_BENCH_REHEARSAL=1."""
+
+    def all_to_all_single(self, out, inp, out_splits=None, in_splits=None) -> None:
+        o = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=self.group)
+        out.copy_(o)
+
+    def all_to_all_start(self, out, inp, out_splits=None, in_splits=None):
+        self.all_to_all_single(out, inp, out_splits, in_splits)
+        return None
+
+    def broadcast(self, t, src: int = 0) -> None:
+        h = t.detach().cpu()
+        dist.broadcast(h, src=src, group=self.group)
+        t.copy_(h)
+
+
 def equal_bounds(n_global: int, world: int) -> list[int]:
     base, rem = divmod(n_global, world)
     b = [0]
@@ -323,7 +343,8 @@ class ShardedGCNConv(Layer):
         halo = sg.halo_buffer(x_local.shape[1], x_local)
         with torch.no_grad():
             work = sg.start_halo_exchange(x_local, halo)
-            out = sg.backend.aggregate_transform(g_own, x_local, self.kernel, bias=bias)
+            with kops.sharing_gpu():  # the exchange's RCCL kernels run beside this pass
+                out = sg.backend.aggregate_transform(g_own, x_local, self.kernel, bias=bias)
             if work is not None:
                 work.wait()
             if g_halo.kept:

@@ -80,6 +80,21 @@ def _spmm_fake(table, rowptr, rows, items, split, idx, w, n_slots, reduce, epilo
     return table.new_empty((rowptr.shape[0] - 1, table.shape[1]))
 
 
+# Launch hint (results unchanged): while set, fused launches leave 1/8 of the
+# block slots free for a concurrent collective (distributed.py's own-source pass).
+_SHARE_GPU = False
+
+
+class sharing_gpu:
+    def __enter__(self):
+        global _SHARE_GPU
+        self._old, _SHARE_GPU = _SHARE_GPU, True
+
+    def __exit__(self, *exc):
+        global _SHARE_GPU
+        _SHARE_GPU = self._old
+
+
 def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale, save_agg):
     x, w, W, bias = _f32c(x), _f32c(w), _f32c(W), _f32c(bias)
     dev = nat.require_device(x, rowptr, rows, idx, w, W, bias, items, split)
@@ -98,7 +113,8 @@ def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, b
         nat.lib().kgx_spmm_gemm(
             reduce, nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, nat.ptr(split), n_split,
             nat.ptr(idx), nat.ptr(w), nat.ptr(x), x.stride(0), x.shape[1], nat.ptr(W), F_out, nat.ptr(bias),
-            int(pre_gin), float(gin_scale), nat.ptr(out), out.stride(0), nat.ptr(partials),
+            int(pre_gin) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0), float(gin_scale), nat.ptr(out), out.stride(0),
+            nat.ptr(partials),
             nat.ptr(agg) if save_agg else None, agg.stride(0) if save_agg else 0, nat.stream(dev),
         ),
         "kgx_spmm_gemm",
