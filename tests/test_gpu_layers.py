@@ -261,3 +261,27 @@ def test_utils(dev, golden):
     exact(loops, R.add_self_loops(T(g["edge_index"]), N).numpy())
     norm = kgx.compute_gcn_normalization(loops, N).cpu().numpy()
     assert_tol(norm, g["gcn_norm_loops"], tol=2e-7)
+
+
+def test_hip_graph_capture_replay(dev, golden):
+    """A 2-layer GCN forward (fused + unfused kernels) captured into a HIP graph
+    (torch.cuda.CUDAGraph) replays to the eager result: the kgx ops launch on
+    the current stream, allocate through torch and never synchronise."""
+    c = golden("cora_like")
+    xc = np.unpackbits(c["x_packed"], axis=1)[:, : int(c["n_features"])].astype(np.float32)
+    x, ei = T(xc).to(dev), T(c["edge_index"]).to(dev)
+    l1, l2 = GCNConv(64), GCNConv(7)
+    with torch.no_grad():
+        ref = l2([torch.relu(l1([x, ei])), ei])  # builds weights + cached CSRs
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                l2([torch.relu(l1([x, ei])), ei])
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = l2([torch.relu(l1([x, ei])), ei])
+        graph.replay()
+        torch.cuda.synchronize()
+    exact(out, ref.detach().cpu().numpy())

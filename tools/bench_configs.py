@@ -214,7 +214,25 @@ def c1(dev):
 
     fwd()
     ms, agg, _ = run(fwd, steps=50, warmup=5)
-    return dict(config="C1 Cora-shaped 2-layer GCN 1433-64-7", layer_ms=ms, agg_ms=agg)
+    # the same forward captured once into a HIP graph and replayed (launch-bound at this size)
+    with torch.no_grad():
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            fwd()
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            fwd()
+        for _ in range(5):
+            graph.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(200):
+            graph.replay()
+        torch.cuda.synchronize()
+        g_ms = (time.perf_counter() - t0) / 200 * 1e3
+    return dict(config="C1 Cora-shaped 2-layer GCN 1433-64-7", layer_ms=ms, agg_ms=agg, hip_graph_ms=g_ms)
 
 
 if __name__ == "__main__":
