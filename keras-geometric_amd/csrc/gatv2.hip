@@ -135,7 +135,7 @@ __global__ __launch_bounds__(kBlock) void gatv2_kernel(GatArgs a) {
       // of the row; edges past the end re-read the last one), masked on use
       float hs[U][K];
 #pragma unroll
-      for (int u = 0; u < U; ++u) vload<K>(hs[u], a.h_src + int64_t(c[u]) * a.ld_h + (valid ? f : 0));
+      for (int u = 0; u < U; ++u) vload<K>(hs[u], a.h_src + row_off(c[u], a.ld_h) + (valid ? f : 0));
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -287,6 +287,7 @@ extern "C" int kgx_gatv2(const int32_t* rowptr, const int32_t* rows, int64_t n_r
   const int64_t HC = int64_t(heads) * channels;
   KGX_REQUIRE(rowptr && rows && col && h_src && h_dst && att && out, KGX_ERR_ARG, "kgx_gatv2: null pointer");
   KGX_REQUIRE(ld_h >= HC && ld_out >= HC, KGX_ERR_ARG, "kgx_gatv2: leading dimension < heads*channels");
+  KGX_REQUIRE(ld_h < (int64_t(1) << 31), KGX_ERR_ARG, "kgx_gatv2: leading dimension >= 2^31");
   const bool use_items = items != nullptr;
   KGX_REQUIRE(!use_items || n_split == 0 || (split && partials), KGX_ERR_ARG,
               "kgx_gatv2: split rows need split list and partials");
@@ -498,7 +499,7 @@ __global__ __launch_bounds__(kBlock) void gatv2_bwd_rows_kernel(GatBwdArgs a) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int32_t ee = e + u < end ? e + u : end - 1;
-        vload<K>(hs[u], a.h_src + int64_t(a.col[ee]) * a.ld_h + f);
+        vload<K>(hs[u], a.h_src + row_off(a.col[ee], a.ld_h) + f);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -567,12 +568,12 @@ __global__ __launch_bounds__(kBlock) void gatv2_bwd_src_kernel(GatBwdArgs a) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int32_t ee = e + u < end ? e + u : end - 1;
-        const int64_t i = a.t_col[ee];
-        const int64_t s = a.t_slot[ee];
-        al[u] = a.alpha[s * a.H + head];
-        dsv[u] = a.ds[s * a.H + head];
-        vload<K>(gr[u], a.grad + i * a.ld_g + f);
-        vload<K>(hd[u], a.h_dst + i * a.ld_h + f);
+        const int32_t i = a.t_col[ee];
+        const int32_t s = a.t_slot[ee];
+        al[u] = a.alpha[row_off(s, a.H) + head];
+        dsv[u] = a.ds[row_off(s, a.H) + head];
+        vload<K>(gr[u], a.grad + row_off(i, a.ld_g) + f);
+        vload<K>(hd[u], a.h_dst + row_off(i, a.ld_h) + f);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -660,6 +661,8 @@ extern "C" int kgx_gatv2_backward(const int32_t* rowptr, const int32_t* rows, in
               KGX_ERR_ARG, "kgx_gatv2_backward: null pointer");
   KGX_REQUIRE(ld_h >= HC && ld_grad >= HC && ld_grad_h >= HC && ld_out >= HC, KGX_ERR_ARG,
               "kgx_gatv2_backward: leading dimension < heads*channels");
+  KGX_REQUIRE(ld_h < (int64_t(1) << 31) && ld_grad < (int64_t(1) << 31), KGX_ERR_ARG,
+              "kgx_gatv2_backward: leading dimension >= 2^31");
   KGX_REQUIRE(((!items || n_split == 0) && (!t_items || t_n_split == 0)) || partials, KGX_ERR_ARG,
               "kgx_gatv2_backward: split rows need partials");
   // K channels per lane: the smallest K (dividing C, with aligned vector

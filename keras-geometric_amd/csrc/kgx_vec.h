@@ -83,6 +83,14 @@ __device__ __forceinline__ float amax_update(float acc, float v) {
 
 __device__ __forceinline__ bool is_inf(float v) { return __builtin_isinf(v); }
 
+// Row offset idx * ld for a gathered row: both operands are non-negative and
+// below 2^32 (checked at the C-ABI), so one 32x32->64 v_mad_u64_u32 replaces
+// the sign-extended 64-bit multiply (six VALU ops, three of them quarter rate)
+// the int64 expression compiles to -- per gathered row, in the hot loops.
+__device__ __forceinline__ uint64_t row_off(int32_t idx, int64_t ld) {
+  return uint64_t(uint32_t(idx)) * uint32_t(ld);
+}
+
 // Counter-based dropout mask: element (key, f) is kept iff the high 32 bits of
 // splitmix64(seed ^ (key << 32 | f) * golden) are >= thresh = p * 2^32.  A
 // function of (seed, edge id, feature) only, so the forward, its backward over

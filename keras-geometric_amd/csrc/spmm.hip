@@ -143,7 +143,7 @@ __device__ __forceinline__ void edge_block(const SpmmArgs& a, int32_t e, int32_t
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int t = 0; t < NT; ++t) vload<VEC>(v[u][t], a.table + int64_t(c[u]) * a.ld_t + fl[t]);
+    for (int t = 0; t < NT; ++t) vload<VEC>(v[u][t], a.table + row_off(c[u], a.ld_t) + fl[t]);
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -385,6 +385,7 @@ extern "C" int kgx_spmm(int reduce, int epilogue, const int32_t* rowptr, const i
   KGX_REQUIRE(F >= 0 && n_rows >= 0 && n_items >= 0 && n_split >= 0, KGX_ERR_ARG, "kgx_spmm: negative size");
   if (F == 0 || n_rows == 0) return KGX_OK;
   KGX_REQUIRE(out && ld_out >= F && ld_table >= F, KGX_ERR_ARG, "kgx_spmm: bad output / leading dimensions");
+  KGX_REQUIRE(ld_table < (int64_t(1) << 31), KGX_ERR_ARG, "kgx_spmm: table leading dimension >= 2^31");
   KGX_REQUIRE(rowptr && rows && idx && table, KGX_ERR_ARG, "kgx_spmm: null CSR / table pointer");
   KGX_REQUIRE(epilogue != KGX_EPI_BIAS || bias, KGX_ERR_ARG, "kgx_spmm: EPI_BIAS needs bias");
   KGX_REQUIRE(epilogue != KGX_EPI_GIN || (xroot && ld_x >= F), KGX_ERR_ARG, "kgx_spmm: EPI_GIN needs xroot");

@@ -219,7 +219,7 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
       if (u < pn)  // exec-masked: rows of degree < PF issue no redundant loads
-        vload<4>(pv[u], a.x + int64_t(c[u]) * a.ld_x + f);
+        vload<4>(pv[u], a.x + row_off(c[u], a.ld_x) + f);
     }
   };
 
@@ -248,7 +248,7 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
       }
       float v[B][4];
 #pragma unroll
-      for (int u = 0; u < B; ++u) vload<4>(v[u], a.x + int64_t(c[u]) * a.ld_x + f);
+      for (int u = 0; u < B; ++u) vload<4>(v[u], a.x + row_off(c[u], a.ld_x) + f);
 #pragma unroll
       for (int u = 0; u < B; ++u)
 #pragma unroll
@@ -447,6 +447,7 @@ extern "C" int kgx_spmm_gemm(int reduce, const int32_t* rowptr, const int32_t* r
               KGX_ERR_ARG, "kgx_spmm_gemm: agg_out must be 16-byte aligned with ld >= F_in, ld %% 4 == 0");
   if (n_rows == 0) return KGX_OK;
   KGX_REQUIRE(rowptr && rows && idx && x && W && out, KGX_ERR_ARG, "kgx_spmm_gemm: null pointer");
+  KGX_REQUIRE(ld_x < (int64_t(1) << 31), KGX_ERR_ARG, "kgx_spmm_gemm: x leading dimension >= 2^31");
   KGX_REQUIRE(ld_x % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0 && ld_out >= F_out, KGX_ERR_ARG,
               "kgx_spmm_gemm: x must be 16-byte aligned with ld %% 4 == 0");
   KGX_REQUIRE(!items || n_split == 0 || (split && partials), KGX_ERR_ARG,
