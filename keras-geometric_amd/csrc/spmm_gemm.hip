@@ -67,7 +67,7 @@ struct FusedArgs {
   int accumulate;   // out += result
   int share_gpu;    // launch 7/8 of the resident grid
   float gin_scale;
-  int debug;        // experiment knob (KGX_FUSED_DEBUG): 1 skip the MFMA phase, 2 skip stores
+  int debug;        // experiment builds only (-DKGX_EXPERIMENTS, env KGX_FUSED_DEBUG): 1 skip MFMA, 2 skip stores
 };
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops
@@ -476,11 +476,15 @@ extern "C" int kgx_spmm_gemm(int reduce, const int32_t* rowptr, const int32_t* r
   a.accumulate = (flags & KGX_FUSED_ACCUMULATE) != 0;
   a.share_gpu = (flags & KGX_FUSED_SHARE_GPU) != 0;
   a.gin_scale = gin_scale;
+#ifdef KGX_EXPERIMENTS  // cost-decomposition knob; never in a product build (it changes results)
   static const int dbg = [] {
     const char* h = getenv("KGX_FUSED_DEBUG");
     return h ? atoi(h) : 0;
   }();
   a.debug = dbg;
+#else
+  a.debug = 0;
+#endif
   const bool wt = w != nullptr;
   switch (reduce) {
     case KGX_SUM: return wt ? launch<KGX_SUM, true>(a, stream) : launch<KGX_SUM, false>(a, stream);
