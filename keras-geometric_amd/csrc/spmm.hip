@@ -59,7 +59,13 @@ struct SpmmArgs {
   uint32_t drop_thresh;
   float drop_scale;
   int f_base;  // first column of this launch (column slicing of wide F)
+  int long_rows;  // EXACT mode: rows of degree >= kLongRow are reduced by spmm_long_kernel
 };
+
+// EXACT mode has no hub split (each row is one sequential reduction), so a hub
+// row of 10^5 edges is a latency chain; rows this long get their own kernel
+// with 32 gathers in flight per group instead of 6.
+constexpr int kLongRow = 2048;
 
 template <int RED>
 struct Reducer {
@@ -199,6 +205,7 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
       beg = a.rowptr[row];
       end = a.rowptr[row + 1];
       slot = -1;
+      if (a.long_rows && end - beg >= kLongRow) continue;  // spmm_long_kernel's row
     }
 
     float acc[NT][VEC];
@@ -228,6 +235,39 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
         else vstore<VEC>(a.out + int64_t(row) * a.ld_o + fo[t], r);
       }
     }
+  }
+}
+
+// EXACT-mode rows of degree >= kLongRow (a prefix of the degree-ordered row
+// list): the same in-order reduction as spmm_kernel, 32 gathers per block.
+template <int VEC, int RED, bool WEIGHTED, bool DROP = false>
+__global__ __launch_bounds__(kBlock) void spmm_long_kernel(SpmmArgs a) {
+  using R = Reducer<RED>;
+  constexpr int U = 32;
+  const int G = a.G;
+  const int lane = threadIdx.x & (G - 1);
+  const int64_t ngroups = (int64_t(gridDim.x) * kBlock) >> a.lgG;
+  int fo[1], fl[1];
+  fo[0] = lane * VEC;
+  const bool fv = fo[0] < a.F;
+  fl[0] = fv ? fo[0] : a.F - VEC;
+  for (int64_t it = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> a.lgG; it < a.n_rows; it += ngroups) {
+    const int32_t row = a.rows[it];
+    const int32_t beg = a.rowptr[row], end = a.rowptr[row + 1];
+    if (end - beg < kLongRow) break;  // rows are in descending degree order
+    float acc[1][VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[0][k] = R::init();
+    int32_t e = beg;
+    for (; e + U <= end; e += U) edge_block<U, VEC, 1, RED, WEIGHTED, DROP>(a, e, end, fl, acc);
+    for (; e < end; e += 4) edge_block<4, VEC, 1, RED, WEIGHTED, DROP>(a, e, end, fl, acc);
+    if (!fv) continue;
+    float r[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k)
+      r[k] = a.epi == KGX_EPI_RAW ? R::finish_raw(acc[0][k], end - beg) : R::finish(acc[0][k], end - beg);
+    epilogue<VEC>(a, row, fo[0], r);
+    vstore<VEC>(a.out + int64_t(row) * a.ld_o + fo[0], r);
   }
 }
 
@@ -313,8 +353,21 @@ __global__ __launch_bounds__(kBlock) void spmm_std_kernel(SpmmArgs a) {
 
 
 template <int VEC, int NT, int RED, bool W>
-int launch_main(const SpmmArgs& a, hipStream_t s) {
+int launch_main(const SpmmArgs& a_in, hipStream_t s) {
+  SpmmArgs a = a_in;
   const int64_t work = a.items ? a.n_items : a.n_rows;
+  if constexpr (NT == 1) {
+    if (!a.items && a.n_rows > 0) {  // EXACT: long rows first, on their own kernel
+      a.long_rows = 1;
+      auto kl = spmm_long_kernel<VEC, RED, W>;
+      if constexpr (RED == KGX_SUM) {
+        if (a.drop_key) kl = spmm_long_kernel<VEC, RED, W, true>;
+      }
+      const int64_t cand = a.n_rows < 16384 ? a.n_rows : 16384;
+      hipLaunchKernelGGL(kl, dim3(resident_grid(kl, cand, a.G)), dim3(kBlock), 0, s, a);
+      KGX_CHECK_LAUNCH();
+    }
+  }
   if (work > 0) {
     auto k = spmm_kernel<VEC, NT, RED, W>;
     if constexpr (RED == KGX_SUM) {
