@@ -350,3 +350,70 @@ class ShardedGCNConv(Layer):
             if g_halo.kept:
                 sg.backend.aggregate_transform(g_halo, halo, self.kernel, out=out)
         return out
+
+
+class _ShardedWrap(Layer):
+    """A single-device conv layer applied to a ShardedGraph: the neighbour
+    reduction runs over the shard CSR (own rows + exchanged halo rows), the
+    node update runs on the shard's own rows with the wrapped layer's weights
+    (broadcast from rank 0 at build)."""
+
+    def __init__(self, conv: Layer, sg: ShardedGraph, **kwargs):
+        super().__init__(**kwargs)
+        self.conv = conv
+        self.sg = sg
+
+    def _ensure_built(self, x_local: torch.Tensor) -> None:
+        if self.conv.built:
+            return
+        self.conv._build_device = x_local.device
+        self.conv.build([tuple(x_local.shape), (2, 0)])
+        with torch.no_grad():
+            for p in self.conv.weights:
+                self.sg.comm.broadcast(p.data, src=0)
+        self.built = True
+
+
+class ShardedGINConv(_ShardedWrap):
+    """GINConv over a ShardedGraph: h_i = MLP((1+eps) x_i + AGG_j x_j)
+    (gin_conv.py:216-225).  Shard graph: no self loops, no GCN norm
+    (ShardedGraph.build(..., self_loops=False, gcn_norm=False)).  The
+    (1+eps) x_i + aggr epilogue is fused into the aggregation as on one GPU,
+    so EXACT-mode h is bit-identical to the single-GPU layer's."""
+
+    def __init__(self, output_dim: int, sg: ShardedGraph, **gin_kwargs):
+        from .layers.gin_conv import GINConv
+
+        super().__init__(GINConv(output_dim, exact=sg.exact, **gin_kwargs), sg)
+
+    def forward(self, x_local: torch.Tensor, training=None) -> torch.Tensor:
+        self._ensure_built(x_local)
+        sg, conv = self.sg, self.conv
+        x_local = x_local.contiguous()
+        with torch.no_grad():
+            h = sg.propagate(x_local, conv.aggregator, epilogue=nat.EPI_GIN, xroot=x_local,
+                             gin_scale=conv._scale())
+            return conv.mlp(h, training=training)
+
+
+class ShardedSAGEConv(_ShardedWrap):
+    """SAGEConv over a ShardedGraph: lin_neigh(AGG_j x_j) + lin_self(x_i) + b
+    (sage_conv.py:405-439; the 'pooling' aggregator exchanges pool_mlp(x)
+    rows and max-reduces them, :300-348).  Shard graph: no self loops, no
+    GCN norm."""
+
+    def __init__(self, output_dim: int, sg: ShardedGraph, **sage_kwargs):
+        from .layers.sage_conv import SAGEConv
+
+        super().__init__(SAGEConv(output_dim, exact=sg.exact, **sage_kwargs), sg)
+
+    def forward(self, x_local: torch.Tensor, training=None) -> torch.Tensor:
+        self._ensure_built(x_local)
+        sg, conv = self.sg, self.conv
+        x_local = x_local.contiguous()
+        with torch.no_grad():
+            if conv.actual_aggregator == "pooling":
+                aggr = sg.propagate(conv.pool_mlp(x_local).contiguous(), "max")
+            else:
+                aggr = sg.propagate(x_local, conv.actual_aggregator)
+            return conv.update_nodes(x_local, aggr)

@@ -132,6 +132,11 @@ class SAGEConv(MessagePassing):
             )
         num_nodes = x.shape[0]
         aggregated = self.aggregate_neighbors(x, ei, num_nodes, training=training, edge_index_obj=edge_index)
+        return self.update_nodes(x, aggregated)
+
+    def update_nodes(self, x, aggregated):
+        """lin_neigh(aggr) + lin_self(x) + bias, activation, L2 norm (sage_conv.py:409-439);
+        also the update step of distributed.ShardedSAGEConv on a shard's rows."""
         h_neigh = self.lin_neigh(aggregated)
         if self.root_weight and self.lin_self is not None:
             out = self.lin_self(x) + h_neigh

@@ -68,7 +68,7 @@ class OracleBackend:
         out += y
         return out
 
-    def aggregate(self, g, table, reduce="sum", weighted=False, epilogue=nat.EPI_NONE, bias=None, **_):
+    def aggregate(self, g, table, reduce="sum", weighted=False, epilogue=nat.EPI_NONE, bias=None, **kw):
         rows = torch.repeat_interleave(torch.arange(g.n_dst), g.deg.long())
         msg = table[g.col.long()]
         if weighted:
@@ -76,6 +76,8 @@ class OracleBackend:
         out = R.aggregate(reduce, msg, rows, g.n_dst)
         if epilogue == nat.EPI_BIAS:
             out = K.add(out, bias)
+        elif epilogue == nat.EPI_GIN:  # (1+eps) x_i + aggr (gin_conv.py:216-222)
+            out = torch.tensor(kw["gin_scale"], dtype=torch.float32) * kw["xroot"] + out
         return out
 
 
@@ -178,3 +180,64 @@ def test_sharded_equals_unsharded_bitwise(world):
     err = np.abs(y_split - y) / np.maximum(1, np.abs(y))
     assert err.max() <= 1e-5
 
+
+
+def _conv_worker(rank, world, port, q):
+    """ShardedGINConv / ShardedSAGEConv on a shard graph without loops or norms."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        s, d, x, _, _ = _graph()
+        bounds = kd.equal_bounds(N, world)
+        lo, hi = bounds[rank], bounds[rank + 1]
+        keep = (d >= lo) & (d < hi)
+        sg = kd.ShardedGraph.build(torch.from_numpy(s[keep]), torch.from_numpy(d[keep]), bounds,
+                                   backend=OracleBackend(), n_features=F_IN, self_loops=False, gcn_norm=False)
+        xl = torch.from_numpy(x[lo:hi])
+        outs = []
+        for layer in (kd.ShardedGINConv(F_OUT, sg, mlp_hidden=[12], aggregator="sum", eps_init=0.25),
+                      kd.ShardedGINConv(F_OUT, sg, aggregator="max"),
+                      kd.ShardedSAGEConv(F_OUT, sg, aggregator="mean", normalize=True),
+                      kd.ShardedSAGEConv(F_OUT, sg, aggregator="pooling", pool_hidden_dim=10)):
+            layer._ensure_built(xl)  # weights drawn per rank, then broadcast from rank 0
+            outs.append((layer(xl).numpy(), list(layer.conv.get_weights())))
+        q.put((rank, outs))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_sharded_gin_sage_layers():
+    """Sharded GIN (sum / max) and SAGE (mean + L2 norm / pooling) equal the
+    oracle layers on the whole graph (within 1e-5), with rank 0's weights."""
+    if torch.cuda.is_initialized():
+        pytest.skip("never start processes from a process that has initialised the GPU")
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_conv_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=90) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    s, d, x, _, _ = _graph()
+    X, EI = torch.from_numpy(x), torch.from_numpy(np.stack([s, d]))
+    for i in range(4):
+        for a, b in zip(res[0][i][1], res[1][i][1]):  # broadcast: identical weights on every rank
+            np.testing.assert_array_equal(a, b)
+    w = [[torch.from_numpy(a) for a in res[0][i][1]] for i in range(4)]
+    refs = [
+        R.gin_forward(X, EI, [(w[0][0], w[0][1], "relu"), (w[0][2], w[0][3], None)], "sum", eps=0.25),
+        R.gin_forward(X, EI, [(w[1][0], w[1][1], None)], "max"),
+        # SAGE weights in Layer.weights order: bias, [pool kernel, pool bias,] lin_neigh, lin_self
+        R.sage_forward(X, EI, w[2][1], w[2][2], w[2][0], "mean", normalize=True),
+        R.sage_forward(X, EI, w[3][3], w[3][4], w[3][0], "pooling", pool=(w[3][1], w[3][2], "relu")),
+    ]
+    for i, ref in enumerate(refs):
+        got = np.concatenate([res[r][i][0] for r in range(world)])
+        ref = ref.numpy()
+        err = np.abs(got - ref) / np.maximum(1, np.abs(ref))
+        assert err.max() <= 1e-5, (i, err.max())

@@ -113,3 +113,53 @@ def test_sharded_hip_equals_single_gpu(world, dev):
     err = np.abs(got - ref) / np.maximum(1.0, np.abs(ref))
     assert err.max() <= 1e-5
 
+
+
+def _run_conv_rank(rank, hub, dev, x, out):
+    try:
+        comm = ThreadComm(hub, rank)
+        sg = kd.ShardedGraph.rmat(N, E, seed=6, device=dev, comm=comm, exact=True, n_features=F,
+                                  self_loops=False, gcn_norm=False)
+        xl = x[sg.lo: sg.lo + sg.n_local]
+        res = []
+        for layer in (kd.ShardedGINConv(32, sg, mlp_hidden=[48], aggregator="sum", eps_init=0.5),
+                      kd.ShardedSAGEConv(32, sg, aggregator="mean"),
+                      kd.ShardedSAGEConv(32, sg, aggregator="max", normalize=True)):
+            y = layer(xl)
+            torch.cuda.synchronize()
+            res.append((y.cpu().numpy(), layer.conv.get_weights()))
+        out[rank] = res
+    except BaseException as e:
+        out[rank] = e
+        hub.barrier.abort()
+
+
+def test_sharded_gin_sage_hip(dev):
+    """C4/C5 shapes in miniature: sharded GIN (sum) and SAGE (mean, max) on the
+    HIP backend equal the single-GPU layers with rank 0's weights."""
+    import keras_geometric_amd as kgx
+    from keras_geometric_amd import synthetic
+
+    world = 2
+    x = torch.randn(N, F, generator=torch.Generator().manual_seed(1)).to(dev)
+    hub = ThreadHub(world)
+    res = {}
+    threads = [threading.Thread(target=_run_conv_rank, args=(r, hub, dev, x, res)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=240)
+    for r in range(world):
+        if isinstance(res.get(r), BaseException):
+            raise res[r]
+    ei = synthetic.rmat_edge_index(N, E, seed=6, device=dev)
+    singles = [kgx.GINConv(32, mlp_hidden=[48], aggregator="sum", eps_init=0.5, exact=True),
+               kgx.SAGEConv(32, aggregator="mean", exact=True),
+               kgx.SAGEConv(32, aggregator="max", normalize=True, exact=True)]
+    for i, layer in enumerate(singles):
+        layer([x, ei])
+        layer.set_weights(res[0][i][1])
+        ref = layer([x, ei]).detach().cpu().numpy()
+        got = np.concatenate([res[r][i][0] for r in range(world)])
+        err = np.abs(got - ref) / np.maximum(1.0, np.abs(ref))
+        assert err.max() <= 1e-5, (i, err.max())
