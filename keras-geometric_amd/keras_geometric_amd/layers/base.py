@@ -287,9 +287,18 @@ class Dense(Layer):
         return self.call(x)
 
     def call(self, x):
-        y = torch.matmul(x, self.kernel)
-        if self.use_bias:
-            y = y + self.bias
+        if self.use_bias and x.dim() == 2:
+            if self.activation is torch.relu and x.is_cuda and not torch.is_grad_enabled():
+                # inference: bias + ReLU in the GEMM epilogue (one pass over the output;
+                # this fused op has no autograd formula)
+                return torch._addmm_activation(self.bias, x, self.kernel)
+            y = torch.addmm(self.bias, x, self.kernel)  # bias in the GEMM epilogue
+            if self.activation is torch.relu:
+                return torch.relu_(y)
+        else:
+            y = torch.matmul(x, self.kernel)
+            if self.use_bias:
+                y = y + self.bias
         if self.activation is not None:
             y = self.activation(y)
         return y

@@ -137,14 +137,18 @@ class SAGEConv(MessagePassing):
     def update_nodes(self, x, aggregated):
         """lin_neigh(aggr) + lin_self(x) + bias, activation, L2 norm (sage_conv.py:409-439);
         also the update step of distributed.ShardedSAGEConv on a shard's rows."""
-        h_neigh = self.lin_neigh(aggregated)
+        use_b = self.use_bias and self.bias is not None
         if self.root_weight and self.lin_self is not None:
-            out = self.lin_self(x) + h_neigh
+            # two GEMMs chained through the epilogue: (b + x W_self) + aggr W_neigh
+            out = torch.addmm(self.bias, x, self.lin_self.kernel) if use_b else torch.matmul(x, self.lin_self.kernel)
+            out = torch.addmm(out, aggregated, self.lin_neigh.kernel)
         else:
-            out = h_neigh
-        if self.use_bias and self.bias is not None:
-            out = out + self.bias
-        if self.activation is not None:
+            out = self.lin_neigh(aggregated)
+            if use_b:
+                out = out + self.bias
+        if self.activation is torch.relu:
+            out = torch.relu_(out)
+        elif self.activation is not None:
             out = self.activation(out)
         if self.normalize:
             out = l2_normalize(out)
