@@ -184,8 +184,10 @@ int kgx_dropout_mask(uint64_t seed, float p, const int32_t* keys, int64_t n, int
  * rows before the transform — what the backward's dW = agg^T dOut needs.
  * ------------------------------------------------------------------------- */
 /* KGX_FUSED_SHARE_GPU: launch 7/8 of the resident grid, leaving block slots
- * for kernels of a concurrent stream (the sharded layer's RCCL exchange). */
-enum { KGX_FUSED_PRE_GIN = 1, KGX_FUSED_ACCUMULATE = 2, KGX_FUSED_SHARE_GPU = 4 };
+ * for kernels of a concurrent stream (the sharded layer's RCCL exchange).
+ * KGX_FUSED_RELU: out = max(bias + ..., 0), the activation of a GIN MLP's
+ * first Dense (gin_conv.py:129-162); not combinable with ACCUMULATE. */
+enum { KGX_FUSED_PRE_GIN = 1, KGX_FUSED_ACCUMULATE = 2, KGX_FUSED_SHARE_GPU = 4, KGX_FUSED_RELU = 8 };
 int kgx_spmm_gemm(int reduce, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
                   const int32_t* items, int64_t n_items, const int32_t* split, int64_t n_split,
                   const int32_t* idx, const float* w, const float* x, int64_t ld_x, int64_t F_in,

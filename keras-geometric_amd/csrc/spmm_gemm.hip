@@ -66,6 +66,7 @@ struct FusedArgs {
   int pre_gin;      // apply gin_scale * x[row] + aggr before the transform
   int accumulate;   // out += result
   int share_gpu;    // launch 7/8 of the resident grid
+  int relu;         // out = max(result, 0) (not with accumulate)
   float gin_scale;
   int debug;        // experiment builds only (-DKGX_EXPERIMENTS, env KGX_FUSED_DEBUG): 1 skip MFMA, 2 skip stores
 };
@@ -339,6 +340,7 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
           const float4 p = *dst;
           v = make_float4(__fadd_rn(p.x, v.x), __fadd_rn(p.y, v.y), __fadd_rn(p.z, v.z), __fadd_rn(p.w, v.w));
         }
+        if (a.relu) v = make_float4(fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f));
         *dst = v;
       }
     }
@@ -385,6 +387,7 @@ __global__ __launch_bounds__(256) void spmm_gemm_fixup_kernel(FusedArgs a) {
         for (int k = 0; k < kFin; ++k) s = fmaf(vrow[g][k], a.W[int64_t(k) * a.F_out + c], s);
         float v = s + (a.bias ? a.bias[c] : 0.0f);
         if (a.accumulate) v = __fadd_rn(a.out[int64_t(row) * a.ld_o + c], v);
+        if (a.relu) v = fmaxf(v, 0.0f);
         a.out[int64_t(row) * a.ld_o + c] = v;
       }
     }
@@ -441,8 +444,10 @@ extern "C" int kgx_spmm_gemm(int reduce, const int32_t* rowptr, const int32_t* r
   KGX_REQUIRE(F_out > 0 && F_out <= 128 && F_out % 16 == 0, KGX_ERR_UNSUPPORTED,
               "kgx_spmm_gemm: F_out must be a multiple of 16 <= 128 (got %lld)", (long long)F_out);
   KGX_REQUIRE(n_rows >= 0 && n_items >= 0 && n_split >= 0, KGX_ERR_ARG, "kgx_spmm_gemm: negative size");
-  KGX_REQUIRE((flags & ~(KGX_FUSED_PRE_GIN | KGX_FUSED_ACCUMULATE | KGX_FUSED_SHARE_GPU)) == 0, KGX_ERR_ARG,
-              "kgx_spmm_gemm: unknown flags 0x%x", flags);
+  KGX_REQUIRE((flags & ~(KGX_FUSED_PRE_GIN | KGX_FUSED_ACCUMULATE | KGX_FUSED_SHARE_GPU | KGX_FUSED_RELU)) == 0,
+              KGX_ERR_ARG, "kgx_spmm_gemm: unknown flags 0x%x", flags);
+  KGX_REQUIRE(!((flags & KGX_FUSED_RELU) && (flags & KGX_FUSED_ACCUMULATE)), KGX_ERR_ARG,
+              "kgx_spmm_gemm: KGX_FUSED_RELU cannot be combined with KGX_FUSED_ACCUMULATE");
   KGX_REQUIRE(!agg_out || (ld_agg >= F_in && reinterpret_cast<uintptr_t>(agg_out) % 16 == 0 && ld_agg % 4 == 0),
               KGX_ERR_ARG, "kgx_spmm_gemm: agg_out must be 16-byte aligned with ld >= F_in, ld %% 4 == 0");
   if (n_rows == 0) return KGX_OK;
@@ -475,6 +480,7 @@ extern "C" int kgx_spmm_gemm(int reduce, const int32_t* rowptr, const int32_t* r
   a.pre_gin = (flags & KGX_FUSED_PRE_GIN) != 0;
   a.accumulate = (flags & KGX_FUSED_ACCUMULATE) != 0;
   a.share_gpu = (flags & KGX_FUSED_SHARE_GPU) != 0;
+  a.relu = (flags & KGX_FUSED_RELU) != 0;
   a.gin_scale = gin_scale;
 #ifdef KGX_EXPERIMENTS  // cost-decomposition knob; never in a product build (it changes results)
   static const int dbg = [] {

@@ -4,7 +4,10 @@ h'_i = MLP((1+eps) * x_i + AGG_{j->i} x_j)   (gin_conv.py:216-225)
 
 kgx forward: ONE fused kernel gathers x_j rows, reduces (sum/mean/max) in the
 reference's edge order and applies the (1+eps)*x_i + aggr epilogue; the MLP
-is Dense GEMMs (hipBLASLt on MFMA).
+is Dense GEMMs (hipBLASLt on MFMA).  When F_in == 128 and the MLP's first
+Dense fits the fused kernel (<= 128 units, bias, none/ReLU), that Dense runs in
+the aggregation's epilogue on MFMA too (kgx_spmm_gemm with KGX_FUSED_PRE_GIN;
+EXACT mode keeps the separate, bit-exact aggregation).
 """
 
 from __future__ import annotations
@@ -112,6 +115,16 @@ class GINConv(MessagePassing):
             # trainable eps: keep (1 + eps) in the autograd graph (gin_conv.py:216-225)
             h = (1 + self.eps) * x + kops.aggregate(g, x.contiguous(), self.aggregator, exact=self.exact)
             return self.mlp(h, training=training)
+        first = self.mlp.layers[0]
+        if (not self.exact and first.activation in (None, torch.relu)
+                and kops.fused_transform_supported(x.shape[1], first.units)):
+            # (1+eps) x + aggr -> the MLP's first Dense (bias, ReLU) in one fused launch
+            h = kops.aggregate_transform(g, x.contiguous(), first.kernel, self.aggregator,
+                                         bias=first.bias if first.use_bias else None, pre_gin=True,
+                                         gin_scale=self._scale(), relu=first.activation is torch.relu)
+            for layer in self.mlp.layers[1:]:
+                h = layer(h, training=training) if isinstance(layer, Dropout) else layer(h)
+            return h
         h = kops.aggregate(g, x.contiguous(), self.aggregator, epilogue=nat.EPI_GIN, xroot=x.contiguous(),
                            gin_scale=self._scale(), exact=self.exact)
         return self.mlp(h, training=training)

@@ -95,7 +95,8 @@ class sharing_gpu:
         _SHARE_GPU = self._old
 
 
-def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale, save_agg):
+def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale, save_agg,
+                    relu=False):
     x, w, W, bias = _f32c(x), _f32c(w), _f32c(W), _f32c(bias)
     dev = nat.require_device(x, rowptr, rows, idx, w, W, bias, items, split)
     n_dst = rowptr.numel() - 1
@@ -113,7 +114,8 @@ def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, b
         nat.lib().kgx_spmm_gemm(
             reduce, nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, nat.ptr(split), n_split,
             nat.ptr(idx), nat.ptr(w), nat.ptr(x), x.stride(0), x.shape[1], nat.ptr(W), F_out, nat.ptr(bias),
-            int(pre_gin) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0), float(gin_scale), nat.ptr(out), out.stride(0),
+            int(pre_gin) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0) | (nat.FUSED_RELU if relu else 0),
+            float(gin_scale), nat.ptr(out), out.stride(0),
             nat.ptr(partials),
             nat.ptr(agg) if save_agg else None, agg.stride(0) if save_agg else 0, nat.stream(dev),
         ),
@@ -137,13 +139,14 @@ def spmm_gemm(
     bias: Optional[torch.Tensor],
     pre_gin: bool,
     gin_scale: float,
+    relu: bool = False,
 ) -> torch.Tensor:
     return _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale,
-                           False)[0]
+                           False, relu)[0]
 
 
 @spmm_gemm.register_fake
-def _spmm_gemm_fake(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale):
+def _spmm_gemm_fake(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale, relu=False):
     return x.new_empty((rowptr.shape[0] - 1, W.shape[1]))
 
 
@@ -529,13 +532,14 @@ def aggregate(
                           int(seed))
 
 
-def _aggregate_transform_raw(g, x, W, red, weighted, bias, pre_gin, gin_scale, exact):
+def _aggregate_transform_raw(g, x, W, red, weighted, bias, pre_gin, gin_scale, exact, relu=False):
     items, _, split, _, n_slots = g.work(exact)
     w = g.w if weighted else None
     if weighted and w is None:
         raise ValueError("graph was built without GCN normalisation weights")
     return _timed(lambda: torch.ops.kgx.spmm_gemm(
-        x, g.rowptr, g.rows, items, split, g.col, w, n_slots, red, W, bias, bool(pre_gin), float(gin_scale)
+        x, g.rowptr, g.rows, items, split, g.col, w, n_slots, red, W, bias, bool(pre_gin), float(gin_scale),
+        bool(relu)
     ))
 
 
@@ -617,12 +621,14 @@ def aggregate_transform(
     gin_scale: float = 1.0,
     exact: bool = False,
     out: torch.Tensor | None = None,
+    relu: bool = False,
 ) -> torch.Tensor:
     """out = bias + PRE(REDUCE_{e in row} x[col_e] * w_e) @ W in one fused launch
-    (out += ... in place when `out` is given).  Differentiable in x, W, bias."""
+    (out += ... in place when `out` is given; relu=True applies max(., 0) in the
+    kernel's store).  Differentiable in x, W, bias."""
     red = _reduce_id(reduce)
     if out is not None:  # accumulate into `out` (sum only: the caller splits a row's edges)
-        if pre_gin or red != nat.SUM:
+        if pre_gin or relu or red != nat.SUM:
             raise ValueError("aggregate_transform(out=...) accumulates plain sums only")
         if _needs_grad(x, W, bias, out):
             raise NotImplementedError("aggregate_transform(out=...) is a forward-only (no_grad) path")
@@ -632,8 +638,9 @@ def aggregate_transform(
                                                    W, bias))
         return out
     if _needs_grad(x, W, bias):
-        return _AggregateTransformFn.apply(x, W, bias, g, red, weighted, pre_gin, float(gin_scale), exact)
-    return _aggregate_transform_raw(g, x, W, red, weighted, bias, pre_gin, gin_scale, exact)
+        y = _AggregateTransformFn.apply(x, W, bias, g, red, weighted, pre_gin, float(gin_scale), exact)
+        return torch.relu(y) if relu else y
+    return _aggregate_transform_raw(g, x, W, red, weighted, bias, pre_gin, gin_scale, exact, relu)
 
 
 def _gatv2_raw(g, h_src, h_dst, att, heads, channels, negative_slope, bias, exact, drop_p=0.0, drop_seed=0):

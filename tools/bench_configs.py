@@ -97,6 +97,24 @@ def c4(dev):
                 edges_per_s=g.kept / ms * 1e3, alg_GBps=b / agg / 1e6)
 
 
+def gin128(dev):
+    """GIN-sum 10M/100M F128 -> MLP [128] + 128: fused (aggregation + first
+    Dense + ReLU in one launch) vs EXACT (aggregation, then the MLP GEMMs)."""
+    n, e, f = 10_000_000, 100_000_000, 128
+    ei = synthetic.rmat_edge_index(n, e, seed=0, device=dev)
+    x = torch.randn(n, f, device=dev)
+    out = {}
+    for exact in (False, True):
+        layer = kgx.GINConv(f, mlp_hidden=[f], aggregator="sum", exact=exact)
+        layer([x, ei])
+        ms, agg, _ = run(lambda: layer([x, ei]), steps=5)
+        out["exact_layer_ms" if exact else "layer_ms"] = ms
+        out["exact_agg_ms" if exact else "agg_ms"] = agg
+    g = graph(layer)
+    return dict(config="GIN-sum 10M/100M F128 MLP[128]+128 (1 GPU)", e_agg=g.kept,
+                edges_per_s=g.kept / out["layer_ms"] * 1e3, **out)
+
+
 def c5(dev):
     n, e, f = 2_449_029, 123_718_280, 100
     ei = synthetic.rmat_edge_index(n, e, seed=0, device=dev)
