@@ -266,6 +266,28 @@ int kgx_gatv2_backward(const int32_t* rowptr, const int32_t* rows, int64_t n_row
                        const int32_t* drop_key, float drop_p, uint64_t drop_seed, kgx_stream_t stream);
 
 /* ---------------------------------------------------------------------------
+ * Dense node transform (the layers' keras Dense / ops.matmul), one launch:
+ *   out[i,:] (+)= ACT( bias + x0[i,:K0] @ W0 + x1[i,:K1] @ W1 )
+ * Replaces GINConv's MLP Dense (gin_conv.py:129-162, applied at :225),
+ * SAGEConv's lin_self(x) + lin_neigh(aggr) + bias (sage_conv.py:407-428: both
+ * terms in ONE pass), GATv2Conv's shared linear map (gatv2_conv.py:224-239) and
+ * GCNConv's x @ kernel (gcn_conv.py:233-235) where the fused kernel does not
+ * apply.  f32-accurate: the product runs on bf16 MFMA as the six significant
+ * cross products of a three-way bf16 split of both operands (dropped terms
+ * <= 2^-24 |x w|); tolerance-equal to fp32 GEMM, not bit-equal.
+ * Shapes: K0 + K1 <= KGX_DENSE_MAX_K, N <= KGX_DENSE_MAX_N, K0 and K1
+ * multiples of 4, x rows 16-byte aligned with ld % 4 == 0; W0 [K0, N] and
+ * W1 [K1, N] row-major contiguous; x1/W1 may be NULL with K1 = 0; bias [N] or
+ * NULL.  KGX_DENSE_RELU: out = max(., 0) (Dense(activation='relu'));
+ * KGX_DENSE_ACCUMULATE: out += (before RELU).
+ * ------------------------------------------------------------------------- */
+enum { KGX_DENSE_RELU = 1, KGX_DENSE_ACCUMULATE = 2 };
+enum { KGX_DENSE_MAX_K = 256, KGX_DENSE_MAX_N = 256 };
+int kgx_dense(int64_t M, const float* x0, int64_t ld_x0, int64_t K0, const float* W0,
+              const float* x1, int64_t ld_x1, int64_t K1, const float* W1, int64_t N,
+              const float* bias, int flags, float* out, int64_t ld_out, kgx_stream_t stream);
+
+/* ---------------------------------------------------------------------------
  * Row gather out[i,:] = table[rows[i], :] — packs halo rows for the multi-GPU
  * exchange (no reference counterpart; the reference is single-device) and
  * scatters per-edge values back to input edge order.

@@ -1,0 +1,391 @@
+// Dense node transform on MFMA for the kgx engine (gfx950, wave64).
+//
+//   out[i, :] (+)= ACT( bias + x0[i, :K0] @ W0 + x1[i, :K1] @ W1 )
+//
+// The dense half of the layers on the propagate path: GINConv's MLP Dense
+// (gin_conv.py:129-162, applied at :225), SAGEConv's lin_self / lin_neigh pair
+// (sage_conv.py:407-428; two terms = ONE pass over x and the aggregate),
+// GATv2Conv's shared linear map (gatv2_conv.py:224-239) and GCNConv's X W when
+// the fused aggregate->transform kernel does not apply.  The reference runs
+// these as fp32 keras Dense / ops.matmul; here the product is taken on the
+// bf16 matrix cores as the six significant cross products of a three-way bf16
+// split of both operands (kgx_bf16x3.h: f32-accurate, IEEE inf/NaN), 16x the
+// per-clock rate of f32-input MFMA.
+//
+// Tiling: a block of WAVES waves owns 32-row tiles of the output and 16 WAVES
+// of its columns; for N > 128 two blocks on the same XCD take the two column
+// halves of the same tiles (blocks b and b + 8 under the round-robin
+// block->XCD dispatch), so x comes from HBM once and from that XCD's L2 the
+// second time.  Wave w owns 16 output columns and keeps W's split fragments for
+// them in registers for the whole kernel (K <= 256: 96 VGPRs), which leaves
+// room for two waves per SIMD.  Per tile the block loads the 32 x K f32 rows
+// (dwordx4, coalesced, two tiles ahead in registers), splits them into three
+// bf16 planes in LDS (double-buffered; row stride = 32 mod 256 bytes, so the
+// ds_read_b128 A-fragment reads are conflict-free), then every wave runs
+// v_mfma_f32_16x16x32_bf16 over K for its columns and stores its 16x16 blocks
+// with the bias / ReLU / accumulate epilogue.  One LDS barrier per tile.
+#include <type_traits>
+
+#include "kgx_bf16x3.h"
+#include "kgx_internal.h"
+
+namespace kgx {
+namespace {
+
+constexpr int kBM = 32;  // rows per tile
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops
+// (lgkmcnt), not its outstanding global loads / stores (vmcnt).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short bf16x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+struct DenseArgs {
+  int64_t M;
+  const float* x0;
+  int64_t ld0;
+  int K0;
+  const float* x1;
+  int64_t ld1;
+  int K1;
+  const float* W0;  // [K0, N] row-major
+  const float* W1;  // [K1, N] row-major
+  int N;
+  const float* bias;
+  float* out;
+  int64_t ld_out;
+  int relu;
+  int accumulate;
+  int cg_count;  // column groups of 16 WAVES columns (1 or 2)
+};
+
+template <int KS>
+struct Geom {
+  static constexpr int KP = 32 * KS;                                         // padded K
+  static constexpr int ROWB = 2 * KP;                                        // bytes of one bf16 plane row
+  static constexpr int STRIDE_B = ROWB + (((32 - ROWB) % 256) + 256) % 256;  // == 32 (mod 256)
+  static constexpr int STRIDE = STRIDE_B / 2;                                // in bf16
+  static constexpr int F4_PER_ROW = KP / 4;
+  static constexpr int F4_PER_TILE = kBM * F4_PER_ROW;
+};
+
+// W element (k, n) of the stacked [W0; W1] (zero outside)
+__device__ __forceinline__ float w_at(const DenseArgs& a, int k, int n) {
+  if (n >= a.N) return 0.0f;
+  if (k < a.K0) return a.W0[int64_t(k) * a.N + n];
+  k -= a.K0;
+  if (k < a.K1) return a.W1[int64_t(k) * a.N + n];
+  return 0.0f;
+}
+
+constexpr int kProducerWaves = 4;
+
+// WAVES consumer waves (MFMA + stores) and kProducerWaves producer waves
+// (global loads -> bf16x3 split -> LDS planes).  The roles only meet at one
+// workgroup barrier per tile: producers stage tile i+1 into one LDS buffer
+// while consumers run tile i from the other.  Keeping the loads (and their
+// vmcnt waits) in waves that issue no MFMA means a wait on a prefetch never
+// stalls the matrix pipe, and the consumers' output stores never delay a
+// prefetch wait.
+template <int KS, int WAVES, bool ACC, bool TWO>
+__global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(DenseArgs a) {
+  using G = Geom<KS>;
+  constexpr int TP = 64 * kProducerWaves;
+  static_assert(TP % G::F4_PER_ROW == 0, "producer load slots must tile whole rows");
+  constexpr int NL = G::F4_PER_TILE / TP;  // float4 loads per producer thread per tile
+  constexpr int RSTEP = TP / G::F4_PER_ROW;
+  __shared__ short As[2][3][kBM][G::STRIDE];
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+
+  int cg = 0;
+  int64_t pid = blockIdx.x, n_pairs = gridDim.x;
+  if (a.cg_count == 2) {
+    if (gridDim.x >= 16) {
+      cg = (blockIdx.x >> 3) & 1;
+      pid = (blockIdx.x & 7) | ((blockIdx.x >> 4) << 3);
+    } else {
+      cg = blockIdx.x & 1;
+      pid = blockIdx.x >> 1;
+    }
+    n_pairs = gridDim.x / 2;
+  }
+  const int64_t n_tiles = (a.M + kBM - 1) / kBM;
+  if (pid >= n_tiles) return;  // uniform per block
+  // tiles of this block: pid, pid + n_pairs, ... (both roles run the same count)
+  const int64_t my_tiles = (n_tiles - 1 - pid) / n_pairs + 1;
+
+  if (wave >= WAVES) {
+    // ---------------- producer ----------------
+    // slot j of a thread covers columns [kk, kk + 4) of the stacked [x0 | x1]
+    // row srow0 + j RSTEP.  Loads are raw buffer loads through a per-tile
+    // descriptor whose record count ends at the tile's last valid row: rows
+    // past M and K padding (offset 0x80000000) read as zero with no branch.
+    // They are issued as inline asm with explicit partial waits: the two
+    // register sets are always in flight in a fixed order, so staging one set
+    // waits with vmcnt(LPS) (the other set's loads stay in flight), where the
+    // compiler's own accounting would drain both (vmcnt(0)).
+    constexpr int LPS = TWO ? 2 * NL : NL;  // loads per register set
+    const int ptid = tid - 64 * WAVES;
+    const int kk = 4 * (ptid % G::F4_PER_ROW);
+    const int srow0 = ptid / G::F4_PER_ROW;
+    uint32_t vo0[NL], vo1[NL];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int64_t row = srow0 + j * RSTEP;
+      vo0[j] = kk < a.K0 ? uint32_t((row * a.ld0 + kk) * 4) : 0x80000000u;
+      vo1[j] = (kk >= a.K0 && kk - a.K0 < a.K1) ? uint32_t((row * a.ld1 + (kk - a.K0)) * 4) : 0x80000000u;
+    }
+    // buffer descriptor {base lo, base hi (stride 0), bytes, config} in SGPRs
+    auto rsrc = [&](const float* base, int64_t ld, int64_t tile) {
+      const int64_t r0 = tile * kBM;
+      int64_t rows = a.M - r0;
+      rows = rows < 0 ? 0 : (rows > kBM ? kBM : rows);
+      const uint64_t addr = reinterpret_cast<uint64_t>(base) + uint64_t(r0 * ld * 4);
+      u32x4 d;
+      d[0] = __builtin_amdgcn_readfirstlane(uint32_t(addr));
+      d[1] = __builtin_amdgcn_readfirstlane(uint32_t(addr >> 32) & 0xffffu);
+      d[2] = __builtin_amdgcn_readfirstlane(uint32_t(rows * ld * 4));
+      d[3] = 0x00020000u;
+      return d;
+    };
+    auto ld16 = [](f32x4& v, uint32_t off, const u32x4& d) {
+      asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(d) : "memory");
+    };
+    f32x4 p0[NL], q0[NL], p1[NL], q1[NL];  // register sets 0 / 1 (q: x1 columns)
+    auto load_tile = [&](f32x4(&p)[NL], f32x4(&q)[NL], int64_t tile) {
+      const u32x4 d0 = rsrc(a.x0 ? a.x0 : a.x1, a.ld0, tile);
+#pragma unroll
+      for (int j = 0; j < NL; ++j) ld16(p[j], vo0[j], d0);
+      if constexpr (TWO) {
+        const u32x4 d1 = rsrc(a.x1, a.ld1, tile);
+#pragma unroll
+        for (int j = 0; j < NL; ++j) ld16(q[j], vo1[j], d1);
+      }
+    };
+    // wait until at most `newer` loads are outstanding, then pin the set's
+    // registers behind the wait (the empty asm "redefines" them)
+    auto wait_set = [&](f32x4(&p)[NL], f32x4(&q)[NL], auto newer) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(decltype(newer)::value) : "memory");
+#pragma unroll
+      for (int j = 0; j < NL; ++j) {
+        asm volatile("" : "+v"(p[j]));
+        if constexpr (TWO) asm volatile("" : "+v"(q[j]));
+      }
+    };
+    auto stage = [&](const f32x4(&p)[NL], const f32x4(&q)[NL], int buf) {
+#pragma unroll
+      for (int j = 0; j < NL; ++j) {
+        const int row = srow0 + j * RSTEP;
+        f32x4 x = p[j];
+        if constexpr (TWO)  // each slot read zero bits from one of the two descriptors
+          x = __builtin_bit_cast(f32x4, __builtin_bit_cast(u32x4, p[j]) | __builtin_bit_cast(u32x4, q[j]));
+        const float v[4] = {x[0], x[1], x[2], x[3]};
+        bf16x4_t ph, pm, pl;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          short h, m, lo;
+          split3(v[e], h, m, lo);
+          ph[e] = h;
+          pm[e] = m;
+          pl[e] = lo;
+        }
+        *reinterpret_cast<bf16x4_t*>(&As[buf][0][row][kk]) = ph;
+        *reinterpret_cast<bf16x4_t*>(&As[buf][1][row][kk]) = pm;
+        *reinterpret_cast<bf16x4_t*>(&As[buf][2][row][kk]) = pl;
+      }
+    };
+    using Zero = std::integral_constant<int, 0>;
+    using Other = std::integral_constant<int, LPS>;
+    int64_t t = pid;
+    load_tile(p0, q0, t);
+    wait_set(p0, q0, Zero{});
+    stage(p0, q0, 0);
+    load_tile(p0, q0, t + n_pairs);
+    load_tile(p1, q1, t + 2 * n_pairs);
+    lds_barrier();
+    // iteration i: consumers run tile i from buffer i & 1; producers stage
+    // tile i + 1 (register set i & 1) into the other buffer and refill that
+    // set with tile i + 3.  Outstanding loads, oldest first: set i & 1, then
+    // the other set.
+    for (int64_t i = 0; i < my_tiles; i += 2) {
+      wait_set(p0, q0, Other{});
+      stage(p0, q0, 1);
+      load_tile(p0, q0, t + 3 * n_pairs);
+      lds_barrier();
+      if (i + 1 >= my_tiles) break;
+      wait_set(p1, q1, Other{});
+      stage(p1, q1, 0);
+      load_tile(p1, q1, t + 4 * n_pairs);
+      lds_barrier();
+      t += 2 * n_pairs;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no loads in flight at exit
+    return;
+  }
+
+  // ---------------- consumer ----------------
+  const int l = tid & 63;
+  const int lr = l & 15;  // fragment row / column
+  const int lq = l >> 4;  // fragment k-chunk / row quad
+  const int n_col = cg * 16 * WAVES + wave * 16 + lr;  // this lane's output column
+
+  // W's split fragments for this wave's columns: lane holds B[k = 32 s + 8 lq + j][n_col]
+  bf16x8_t wh[KS], wm[KS], wl[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      short h, m, lo;
+      split3(w_at(a, 32 * s + 8 * lq + j, n_col), h, m, lo);
+      wh[s][j] = h;
+      wm[s][j] = m;
+      wl[s][j] = lo;
+    }
+  const float bcol = (a.bias && n_col < a.N) ? a.bias[n_col] : 0.0f;
+  const bool wave_cols_full = __builtin_amdgcn_readfirstlane(n_col - lr + 16) <= a.N;  // wave-uniform
+  lds_barrier();
+
+  int64_t t = pid;
+  for (int64_t i = 0; i < my_tiles; ++i, t += n_pairs) {
+    const int buf = int(i & 1);
+    f32x4 acc[2];
+    acc[0] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    acc[1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      bf16x8_t ah[2], am[2], al[2];
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int row = 16 * r + lr;
+        const int k = 32 * s + 8 * lq;
+        ah[r] = *reinterpret_cast<const bf16x8_t*>(&As[buf][0][row][k]);
+        am[r] = *reinterpret_cast<const bf16x8_t*>(&As[buf][1][row][k]);
+        al[r] = *reinterpret_cast<const bf16x8_t*>(&As[buf][2][row][k]);
+      }
+      // small terms first; two independent accumulator chains (row tiles)
+#pragma unroll
+      for (int r = 0; r < 2; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[r], wh[s], acc[r], 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 2; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[r], wl[s], acc[r], 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 2; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[r], wm[s], acc[r], 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 2; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[r], wh[s], acc[r], 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 2; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[r], wm[s], acc[r], 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 2; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[r], wh[s], acc[r], 0, 0, 0);
+    }
+    // epilogue: lane holds rows 4 lq + j of column lr of each 16x16 block
+    const int64_t r0 = t * kBM;
+    auto put = [&](int r, int j) {
+      float* o = a.out + (r0 + 16 * r + 4 * lq + j) * a.ld_out + n_col;
+      float v = acc[r][j] + bcol;
+      if constexpr (ACC) v = __fadd_rn(*o, v);
+      if (a.relu) v = fmaxf(v, 0.0f);
+      *o = v;
+    };
+    if (wave_cols_full && r0 + kBM <= a.M) {
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) put(r, j);
+    } else if (n_col < a.N) {
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (r0 + 16 * r + 4 * lq + j < a.M) put(r, j);
+    }
+    lds_barrier();  // buffer `buf` free for the producers; the stores stay in flight
+  }
+}
+
+template <int KS, int WAVES>
+int launch(const DenseArgs& a, hipStream_t s) {
+  auto k = a.accumulate ? (a.K1 > 0 ? dense_kernel<KS, WAVES, true, true> : dense_kernel<KS, WAVES, true, false>)
+                        : (a.K1 > 0 ? dense_kernel<KS, WAVES, false, true> : dense_kernel<KS, WAVES, false, false>);
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 64 * (WAVES + kProducerWaves), 0) != hipSuccess ||
+      per_cu <= 0)
+    per_cu = 1;
+  const int64_t n_tiles = (a.M + kBM - 1) / kBM;
+  const int64_t cap = int64_t(per_cu) * cus;
+  const int64_t want = n_tiles * a.cg_count;
+  int64_t grid = want < cap ? want : cap;
+  if (a.cg_count == 2) grid = grid >= 16 ? grid / 16 * 16 : grid / 2 * 2;  // whole XCD pairs
+  hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(64 * (WAVES + kProducerWaves)), 0, s, a);
+  KGX_CHECK_LAUNCH();
+  return KGX_OK;
+}
+
+// K padded to 32, 64, 128 or 256 (whole rows per load slot; see load_tile)
+template <int WAVES>
+int launch_ks(int K, const DenseArgs& a, hipStream_t s) {
+  if (K <= 32) return launch<1, WAVES>(a, s);
+  if (K <= 64) return launch<2, WAVES>(a, s);
+  if (K <= 128) return launch<4, WAVES>(a, s);
+  return launch<8, WAVES>(a, s);
+}
+
+}  // namespace
+}  // namespace kgx
+
+using namespace kgx;
+
+extern "C" int kgx_dense(int64_t M, const float* x0, int64_t ld_x0, int64_t K0, const float* W0,
+                         const float* x1, int64_t ld_x1, int64_t K1, const float* W1, int64_t N,
+                         const float* bias, int flags, float* out, int64_t ld_out, kgx_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  KGX_REQUIRE(M >= 0 && K0 >= 0 && K1 >= 0 && N >= 0, KGX_ERR_ARG, "kgx_dense: negative size");
+  KGX_REQUIRE((flags & ~(KGX_DENSE_RELU | KGX_DENSE_ACCUMULATE)) == 0, KGX_ERR_ARG, "kgx_dense: unknown flags 0x%x",
+              flags);
+  KGX_REQUIRE(K0 + K1 <= KGX_DENSE_MAX_K && N <= KGX_DENSE_MAX_N, KGX_ERR_UNSUPPORTED,
+              "kgx_dense: K0 + K1 must be <= %d and N <= %d (got K %lld, N %lld)", KGX_DENSE_MAX_K,
+              KGX_DENSE_MAX_N, (long long)(K0 + K1), (long long)N);
+  KGX_REQUIRE(K0 % 4 == 0 && K1 % 4 == 0, KGX_ERR_UNSUPPORTED, "kgx_dense: K0 and K1 must be multiples of 4");
+  if (M == 0 || N == 0) return KGX_OK;
+  KGX_REQUIRE(out && ld_out >= N, KGX_ERR_ARG, "kgx_dense: null out or ld_out < N");
+  KGX_REQUIRE(K0 == 0 || (x0 && W0 && ld_x0 >= K0 && ld_x0 % 4 == 0 && reinterpret_cast<uintptr_t>(x0) % 16 == 0),
+              KGX_ERR_ARG, "kgx_dense: x0 must be 16-byte aligned with ld %% 4 == 0 and ld >= K0");
+  KGX_REQUIRE(K1 == 0 || (x1 && W1 && ld_x1 >= K1 && ld_x1 % 4 == 0 && reinterpret_cast<uintptr_t>(x1) % 16 == 0),
+              KGX_ERR_ARG, "kgx_dense: x1 must be 16-byte aligned with ld %% 4 == 0 and ld >= K1");
+  KGX_REQUIRE(ld_x0 < (int64_t(1) << 24) && ld_x1 < (int64_t(1) << 24), KGX_ERR_ARG,
+              "kgx_dense: x leading dimension >= 2^24 (32-bit tile offsets)");
+  DenseArgs a{};
+  a.M = M;
+  a.x0 = x0;
+  a.ld0 = ld_x0;
+  a.K0 = int(K0);
+  a.x1 = x1;
+  a.ld1 = ld_x1;
+  a.K1 = int(K1);
+  a.W0 = W0;
+  a.W1 = W1;
+  a.N = int(N);
+  a.bias = bias;
+  a.out = out;
+  a.ld_out = ld_out;
+  a.relu = (flags & KGX_DENSE_RELU) != 0;
+  a.accumulate = (flags & KGX_DENSE_ACCUMULATE) != 0;
+  const int K = int(K0 + K1);
+  a.cg_count = N <= 128 ? 1 : 2;
+  if (N <= 64) return launch_ks<4>(K, a, stream);
+  return launch_ks<8>(K, a, stream);
+}

@@ -27,6 +27,7 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "kgx_bf16x3.h"
 #include "kgx_internal.h"
 #include "kgx_vec.h"
 
@@ -81,29 +82,13 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 // ---- three-way bf16 split of f32 operands (the "bf16x3" product) ---------
-// x = hi + mid + lo exactly (each a bf16, round-to-nearest-even residuals;
-// non-finite x keeps hi = x and zero residuals).  x*w is then taken as the six
-// bf16 x bf16 products whose orders sum to <= 2 (dropped terms are <= 2^-24
-// |x w|, the f32 rounding level), each exact in the MFMA's f32 accumulator,
-// on v_mfma_f32_16x16x32_bf16 -- 16x the per-clock rate of the f32-input MFMA.
+// split3 (kgx_bf16x3.h): x = hi + mid + lo; x*w is taken as the six
+// significant bf16 x bf16 products (dropped terms <= 2^-24 |x w|), each exact
+// in the MFMA's f32 accumulator, on v_mfma_f32_16x16x32_bf16 -- 16x the
+// per-clock rate of the f32-input MFMA.  Infinite / NaN aggregates follow
+// IEEE f32 products (kgx_bf16x3.h).
 typedef short bf16x8_t __attribute__((ext_vector_type(8)));
 typedef short bf16x4_t __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ short bf16_bits(float x) {
-  const __bf16 h = static_cast<__bf16>(x);  // v_cvt_pk_bf16_f32 (RNE, NaN-preserving)
-  return __builtin_bit_cast(short, h);
-}
-__device__ __forceinline__ float bf16_value(short b) {
-  return __builtin_bit_cast(float, static_cast<uint32_t>(static_cast<uint16_t>(b)) << 16);
-}
-__device__ __forceinline__ __attribute__((unused)) void split3(float x, short& hi, short& mid, short& lo) {
-  hi = bf16_bits(x);
-  const float h = bf16_value(hi);
-  float r = __builtin_isfinite(h) ? __fsub_rn(x, h) : 0.0f;  // exact
-  mid = bf16_bits(r);
-  r = __fsub_rn(r, bf16_value(mid));  // exact
-  lo = bf16_bits(r);
-}
 
 template <int RED>
 struct Red {

@@ -23,6 +23,8 @@ SUM, MEAN, MAX, MIN, STD = range(5)
 EPI_NONE, EPI_BIAS, EPI_GIN, EPI_RAW = range(4)
 FUSED_PRE_GIN, FUSED_ACCUMULATE, FUSED_SHARE_GPU, FUSED_RELU = 1, 2, 4, 8
 CSR_SELF_LOOPS, CSR_SEGMENT_ONLY, CSR_GCN_NORM = 1, 2, 4
+DENSE_RELU, DENSE_ACCUMULATE = 1, 2
+DENSE_MAX_K, DENSE_MAX_N = 256, 256
 
 REDUCE_IDS = {"sum": SUM, "mean": MEAN, "max": MAX, "min": MIN, "std": STD}
 
@@ -72,6 +74,9 @@ _SIGNATURES = {
         _i32p, _i32p, _i64, _i32p, _i64, _i32p, _i64,
         _i32p, _f32p, _f32p, _i64, _f32p, _int, _int, ctypes.c_float,
         _f32p, _i64, _f32p, _f32p, _f32p, _i32p, ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p,
+    ],
+    "kgx_dense": [
+        _i64, _f32p, _i64, _i64, _f32p, _f32p, _i64, _i64, _f32p, _i64, _f32p, _int, _f32p, _i64, ctypes.c_void_p,
     ],
     "kgx_gather_rows": [_f32p, _i64, _i32p, _i64, _i64, _f32p, _i64, ctypes.c_void_p],
     "kgx_scatter_f32": [_f32p, _i32p, _i64, _f32p, ctypes.c_void_p],

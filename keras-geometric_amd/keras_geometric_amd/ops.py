@@ -732,3 +732,119 @@ def gatv2_aggregate(
         return _GATv2Fn.apply(h_src, h_dst, att, bias, g, heads, channels, negative_slope, exact, float(dropout),
                               int(seed))
     return _gatv2_raw(g, h_src, h_dst, att, heads, channels, negative_slope, bias, exact, float(dropout), int(seed))
+
+
+# ---------------------------------------------------------------------------
+# Dense node transform: kgx_dense (bf16x3-split MFMA, f32-accurate)
+# ---------------------------------------------------------------------------
+def _aligned16(t: torch.Tensor) -> torch.Tensor:
+    """Contiguous fp32 rows on a 16-byte boundary (what kgx_dense's dwordx4 loads need)."""
+    t = _f32c(t)
+    return t if t.data_ptr() % 16 == 0 else t.clone()
+
+
+def dense_supported(x0: torch.Tensor, W0: torch.Tensor, W1: torch.Tensor | None = None) -> bool:
+    """Shapes kgx_dense implements: K0 + K1 <= 256, N <= 256, K0, K1 multiples of 4."""
+    if not (x0.is_cuda and x0.dim() == 2 and W0.dim() == 2):
+        return False
+    k0, n = W0.shape
+    k1 = 0 if W1 is None else W1.shape[0]
+    return (0 < n <= nat.DENSE_MAX_N and k0 + k1 <= nat.DENSE_MAX_K and k0 % 4 == 0 and k1 % 4 == 0
+            and (W1 is None or W1.shape[1] == n))
+
+
+@torch.library.custom_op("kgx::dense", mutates_args=())
+def dense_op(
+    x0: torch.Tensor,
+    W0: torch.Tensor,
+    x1: Optional[torch.Tensor],
+    W1: Optional[torch.Tensor],
+    bias: Optional[torch.Tensor],
+    relu: bool,
+) -> torch.Tensor:
+    x0, W0, bias = _aligned16(x0), _f32c(W0), _f32c(bias)
+    x1 = None if x1 is None else _aligned16(x1)
+    W1 = None if W1 is None else _f32c(W1)
+    dev = nat.require_device(x0, W0, x1, W1, bias)
+    M, N = x0.shape[0], W0.shape[1]
+    if x1 is not None and x1.shape[0] != M:
+        raise ValueError(f"kgx.dense: x1 has {x1.shape[0]} rows, x0 has {M}")
+    out = torch.empty((M, N), dtype=torch.float32, device=dev)
+    nat.check(
+        nat.lib().kgx_dense(
+            M, nat.ptr(x0), x0.stride(0), x0.shape[1], nat.ptr(W0),
+            nat.ptr(x1), x1.stride(0) if x1 is not None else 0, x1.shape[1] if x1 is not None else 0, nat.ptr(W1),
+            N, nat.ptr(bias), nat.DENSE_RELU if relu else 0, nat.ptr(out), out.stride(0), nat.stream(dev),
+        ),
+        "kgx_dense",
+    )
+    return out
+
+
+@dense_op.register_fake
+def _dense_fake(x0, W0, x1, W1, bias, relu):
+    return x0.new_empty((x0.shape[0], W0.shape[1]))
+
+
+def _matmul_t(g: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
+    """g @ W^T on kgx_dense when the transposed shape fits, else the library GEMM."""
+    Wt = W.t().contiguous()
+    if dense_supported(g, Wt):
+        return torch.ops.kgx.dense(g, Wt, None, None, None, False)
+    return g @ W.t()
+
+
+class _DenseFn(torch.autograd.Function):
+    """y = relu?(bias + x0 W0 + x1 W1).  Backward: dz = dy * (y > 0) for ReLU;
+    dx_t = dz W_t^T (kgx_dense again), dW_t = x_t^T dz (split-K), db = sum dz."""
+
+    @staticmethod
+    def forward(ctx, x0, W0, x1, W1, bias, relu):
+        y = torch.ops.kgx.dense(x0, W0, x1, W1, bias, relu)
+        ctx.relu = relu
+        ctx.save_for_backward(x0, W0, x1, W1, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, grad):
+        x0, W0, x1, W1, y = ctx.saved_tensors
+        dz = grad.contiguous()
+        if ctx.relu:
+            dz = dz * (y > 0)
+        g = [None] * 6
+        if ctx.needs_input_grad[0]:
+            g[0] = _matmul_t(dz, W0)
+        if ctx.needs_input_grad[1]:
+            g[1] = _gemm_tn_tall(x0, dz)
+        if x1 is not None and ctx.needs_input_grad[2]:
+            g[2] = _matmul_t(dz, W1)
+        if x1 is not None and ctx.needs_input_grad[3]:
+            g[3] = _gemm_tn_tall(x1, dz)
+        if ctx.needs_input_grad[4]:
+            g[4] = dz.sum(0)
+        return tuple(g)
+
+
+def dense(
+    x0: torch.Tensor,
+    W0: torch.Tensor,
+    bias: torch.Tensor | None = None,
+    *,
+    x1: torch.Tensor | None = None,
+    W1: torch.Tensor | None = None,
+    relu: bool = False,
+) -> torch.Tensor:
+    """relu?(bias + x0 @ W0 (+ x1 @ W1)) -- keras Dense / SAGEConv's two linear
+    maps in one kgx_dense launch (differentiable).  Shapes kgx_dense does not
+    implement (K > 256, N > 256, K % 4 != 0) run as the library GEMM
+    (hipBLASLt) on the same device."""
+    if (x1 is None) != (W1 is None):
+        raise ValueError("dense: x1 and W1 go together")
+    if dense_supported(x0, W0, W1):
+        if _needs_grad(x0, W0, x1, W1, bias):
+            return _DenseFn.apply(x0, W0, x1, W1, bias, bool(relu))
+        return torch.ops.kgx.dense(x0, W0, x1, W1, bias, bool(relu))
+    y = torch.addmm(bias, x0, W0) if bias is not None else x0 @ W0
+    if x1 is not None:
+        y = torch.addmm(y, x1, W1)
+    return torch.relu(y) if relu else y
