@@ -25,6 +25,7 @@
 // v_mfma_f32_16x16x32_bf16 over K for its columns and stores its 16x16 blocks
 // with the bias / ReLU / accumulate epilogue.  One LDS barrier per tile.
 #include <type_traits>
+#include <utility>
 
 #include "kgx_bf16x3.h"
 #include "kgx_internal.h"
@@ -64,6 +65,7 @@ struct DenseArgs {
   int relu;
   int accumulate;
   int cg_count;  // column groups of 16 WAVES columns (1 or 2)
+  int debug;     // experiment builds only (-DKGX_EXPERIMENTS, env KGX_DENSE_DEBUG): 1 skip MFMA, 2 skip stores
 };
 
 template <int KS>
@@ -134,6 +136,12 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
     // waits with vmcnt(LPS) (the other set's loads stay in flight), where the
     // compiler's own accounting would drain both (vmcnt(0)).
     constexpr int LPS = TWO ? 2 * NL : NL;  // loads per register set
+    // register sets in flight: about 128 KB of x per CU (4 x 32 KB tiles at
+    // K 256, 8 x 16 KB at K 128; half with two operands, whose sets take
+    // twice the registers).  The loads are latency-bound, not bandwidth-bound,
+    // below that: 64 KB per CU measured 3 TB/s.
+    constexpr int NSETS_ = (32 / KS < 2 ? 2 : (32 / KS > 8 ? 8 : 32 / KS));
+    constexpr int NSETS = TWO ? (NSETS_ / 2 < 2 ? 2 : NSETS_ / 2) : NSETS_;
     const int ptid = tid - 64 * WAVES;
     const int kk = 4 * (ptid % G::F4_PER_ROW);
     const int srow0 = ptid / G::F4_PER_ROW;
@@ -160,7 +168,7 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
     auto ld16 = [](f32x4& v, uint32_t off, const u32x4& d) {
       asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(d) : "memory");
     };
-    f32x4 p0[NL], q0[NL], p1[NL], q1[NL];  // register sets 0 / 1 (q: x1 columns)
+    f32x4 P[NSETS][NL], Q[NSETS][NL];  // register sets (Q: x1 columns)
     auto load_tile = [&](f32x4(&p)[NL], f32x4(&q)[NL], int64_t tile) {
       const u32x4 d0 = rsrc(a.x0 ? a.x0 : a.x1, a.ld0, tile);
 #pragma unroll
@@ -188,45 +196,52 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
         f32x4 x = p[j];
         if constexpr (TWO)  // each slot read zero bits from one of the two descriptors
           x = __builtin_bit_cast(f32x4, __builtin_bit_cast(u32x4, p[j]) | __builtin_bit_cast(u32x4, q[j]));
-        const float v[4] = {x[0], x[1], x[2], x[3]};
-        bf16x4_t ph, pm, pl;
+        uint32_t h[2], m[2], lo[2];
+        bool bad;
+        split3x4_fast(x, h, m, lo, bad);
+        if (bad) {  // inf / NaN / near-FLT_MAX values: the exact scalar split (rare)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          short h, m, lo;
-          split3(v[e], h, m, lo);
-          ph[e] = h;
-          pm[e] = m;
-          pl[e] = lo;
+          for (int e = 0; e < 4; e += 2) {
+            short h0, m0, l0, h1, m1, l1;
+            split3(x[e], h0, m0, l0);
+            split3(x[e + 1], h1, m1, l1);
+            h[e / 2] = uint32_t(uint16_t(h0)) | (uint32_t(uint16_t(h1)) << 16);
+            m[e / 2] = uint32_t(uint16_t(m0)) | (uint32_t(uint16_t(m1)) << 16);
+            lo[e / 2] = uint32_t(uint16_t(l0)) | (uint32_t(uint16_t(l1)) << 16);
+          }
         }
-        *reinterpret_cast<bf16x4_t*>(&As[buf][0][row][kk]) = ph;
-        *reinterpret_cast<bf16x4_t*>(&As[buf][1][row][kk]) = pm;
-        *reinterpret_cast<bf16x4_t*>(&As[buf][2][row][kk]) = pl;
+        *reinterpret_cast<uint2*>(&As[buf][0][row][kk]) = make_uint2(h[0], h[1]);
+        *reinterpret_cast<uint2*>(&As[buf][1][row][kk]) = make_uint2(m[0], m[1]);
+        *reinterpret_cast<uint2*>(&As[buf][2][row][kk]) = make_uint2(lo[0], lo[1]);
       }
     };
     using Zero = std::integral_constant<int, 0>;
-    using Other = std::integral_constant<int, LPS>;
+    using Others = std::integral_constant<int, (NSETS - 1) * LPS>;
+    static_assert((NSETS - 1) * LPS <= 63, "vmcnt immediate");
     int64_t t = pid;
-    load_tile(p0, q0, t);
-    wait_set(p0, q0, Zero{});
-    stage(p0, q0, 0);
-    load_tile(p0, q0, t + n_pairs);
-    load_tile(p1, q1, t + 2 * n_pairs);
+    load_tile(P[0], Q[0], t);
+    wait_set(P[0], Q[0], Zero{});
+    stage(P[0], Q[0], 0);
+#pragma unroll
+    for (int k = 0; k < NSETS; ++k) load_tile(P[k], Q[k], t + (k + 1) * n_pairs);
     lds_barrier();
-    // iteration i: consumers run tile i from buffer i & 1; producers stage
-    // tile i + 1 (register set i & 1) into the other buffer and refill that
-    // set with tile i + 3.  Outstanding loads, oldest first: set i & 1, then
-    // the other set.
-    for (int64_t i = 0; i < my_tiles; i += 2) {
-      wait_set(p0, q0, Other{});
-      stage(p0, q0, 1);
-      load_tile(p0, q0, t + 3 * n_pairs);
-      lds_barrier();
-      if (i + 1 >= my_tiles) break;
-      wait_set(p1, q1, Other{});
-      stage(p1, q1, 0);
-      load_tile(p1, q1, t + 4 * n_pairs);
-      lds_barrier();
-      t += 2 * n_pairs;
+    // step i (tile i of this block): consumers run tile i from buffer i & 1;
+    // producers stage tile i + 1 (register set i % NSETS) into the other
+    // buffer and refill that set with tile i + 1 + NSETS.  Outstanding loads,
+    // oldest first, are the sets in cyclic order, so a set's wait leaves the
+    // other NSETS - 1 sets in flight.
+    for (int64_t i = 0; i < my_tiles; i += NSETS, t += NSETS * n_pairs) {
+      bool done = false;
+#pragma unroll
+      for (int k = 0; k < NSETS; ++k) {
+        if (!done) {
+          wait_set(P[k], Q[k], Others{});
+          stage(P[k], Q[k], int((i + k + 1) & 1));
+          load_tile(P[k], Q[k], t + (k + 1 + NSETS) * n_pairs);
+          lds_barrier();
+          done = i + k + 1 >= my_tiles;
+        }
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no loads in flight at exit
     return;
@@ -251,7 +266,9 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
       wl[s][j] = lo;
     }
   const float bcol = (a.bias && n_col < a.N) ? a.bias[n_col] : 0.0f;
-  const bool wave_cols_full = __builtin_amdgcn_readfirstlane(n_col - lr + 16) <= a.N;  // wave-uniform
+  // byte offset of this lane's first output element within a tile (row 4 lq, column n_col);
+  // out-of-range for columns past N, so their stores are dropped
+  const uint32_t out_lane = n_col < a.N ? uint32_t((4 * lq * a.ld_out + n_col) * 4) : 0x80000000u;
   lds_barrier();
 
   int64_t t = pid;
@@ -260,51 +277,92 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
     f32x4 acc[2];
     acc[0] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     acc[1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      bf16x8_t ah[2], am[2], al[2];
+    // A fragments are software-pipelined one k-step ahead: the six LDS reads
+    // of step s + 1 are issued (inline asm, so the scheduler cannot sink them
+    // next to their use) before step s's 12 MFMAs, and step s waits with
+    // lgkmcnt(6), leaving step s + 1's reads in flight.  The empty asm after
+    // each wait pins the fragments (and the accumulators, which orders the
+    // MFMAs of step s before the wait of step s + 1).
+    struct Frags {
+      bf16x8_t h[2], m[2], l[2];
+    };
+    const uint32_t lds_lane = uint32_t(reinterpret_cast<uintptr_t>(&As[buf][0][lr][8 * lq]));
+    auto read_frags = [](Frags& f, auto S, uint32_t lane) {
+      constexpr int s = decltype(S)::value;
+      constexpr uint32_t P = uint32_t(kBM) * G::STRIDE * 2;  // bytes per plane
+      constexpr uint32_t R = 16u * G::STRIDE * 2;            // bytes per 16 rows
+      constexpr uint32_t K = 64u * s;                        // 32 bf16 per k-step
 #pragma unroll
       for (int r = 0; r < 2; ++r) {
-        const int row = 16 * r + lr;
-        const int k = 32 * s + 8 * lq;
-        ah[r] = *reinterpret_cast<const bf16x8_t*>(&As[buf][0][row][k]);
-        am[r] = *reinterpret_cast<const bf16x8_t*>(&As[buf][1][row][k]);
-        al[r] = *reinterpret_cast<const bf16x8_t*>(&As[buf][2][row][k]);
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f.h[r]) : "v"(lane), "i"(0 * P + R * r + K));
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f.m[r]) : "v"(lane), "i"(1 * P + R * r + K));
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f.l[r]) : "v"(lane), "i"(2 * P + R * r + K));
       }
-      // small terms first; two independent accumulator chains (row tiles)
-#pragma unroll
-      for (int r = 0; r < 2; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[r], wh[s], acc[r], 0, 0, 0);
-#pragma unroll
-      for (int r = 0; r < 2; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[r], wl[s], acc[r], 0, 0, 0);
-#pragma unroll
-      for (int r = 0; r < 2; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[r], wm[s], acc[r], 0, 0, 0);
-#pragma unroll
-      for (int r = 0; r < 2; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[r], wh[s], acc[r], 0, 0, 0);
-#pragma unroll
-      for (int r = 0; r < 2; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[r], wm[s], acc[r], 0, 0, 0);
-#pragma unroll
-      for (int r = 0; r < 2; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[r], wh[s], acc[r], 0, 0, 0);
-    }
-    // epilogue: lane holds rows 4 lq + j of column lr of each 16x16 block
-    const int64_t r0 = t * kBM;
-    auto put = [&](int r, int j) {
-      float* o = a.out + (r0 + 16 * r + 4 * lq + j) * a.ld_out + n_col;
-      float v = acc[r][j] + bcol;
-      if constexpr (ACC) v = __fadd_rn(*o, v);
-      if (a.relu) v = fmaxf(v, 0.0f);
-      *o = v;
     };
-    if (wave_cols_full && r0 + kBM <= a.M) {
+    auto wait_frags = [](Frags& f, f32x4(&acc)[2], auto N) {
+      asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(decltype(N)::value) : "memory");
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        asm volatile("" : "+v"(f.h[r]), "+v"(f.m[r]), "+v"(f.l[r]), "+v"(acc[r]));
+      }
+    };
+    Frags fa, fb;
+    if (!(a.debug & 1)) {
+      read_frags(fa, std::integral_constant<int, 0>{}, lds_lane);
+      auto step = [&](auto S) {
+        constexpr int s = decltype(S)::value;
+        Frags& cur = (s & 1) ? fb : fa;
+        Frags& nxt = (s & 1) ? fa : fb;
+        if constexpr (s + 1 < KS) {
+          read_frags(nxt, std::integral_constant<int, s + 1>{}, lds_lane);
+          wait_frags(cur, acc, std::integral_constant<int, 6>{});
+        } else {
+          wait_frags(cur, acc, std::integral_constant<int, 0>{});
+        }
+        // small terms first; two independent accumulator chains (row tiles)
+#pragma unroll
+        for (int r = 0; r < 2; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.l[r], wh[s], acc[r], 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.h[r], wl[s], acc[r], 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.m[r], wm[s], acc[r], 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.m[r], wh[s], acc[r], 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.h[r], wm[s], acc[r], 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.h[r], wh[s], acc[r], 0, 0, 0);
+      };
+      [&]<int... S>(std::integer_sequence<int, S...>) {
+        (step(std::integral_constant<int, S>{}), ...);
+      }(std::make_integer_sequence<int, KS>{});
+    }
+    // epilogue: lane holds rows 4 lq + j of column lr of each 16x16 block.
+    // Raw buffer stores through a per-tile descriptor: rows past M fall
+    // outside its record count and columns past N carry an out-of-range
+    // offset, so both are dropped by the range check (no branches); the
+    // per-row part of the offset is wave-uniform (soffset).
+    if (!(a.debug & 2)) {
+      const int64_t r0 = t * kBM;
+      int64_t rows = a.M - r0;
+      rows = rows > kBM ? kBM : rows;
+      const uint64_t addr = reinterpret_cast<uint64_t>(a.out) + uint64_t(r0 * a.ld_out * 4);
+      const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(addr));
+      const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(addr >> 32));
+      const int bytes = __builtin_amdgcn_readfirstlane(int(rows * a.ld_out * 4));
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((uint64_t(hi) << 32) | lo), 0,
+                                                        bytes, 0x00020000);
 #pragma unroll
       for (int r = 0; r < 2; ++r)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) put(r, j);
-    } else if (n_col < a.N) {
-#pragma unroll
-      for (int r = 0; r < 2; ++r)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (r0 + 16 * r + 4 * lq + j < a.M) put(r, j);
+        for (int j = 0; j < 4; ++j) {
+          const int soff = int((16 * r + j) * a.ld_out * 4);
+          float v = acc[r][j] + bcol;
+          if constexpr (ACC)
+            v = __fadd_rn(__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, out_lane, soff, 0)), v);
+          if (a.relu) v = fmaxf(v, 0.0f);
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rs, out_lane, soff, 0);
+        }
     }
     lds_barrier();  // buffer `buf` free for the producers; the stores stay in flight
   }
@@ -366,8 +424,8 @@ extern "C" int kgx_dense(int64_t M, const float* x0, int64_t ld_x0, int64_t K0, 
               KGX_ERR_ARG, "kgx_dense: x0 must be 16-byte aligned with ld %% 4 == 0 and ld >= K0");
   KGX_REQUIRE(K1 == 0 || (x1 && W1 && ld_x1 >= K1 && ld_x1 % 4 == 0 && reinterpret_cast<uintptr_t>(x1) % 16 == 0),
               KGX_ERR_ARG, "kgx_dense: x1 must be 16-byte aligned with ld %% 4 == 0 and ld >= K1");
-  KGX_REQUIRE(ld_x0 < (int64_t(1) << 24) && ld_x1 < (int64_t(1) << 24), KGX_ERR_ARG,
-              "kgx_dense: x leading dimension >= 2^24 (32-bit tile offsets)");
+  KGX_REQUIRE(ld_x0 < (int64_t(1) << 24) && ld_x1 < (int64_t(1) << 24) && ld_out < (int64_t(1) << 24), KGX_ERR_ARG,
+              "kgx_dense: leading dimension >= 2^24 (32-bit tile offsets)");
   DenseArgs a{};
   a.M = M;
   a.x0 = x0;
@@ -386,6 +444,13 @@ extern "C" int kgx_dense(int64_t M, const float* x0, int64_t ld_x0, int64_t K0, 
   a.accumulate = (flags & KGX_DENSE_ACCUMULATE) != 0;
   const int K = int(K0 + K1);
   a.cg_count = N <= 128 ? 1 : 2;
+#ifdef KGX_EXPERIMENTS  // cost-decomposition knob; never in a product build (it changes results)
+  static const int dbg = [] {
+    const char* h = getenv("KGX_DENSE_DEBUG");
+    return h ? atoi(h) : 0;
+  }();
+  a.debug = dbg;
+#endif
   if (N <= 64) return launch_ks<4>(K, a, stream);
   return launch_ks<8>(K, a, stream);
 }

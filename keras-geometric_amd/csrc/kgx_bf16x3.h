@@ -42,4 +42,37 @@ __device__ __forceinline__ void split3(float x, short& hi, short& mid, short& lo
   lo = fin ? l : bf16_bits(x);  // +-inf / NaN: lo plane only (see above)
 }
 
+// Packed split of four values for staging loops (about 5 VALU ops per value
+// instead of ~19): pairs go through v_cvt_pk_bf16_f32 and v_pk_add_f32, and
+// each plane comes out as a bf16x4 (two packed dwords) ready for one 8-byte
+// LDS store.  Valid only when every hi value is finite and their sum does not
+// overflow; `bad` is set otherwise (inf / NaN, or |x| near FLT_MAX), and the
+// caller redoes those values with split3.
+typedef float kgx_f32x2 __attribute__((ext_vector_type(2)));
+typedef float kgx_f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 kgx_bf16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t bf16_pack2(kgx_f32x2 v) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, kgx_bf16x2));  // RNE
+}
+__device__ __forceinline__ kgx_f32x2 bf16_unpack2(uint32_t p) {
+  return kgx_f32x2{__builtin_bit_cast(float, p << 16), __builtin_bit_cast(float, p & 0xffff0000u)};
+}
+__device__ __forceinline__ void split3x4_fast(kgx_f32x4 x, uint32_t (&h)[2], uint32_t (&m)[2], uint32_t (&l)[2],
+                                              bool& bad) {
+  const kgx_f32x2 a = {x[0], x[1]}, b = {x[2], x[3]};
+  h[0] = bf16_pack2(a);
+  h[1] = bf16_pack2(b);
+  const kgx_f32x2 ha = bf16_unpack2(h[0]), hb = bf16_unpack2(h[1]);
+  const kgx_f32x2 hs = ha + hb;
+  bad = !__builtin_isfinite(hs[0] + hs[1]);
+  kgx_f32x2 ra = a - ha, rb = b - hb;  // exact
+  m[0] = bf16_pack2(ra);
+  m[1] = bf16_pack2(rb);
+  ra = ra - bf16_unpack2(m[0]);  // exact
+  rb = rb - bf16_unpack2(m[1]);
+  l[0] = bf16_pack2(ra);
+  l[1] = bf16_pack2(rb);
+}
+
 }  // namespace kgx

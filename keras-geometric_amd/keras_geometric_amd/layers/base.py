@@ -287,6 +287,14 @@ class Dense(Layer):
         return self.call(x)
 
     def call(self, x):
+        if x.dim() == 2 and x.is_cuda:
+            from .. import ops as kops  # deferred: ops imports the layers' graph cache
+
+            if kops.dense_supported(x, self.kernel):
+                # kgx_dense: bias and ReLU in the MFMA kernel's epilogue (differentiable)
+                relu = self.activation is torch.relu
+                y = kops.dense(x, self.kernel, self.bias if self.use_bias else None, relu=relu)
+                return y if (relu or self.activation is None) else self.activation(y)
         if self.use_bias and x.dim() == 2:
             if self.activation is torch.relu and x.is_cuda and not torch.is_grad_enabled():
                 # inference: bias + ReLU in the GEMM epilogue (one pass over the output;

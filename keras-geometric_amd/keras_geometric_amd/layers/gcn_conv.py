@@ -119,7 +119,7 @@ class GCNConv(MessagePassing):
             # aggregate-then-transform in one launch (W on f32 MFMA in the epilogue)
             return kops.aggregate_transform(g, x.contiguous(), self.kernel, "sum", weighted=self.normalize,
                                             bias=self.bias if use_b else None)
-        h = torch.matmul(x, self.kernel)  # node-level X W (MFMA GEMM)
+        h = kops.dense(x, self.kernel)  # node-level X W (kgx_dense on MFMA; library GEMM past 256)
         return kops.aggregate(
             g, h, "sum", weighted=self.normalize,
             epilogue=nat.EPI_BIAS if use_b else nat.EPI_NONE, bias=self.bias if use_b else None,

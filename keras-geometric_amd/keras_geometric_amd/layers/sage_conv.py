@@ -138,17 +138,14 @@ class SAGEConv(MessagePassing):
         """lin_neigh(aggr) + lin_self(x) + bias, activation, L2 norm (sage_conv.py:409-439);
         also the update step of distributed.ShardedSAGEConv on a shard's rows."""
         use_b = self.use_bias and self.bias is not None
+        relu = self.activation is torch.relu
         if self.root_weight and self.lin_self is not None:
-            # two GEMMs chained through the epilogue: (b + x W_self) + aggr W_neigh
-            out = torch.addmm(self.bias, x, self.lin_self.kernel) if use_b else torch.matmul(x, self.lin_self.kernel)
-            out = torch.addmm(out, aggregated, self.lin_neigh.kernel)
+            # ONE kgx_dense pass: relu?(b + x W_self + aggr W_neigh), reading x and aggr once
+            out = kops.dense(x, self.lin_self.kernel, self.bias if use_b else None,
+                             x1=aggregated, W1=self.lin_neigh.kernel, relu=relu)
         else:
-            out = self.lin_neigh(aggregated)
-            if use_b:
-                out = out + self.bias
-        if self.activation is torch.relu:
-            out = torch.relu_(out)
-        elif self.activation is not None:
+            out = kops.dense(aggregated, self.lin_neigh.kernel, self.bias if use_b else None, relu=relu)
+        if self.activation is not None and not relu:
             out = self.activation(out)
         if self.normalize:
             out = l2_normalize(out)

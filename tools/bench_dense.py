@@ -40,9 +40,13 @@ def timeit(fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--only", default="", help="comma-separated substrings of shape names to run")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
+    only = [o for o in args.only.split(",") if o]
     for name, (M, K0, K1, N, relu) in SHAPES.items():
+        if only and not any(o in name for o in only):
+            continue
         x0 = torch.randn(M, K0, device=dev)
         W0 = torch.randn(K0, N, device=dev) * 0.05
         x1 = torch.randn(M, K1, device=dev) if K1 else None
