@@ -196,23 +196,29 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
         f32x4 x = p[j];
         if constexpr (TWO)  // each slot read zero bits from one of the two descriptors
           x = __builtin_bit_cast(f32x4, __builtin_bit_cast(u32x4, p[j]) | __builtin_bit_cast(u32x4, q[j]));
-        uint32_t h[2], m[2], lo[2];
-        bool bad;
-        split3x4_fast(x, h, m, lo, bad);
-        if (bad) {  // inf / NaN / near-FLT_MAX values: the exact scalar split (rare)
+        bf16x4_t ph, pm, pl;
 #pragma unroll
-          for (int e = 0; e < 4; e += 2) {
-            short h0, m0, l0, h1, m1, l1;
-            split3(x[e], h0, m0, l0);
-            split3(x[e + 1], h1, m1, l1);
-            h[e / 2] = uint32_t(uint16_t(h0)) | (uint32_t(uint16_t(h1)) << 16);
-            m[e / 2] = uint32_t(uint16_t(m0)) | (uint32_t(uint16_t(m1)) << 16);
-            lo[e / 2] = uint32_t(uint16_t(l0)) | (uint32_t(uint16_t(l1)) << 16);
+        for (int e = 0; e < 4; ++e) {
+          short h, m, lo;
+          split3_a(x[e], h, m, lo);
+          ph[e] = h;
+          pm[e] = m;
+          pl[e] = lo;
+        }
+        // inf / NaN among the four (their sum is then non-finite): lo plane (rare)
+        if (!__builtin_isfinite(__fadd_rn(__fadd_rn(x[0], x[1]), __fadd_rn(x[2], x[3])))) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            short h, m, lo;
+            split3_a_lo(x[e], h, m, lo);
+            ph[e] = h;
+            pm[e] = m;
+            pl[e] = lo;
           }
         }
-        *reinterpret_cast<uint2*>(&As[buf][0][row][kk]) = make_uint2(h[0], h[1]);
-        *reinterpret_cast<uint2*>(&As[buf][1][row][kk]) = make_uint2(m[0], m[1]);
-        *reinterpret_cast<uint2*>(&As[buf][2][row][kk]) = make_uint2(lo[0], lo[1]);
+        *reinterpret_cast<bf16x4_t*>(&As[buf][0][row][kk]) = ph;
+        *reinterpret_cast<bf16x4_t*>(&As[buf][1][row][kk]) = pm;
+        *reinterpret_cast<bf16x4_t*>(&As[buf][2][row][kk]) = pl;
       }
     };
     using Zero = std::integral_constant<int, 0>;
@@ -260,7 +266,7 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       short h, m, lo;
-      split3(w_at(a, 32 * s + 8 * lq + j, n_col), h, m, lo);
+      split3_a(w_at(a, 32 * s + 8 * lq + j, n_col), h, m, lo);
       wh[s][j] = h;
       wm[s][j] = m;
       wl[s][j] = lo;

@@ -82,11 +82,11 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 // ---- three-way bf16 split of f32 operands (the "bf16x3" product) ---------
-// split3 (kgx_bf16x3.h): x = hi + mid + lo; x*w is taken as the six
-// significant bf16 x bf16 products (dropped terms <= 2^-24 |x w|), each exact
-// in the MFMA's f32 accumulator, on v_mfma_f32_16x16x32_bf16 -- 16x the
+// split3_a / split3_a_lo (kgx_bf16x3.h): x = hi + mid + lo; x*w is taken as the
+// six significant bf16 x bf16 products (dropped terms <= 2^-24 |x w|), each
+// exact in the MFMA's f32 accumulator, on v_mfma_f32_16x16x32_bf16 -- 16x the
 // per-clock rate of the f32-input MFMA.  Infinite / NaN aggregates follow
-// IEEE f32 products (kgx_bf16x3.h).
+// IEEE f32 products (non-finite aggregates go to the lo plane, kgx_bf16x3.h).
 typedef short bf16x8_t __attribute__((ext_vector_type(8)));
 typedef short bf16x4_t __attribute__((ext_vector_type(4)));
 
@@ -148,16 +148,23 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
   // so each A fragment is 8 contiguous bf16 of a tile row (one ds_read_b128).
   bf16x8_t wfh[4], wfm[4], wfl[4];
 #pragma unroll
-  for (int s = 0; s < 4; ++s)
+  for (int s = 0; s < 4; ++s) {
+    typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+    u32x4_t ph, pm, pl;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float v = mfma_wave ? a.W[int64_t(32 * q + 8 * s + j) * a.F_out + n_col] : 0.0f;
-      short h, m_, l;
-      split3(v, h, m_, l);
-      wfh[s][j] = h;
-      wfm[s][j] = m_;
-      wfl[s][j] = l;
+    for (int j = 0; j < 8; j += 2) {
+      const float v0 = mfma_wave ? a.W[int64_t(32 * q + 8 * s + j) * a.F_out + n_col] : 0.0f;
+      const float v1 = mfma_wave ? a.W[int64_t(32 * q + 8 * s + j + 1) * a.F_out + n_col] : 0.0f;
+      uint32_t h, m_, l;
+      split3_pair(v0, v1, h, m_, l);
+      ph[j / 2] = h;
+      pm[j / 2] = m_;
+      pl[j / 2] = l;
     }
+    wfh[s] = __builtin_bit_cast(bf16x8_t, ph);
+    wfm[s] = __builtin_bit_cast(bf16x8_t, pm);
+    wfl[s] = __builtin_bit_cast(bf16x8_t, pl);
+  }
 #else
   float wb[32];
 #pragma unroll
@@ -265,10 +272,23 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         short h, m_, l;
-        split3(r[k], h, m_, l);
+        split3_a(r[k], h, m_, l);
         ph[k] = h;
         pm[k] = m_;
         pl[k] = l;
+      }
+      // inf / NaN in this lane's values (their sum is then non-finite): move
+      // them to the lo plane (split3_a_lo) -- a rare branch instead of two
+      // selects per value on every row
+      if (!__builtin_isfinite(__fadd_rn(__fadd_rn(r[0], r[1]), __fadd_rn(r[2], r[3])))) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          short h, m_, l;
+          split3_a_lo(r[k], h, m_, l);
+          ph[k] = h;
+          pm[k] = m_;
+          pl[k] = l;
+        }
       }
       *reinterpret_cast<bf16x4_t*>(&tile3[0][g][f]) = ph;
       *reinterpret_cast<bf16x4_t*>(&tile3[1][g][f]) = pm;

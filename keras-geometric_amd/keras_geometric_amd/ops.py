@@ -787,10 +787,10 @@ def _dense_fake(x0, W0, x1, W1, bias, relu):
 
 
 def _matmul_t(g: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
-    """g @ W^T on kgx_dense when the transposed shape fits, else the library GEMM."""
-    Wt = W.t().contiguous()
-    if dense_supported(g, Wt):
-        return torch.ops.kgx.dense(g, Wt, None, None, None, False)
+    """g @ W^T for the backward: the library fp32 GEMM, so gradients keep the
+    reference autograd's fp32 GEMM numerics (kgx_dense is f32-accurate too,
+    but its re-associated sums moved GIN's d/dx past the 1e-5 gradient bar
+    on the toy graph of tests/test_gpu_backward.py)."""
     return g @ W.t()
 
 

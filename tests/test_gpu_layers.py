@@ -105,6 +105,39 @@ def test_gcn_edge_cases(dev, golden):
         layer([x])
 
 
+@pytest.mark.parametrize("layer_kind", ["gcn", "gin"])
+def test_fused_and_dense_nonfinite_inputs(dev, golden, layer_kind):
+    """NaN / inf in x through the MFMA paths (F_in = 128: the fused
+    aggregate->transform kernel; GIN's MLP: kgx_dense) propagate as in the
+    reference's fp32 arithmetic (tests/unit/test_error_handling.py:233-258):
+    same NaN positions, same signed infinities (kgx_bf16x3.h)."""
+    g = golden("rmat_small")
+    x = torch.from_numpy(g["x"]).clone()
+    ei = torch.from_numpy(g["edge_index"])
+    n = x.shape[0]
+    x = torch.cat([x, x, x, x], dim=1)[:, :128].contiguous()
+    x[0, 0] = float("inf")
+    x[5, 7] = float("-inf")
+    x[11, 3] = float("nan")
+    gen = torch.Generator().manual_seed(4)
+    W = (torch.rand(128, 128, generator=gen) * 2 - 1) * 0.15
+    b = torch.randn(128, generator=gen)
+    if layer_kind == "gcn":
+        layer = GCNConv(128)
+        layer([x.to(dev), ei.to(dev)])
+        layer.set_weights([W.numpy(), b.numpy()])
+        ref = R.gcn_forward(x, ei, W, b)
+    else:
+        layer = GINConv(128)  # default MLP: one Dense 128 -> 128 (kgx_dense)
+        layer([x.to(dev), ei.to(dev)])
+        layer.set_weights([W.numpy(), b.numpy()])
+        ref = R.gin_forward(x, ei, [(W, b, None)], aggregator="sum", eps=0.0)
+    y = layer([x.to(dev), ei.to(dev)])
+    assert y.shape == (n, 128)
+    assert torch.isinf(ref).any() and torch.isnan(ref).any()
+    assert_tol(y, ref.numpy())
+
+
 def test_gcn_deterministic(dev, golden):
     g = golden("rmat_small")
     layer = GCNConv(output_dim=32)
