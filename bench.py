@@ -184,7 +184,8 @@ def main() -> None:
             with torch.no_grad():
                 return layer(x)
 
-        shard_info = {"halo_rows_per_rank": sg.n_halo, "halo_MB_per_layer": sg.n_halo * f_in * 4 / 1e6}
+        shard_info = {"halo_rows_per_rank": sg.n_halo, "halo_MB_per_layer": sg.n_halo * f_in * 4 / 1e6,
+                      "halo_chunks": len(sg.chunks)}
 
     for _ in range(args.warmup):
         step()
@@ -224,9 +225,9 @@ def main() -> None:
     from keras_geometric_amd import ops as _ops
 
     fused = not args.exact and _ops.fused_transform_supported(f_in, f_out)
+    # SURVEY.md §8d per rank; at N>1 the accumulating halo-chunk passes' re-reads
+    # of the rows they add to are implementation overhead, not algorithmic bytes
     balg = b_alg_spmm(n_rows, e_agg, f_in if fused else f_out, weighted=True, f_out=f_out)
-    if world > 1 and fused:  # second (halo-source) launch: its rowptr + read-back of out
-        balg += 4 * (n_rows + 1) + 4 * n_rows * f_out
     achieved = balg / (kern_ms * 1e-3) / 1e9
     traffic, traffic_src = (None, None)
     if world == 1:

@@ -10,12 +10,14 @@ Sources owned by other ranks ("halo" rows) are fetched once per layer with a
 single all-to-all-v over RCCL (torch.distributed "nccl" = RCCL on ROCm, over
 xGMI): the send lists are planned once per graph.
 
-GCN layer, default mode (aggregate-then-transform, exchange overlapped):
-    side stream:  send = gather(x_local, send_rows); RCCL all-to-all -> halo
+GCN layer, default mode (aggregate-then-transform, exchange pipelined in K
+chunks; chunk k = the k-th slice of every owner's requested rows):
+    side stream:  per chunk k: send_k = gather(x_local, send_rows_k);
+                  RCCL all-to-all -> halo[k]
     main stream:  out  = bias + (A_own x_local) W        fused kgx kernel
-                  wait for the halo
-                  out += (A_halo halo) W                  same kernel, accumulate
-  (each row's sum is split own-sources-then-halo: tolerance-equal to one GPU)
+                  per chunk k: wait for halo[k];
+                  out += (A_k halo[k]) W                  same kernel, accumulate
+  (each row's sum is split own-sources-then-chunks: tolerance-equal to one GPU)
 EXACT mode (and the generic propagate):
     table[:n_local] = x_local (@ W);  table[n_local:] = halo all-to-all
     out = kgx aggregation over the shard CSR in global input order
@@ -28,6 +30,8 @@ exchange logic under gloo (tests/test_distributed_gloo.py).
 
 from __future__ import annotations
 
+import contextlib
+import os
 from dataclasses import dataclass
 
 import torch
@@ -63,8 +67,10 @@ class KgxBackend:
     def gather_rows(self, table: torch.Tensor, rows: torch.Tensor) -> torch.Tensor:
         return kops.gather_rows(table, rows)
 
-    def split_by_source(self, g, n_own: int):
-        return G.split_by_source(g, n_own)
+    def split_by_source(self, g, cuts: list):
+        """Parts of g by source range [cuts[k], cuts[k+1]); every part after the
+        first is accumulate-only (graph.split_by_source_ranges)."""
+        return G.split_by_source_ranges(g, cuts, accumulate_from=1)
 
     def supports_fused(self, f_in: int, f_out: int) -> bool:
         return kops.fused_transform_supported(f_in, f_out)
@@ -133,6 +139,64 @@ def equal_bounds(n_global: int, world: int) -> list[int]:
     return b
 
 
+def default_halo_chunks(world: int) -> int:
+    """Exchange steps per layer (KGX_HALO_CHUNKS overrides; every rank must use
+    the same count).  The halo volume is a property of the graph (DESIGN.md
+    §6: ~6 GB per rank per layer at 8 weak-scaled shards), so a single
+    all-to-all leaves the halo pass waiting for all of it; in chunks, pass k
+    runs while chunk k+1 is on the links, for about one extra read-modify-write
+    of the rows each pass touches."""
+    v = os.environ.get("KGX_HALO_CHUNKS")
+    if v:
+        return max(1, int(v))
+    return 4 if world > 1 else 1
+
+
+@dataclass
+class HaloChunk:
+    """One exchange step.  Every rank sends each peer the k-th slice of the
+    rows that peer requested from it and receives the k-th slice of each of its
+    own requests, into the contiguous halo-table rows [lo, hi) (the halo table
+    is chunk-major, then grouped by owner)."""
+    lo: int
+    hi: int
+    recv_splits: list
+    send_splits: list
+    send_rows: torch.Tensor  # int32 local rows to send, grouped by destination rank
+
+
+def _plan_chunks(requested_local: torch.Tensor, send_counts: list, recv_counts: list, n_chunks: int,
+                 dev) -> tuple[list, torch.Tensor]:
+    """(chunks, pos): pos[i] = halo-table row of the i-th sorted halo id.  The
+    slice bounds floor(count*k/K) are computed identically by the requester and
+    the owner from the same count, so both sides agree on every chunk."""
+    K = max(1, n_chunks)
+    rstart = [0]
+    for c in recv_counts:
+        rstart.append(rstart[-1] + c)
+    sstart = [0]
+    for c in send_counts:
+        sstart.append(sstart[-1] + c)
+    pos = torch.empty(rstart[-1], dtype=torch.long, device=dev)
+    chunks, off = [], 0
+    for k in range(K):
+        recv_splits, send_splits, send_parts = [], [], []
+        lo = off
+        for p, R in enumerate(recv_counts):
+            a, b = rstart[p] + R * k // K, rstart[p] + R * (k + 1) // K
+            pos[a:b] = torch.arange(off, off + b - a, device=dev)
+            off += b - a
+            recv_splits.append(b - a)
+        for p, S in enumerate(send_counts):
+            a, b = sstart[p] + S * k // K, sstart[p] + S * (k + 1) // K
+            send_parts.append(requested_local[a:b])
+            send_splits.append(b - a)
+        rows = torch.cat(send_parts) if send_parts else requested_local[:0]
+        chunks.append(HaloChunk(lo=lo, hi=off, recv_splits=recv_splits, send_splits=send_splits,
+                                send_rows=rows.to(torch.int32).contiguous()))
+    return chunks, pos
+
+
 @dataclass
 class ShardedGraph:
     rank: int
@@ -140,15 +204,15 @@ class ShardedGraph:
     n_global: int
     bounds: list[int]
     graph: object  # CSRGraph over local rows; sources index [own rows | halo rows]
-    send_rows: torch.Tensor  # int32, local row ids to send, grouped by destination rank
-    send_counts: list[int]
-    recv_counts: list[int]
-    halo_ids: torch.Tensor  # global ids of halo rows in table order
+    send_counts: list[int]  # rows this rank sends to each rank per layer
+    recv_counts: list[int]  # halo rows this rank receives from each rank per layer
+    halo_ids: torch.Tensor  # global ids of halo rows in table order (chunk-major)
+    chunks: list  # one HaloChunk per exchange step
     dinv_table: torch.Tensor | None
     backend: object
     comm: object = None
     exact: bool = False
-    _parts: tuple | None = None  # (own-source CSR, halo-source CSR), built on first use
+    _parts: tuple | None = None  # (own-source CSR, [halo-chunk CSRs]), built on first use
     _side: object = None  # HIP stream for the halo exchange
     _halo_buf: dict | None = None
 
@@ -168,12 +232,14 @@ class ShardedGraph:
     @classmethod
     def build(cls, src: torch.Tensor, dst: torch.Tensor, bounds: list[int], *, comm=None,
               self_loops: bool = True, gcn_norm: bool = True, backend=None, n_features: int = 128,
-              exact: bool = False) -> "ShardedGraph":
+              exact: bool = False, halo_chunks: int | None = None) -> "ShardedGraph":
         """src/dst: this rank's edges (global ids, int32) whose dst lies in its range,
-        in global input order."""
+        in global input order.  halo_chunks: exchange steps per layer (the same
+        on every rank; default `default_halo_chunks`)."""
         backend = backend or KgxBackend()
         comm = comm or TorchComm()
         rank, world = comm.rank(), comm.world()
+        n_chunks = default_halo_chunks(world) if halo_chunks is None else max(1, int(halo_chunks))
         lo, hi = bounds[rank], bounds[rank + 1]
         n_local = hi - lo
         dev = src.device
@@ -194,8 +260,14 @@ class ShardedGraph:
         send_counts = [int(v) for v in send_counts_t.cpu()]
         requested = torch.empty(sum(send_counts), dtype=torch.long, device=dev)
         comm.all_to_all_single(requested, halo_ids, send_counts, recv_counts)
-        send_rows = (requested - lo).to(torch.int32)
-        col = torch.where(local, src - lo, n_local + torch.searchsorted(halo_ids, src))
+        chunks, pos = _plan_chunks(requested - lo, send_counts, recv_counts, n_chunks, dev)
+        if pos.numel():
+            hidx = torch.searchsorted(halo_ids, src).clamp_(max=pos.numel() - 1)
+            col = torch.where(local, src - lo, n_local + pos[hidx])
+        else:
+            col = src - lo
+        halo_table_ids = torch.empty_like(halo_ids)
+        halo_table_ids[pos] = halo_ids
         row = dst - lo
         if self_loops:  # utils/main.py:8-16 — loop i after all input edges
             ar = torch.arange(n_local, device=dev)
@@ -204,9 +276,9 @@ class ShardedGraph:
         n_src = n_local + int(halo_ids.numel())
         g = backend.build_graph(col.to(torch.int32).contiguous(), row.to(torch.int32).contiguous(), n_src, n_local,
                                 n_features)
-        sg = cls(rank=rank, world=world, n_global=bounds[-1], bounds=list(bounds), graph=g, send_rows=send_rows,
-                 send_counts=send_counts, recv_counts=recv_counts, halo_ids=halo_ids.to(torch.int32),
-                 dinv_table=None, backend=backend, comm=comm, exact=exact)
+        sg = cls(rank=rank, world=world, n_global=bounds[-1], bounds=list(bounds), graph=g,
+                 send_counts=send_counts, recv_counts=recv_counts, halo_ids=halo_table_ids.to(torch.int32),
+                 chunks=chunks, dinv_table=None, backend=backend, comm=comm, exact=exact)
         if gcn_norm:
             dinv_local = backend.dinv(g.deg)
             table = torch.empty((n_src, 1), dtype=torch.float32, device=dev)
@@ -233,17 +305,27 @@ class ShardedGraph:
     def new_table(self, features: int, like: torch.Tensor) -> torch.Tensor:
         return torch.empty((self.n_local + self.n_halo, features), dtype=torch.float32, device=like.device)
 
+    def _pack(self, x_local: torch.Tensor, c: HaloChunk) -> torch.Tensor:
+        if c.send_rows.numel():
+            return self.backend.gather_rows(x_local, c.send_rows)
+        return x_local.new_empty((0, x_local.shape[1]))
+
     def halo_exchange(self, table: torch.Tensor) -> None:
-        """table[n_local:] <- rows other ranks own (one all-to-all-v over RCCL)."""
-        send = self.backend.gather_rows(table[: self.n_local], self.send_rows) if self.send_rows.numel() else \
-            table.new_empty((0, table.shape[1]))
-        self.comm.all_to_all_single(table[self.n_local:], send, self.recv_counts, self.send_counts)
+        """table[n_local:] <- rows other ranks own (one all-to-all-v over RCCL
+        per chunk, each landing in its contiguous slice of the halo rows)."""
+        own, halo = table[: self.n_local], table[self.n_local:]
+        for c in self.chunks:
+            self.comm.all_to_all_single(halo[c.lo: c.hi], self._pack(own, c), c.recv_splits, c.send_splits)
 
     def own_halo_parts(self):
-        """The shard CSR split into own-source and halo-source parts (CSR order
-        kept inside each), halo sources indexed from 0 within the halo rows."""
+        """(own-source CSR, [one CSR per halo chunk]): the shard CSR split by
+        source range, CSR order kept inside each part; a chunk part's sources
+        index that chunk's halo rows from 0 and its schedule skips the rows the
+        chunk does not touch (accumulate-only)."""
         if self._parts is None:
-            self._parts = self.backend.split_by_source(self.graph, self.n_local)
+            cuts = [0, self.n_local] + [self.n_local + c.hi for c in self.chunks]
+            parts = self.backend.split_by_source(self.graph, cuts)
+            self._parts = (parts[0], list(parts[1:]))
         return self._parts
 
     def halo_buffer(self, features: int, like: torch.Tensor) -> torch.Tensor:
@@ -257,17 +339,22 @@ class ShardedGraph:
             self._halo_buf[key] = buf
         return buf
 
-    def start_halo_exchange(self, x_local: torch.Tensor, halo: torch.Tensor):
-        """Pack the rows other ranks need and start the all-to-all into `halo`
-        on a side stream; returns a handle with wait() (or None if done)."""
+    def start_halo_exchange(self, x_local: torch.Tensor, halo: torch.Tensor) -> list:
+        """Per chunk: pack the rows other ranks need and start the all-to-all
+        into halo[chunk] on a side stream.  Returns one handle per chunk whose
+        wait() orders the then-current stream after that chunk's rows (None:
+        the comm ran synchronously and the rows are already ordered)."""
         def run():
-            send = self.backend.gather_rows(x_local, self.send_rows) if self.send_rows.numel() else \
-                x_local.new_empty((0, x_local.shape[1]))
             start = getattr(self.comm, "all_to_all_start", None)
-            if start is None:
-                self.comm.all_to_all_single(halo, send, self.recv_counts, self.send_counts)
-                return None
-            return start(halo, send, self.recv_counts, self.send_counts)
+            works = []
+            for c in self.chunks:
+                send = self._pack(x_local, c)
+                if start is None:
+                    self.comm.all_to_all_single(halo[c.lo: c.hi], send, c.recv_splits, c.send_splits)
+                    works.append(None)
+                else:
+                    works.append(start(halo[c.lo: c.hi], send, c.recv_splits, c.send_splits))
+            return works
 
         if not x_local.is_cuda:
             return run()
@@ -276,10 +363,10 @@ class ShardedGraph:
         cur = torch.cuda.current_stream(x_local.device)
         self._side.wait_stream(cur)
         with torch.cuda.stream(self._side):
-            work = run()
-        if work is None:  # synchronous comm: order the halo rows before later work
+            works = run()
+        if any(w is None for w in works):  # synchronous comm: order the halo rows before later work
             cur.wait_stream(self._side)
-        return work
+        return works
 
     def propagate(self, x_local: torch.Tensor, reduce: str = "sum", **kw) -> torch.Tensor:
         """Sharded MessagePassing.propagate with the default message x_j."""
@@ -330,25 +417,33 @@ class ShardedGCNConv(Layer):
                                     bias=self.bias if use_b else None, exact=sg.exact)
 
     def _forward_overlapped(self, x_local: torch.Tensor, bias) -> torch.Tensor:
-        """Aggregate-then-transform with the halo exchange overlapped:
-        side stream: pack send rows of X -> RCCL all-to-all into the halo buffer;
-        main stream: out = bias + (A_own X_own) W   (fused kernel, own sources);
-        then, once the halo has landed: out += (A_halo X_halo) W   (same kernel,
-        accumulate mode).  Each row's sum is split own-then-halo, a
-        re-association of the one-pass order (tolerance-equal; EXACT mode keeps
-        the one-pass order and waits for the halo)."""
+        """Aggregate-then-transform with the halo exchange pipelined in chunks:
+        side stream, per chunk k: pack its send rows of X -> RCCL all-to-all
+        into halo[k];
+        main stream: out = bias + (A_own X_own) W   (fused kernel, own sources),
+        then per chunk k, once its rows have landed: out += (A_k X_halo[k]) W
+        (same kernel, accumulate mode, only the rows chunk k touches) -- so
+        pass k runs while chunk k+1 is on the links.  Each row's sum is split
+        own-then-chunks, a re-association of the one-pass order
+        (tolerance-equal; EXACT mode keeps the one-pass order and waits for the
+        whole halo)."""
         sg = self.sg
-        g_own, g_halo = sg.own_halo_parts()
+        g_own, g_chunks = sg.own_halo_parts()
         x_local = x_local.contiguous()
         halo = sg.halo_buffer(x_local.shape[1], x_local)
         with torch.no_grad():
-            work = sg.start_halo_exchange(x_local, halo)
+            works = sg.start_halo_exchange(x_local, halo)
             with kops.sharing_gpu():  # the exchange's RCCL kernels run beside this pass
                 out = sg.backend.aggregate_transform(g_own, x_local, self.kernel, bias=bias)
-            if work is not None:
-                work.wait()
-            if g_halo.kept:
-                sg.backend.aggregate_transform(g_halo, halo, self.kernel, out=out)
+            last = max((k for k, g in enumerate(g_chunks) if g.kept), default=-1)
+            for k, (c, g) in enumerate(zip(sg.chunks, g_chunks)):
+                if works[k] is not None:
+                    works[k].wait()
+                if not g.kept:
+                    continue
+                # leave block slots to the chunks still in flight; the last pass takes the whole GPU
+                with kops.sharing_gpu() if k < last else contextlib.nullcontext():
+                    sg.backend.aggregate_transform(g, halo[c.lo: c.hi], self.kernel, out=out)
         return out
 
 

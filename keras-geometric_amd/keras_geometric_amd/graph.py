@@ -217,10 +217,30 @@ def split_by_source(g: CSRGraph, n_own: int) -> tuple[CSRGraph, CSRGraph]:
     on a row's own-source part while its halo rows are still in flight
     (distributed.py); sum(own) + sum(other) re-associates the row's sum, so the
     split path is tolerance-equal, not bit-equal, to the one-pass row."""
+    own, other = split_by_source_ranges(g, [0, n_own, g.n_src], accumulate_from=2)
+    return own, other
+
+
+def split_by_source_ranges(g: CSRGraph, cuts: list[int], accumulate_from: int = 1) -> list[CSRGraph]:
+    """Split every CSR row by source range: part k holds the row's edges with
+    cuts[k] <= col < cuts[k+1] (CSR order kept, sources re-based to cuts[k],
+    edge weights sliced along).  The sharded GCN layer runs part 0 (own
+    sources) while the halo rows are in flight and then one accumulating pass
+    per arrived halo chunk (distributed.py).
+
+    Parts k >= accumulate_from are meant for accumulate-mode launches
+    (out += part): their schedules drop the items of rows with no edges in the
+    part (a degree-sorted suffix), so such a pass neither reads nor rewrites
+    rows it contributes nothing to -- and adds no 0 * W term, which would turn
+    -0 into +0 or an inf/NaN weight into NaN where the one-pass row has none."""
+    if len(cuts) < 2 or cuts[0] != 0 or cuts[-1] != g.n_src or any(a > b for a, b in zip(cuts, cuts[1:])):
+        raise ValueError(f"split_by_source_ranges: cuts must rise from 0 to n_src={g.n_src} (got {cuts})")
     row_of = row_of_slot(g)
-    own = g.col < n_own
+    part_of = torch.bucketize(g.col, torch.tensor(cuts[1:-1], dtype=torch.int32, device=g.device), right=True)
     parts = []
-    for m, base, n_src in ((own, 0, n_own), (~own, n_own, g.n_src - n_own)):
+    for k in range(len(cuts) - 1):
+        m = part_of == k
+        base, n_src = cuts[k], cuts[k + 1] - cuts[k]
         deg = torch.bincount(row_of[m], minlength=g.n_dst).to(torch.int32)[: g.n_dst]
         rowptr = torch.zeros(g.n_dst + 1, dtype=torch.int32, device=g.device)
         rowptr[1:] = torch.cumsum(deg, 0)
@@ -233,8 +253,13 @@ def split_by_source(g: CSRGraph, n_own: int) -> tuple[CSRGraph, CSRGraph]:
             dinv=g.dinv, w=g.w[m].contiguous() if g.w is not None else None,
         )
         _build_schedule(sub, default_split_len(kept))
+        if k >= accumulate_from and sub.n_items:
+            empty = int((deg == 0).sum())  # one item each, last in the degree-descending schedule
+            sub.n_items -= empty
+            sub.items = sub.items[: sub.n_items]
+            sub.extras["accumulate_only"] = True
         parts.append(sub)
-    return parts[0], parts[1]
+    return parts
 
 
 # ---------------------------------------------------------------------------

@@ -43,17 +43,18 @@ class OracleBackend:
     def gather_rows(self, table, rows):
         return table[rows.long()]
 
-    def split_by_source(self, g, n_own):
+    def split_by_source(self, g, cuts):
         rows = torch.repeat_interleave(torch.arange(g.n_dst), g.deg.long())
-        own = g.col.long() < n_own
+        col = g.col.long()
         parts = []
-        for m, base in ((own, 0), (~own, n_own)):
+        for lo, hi in zip(cuts, cuts[1:]):
+            m = (col >= lo) & (col < hi)
             deg = torch.bincount(rows[m], minlength=g.n_dst).int()
             rowptr = torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(deg.long(), 0)]).int()
-            parts.append(SimpleNamespace(rowptr=rowptr, col=(g.col[m].long() - base).int(), eid=g.eid[m], deg=deg,
+            parts.append(SimpleNamespace(rowptr=rowptr, col=(col[m] - lo).int(), eid=g.eid[m], deg=deg,
                                          n_dst=g.n_dst, kept=int(m.sum()), dinv=None, w=g.w[m],
                                          device=torch.device("cpu")))
-        return parts[0], parts[1]
+        return parts
 
     def supports_fused(self, f_in, f_out):
         return True
@@ -115,7 +116,7 @@ def _full_graph_reference(world_size=1):
         be.aggregate(g, torch.from_numpy(x), "max")
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, chunks, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -124,7 +125,8 @@ def _worker(rank, world, port, q):
         lo, hi = bounds[rank], bounds[rank + 1]
         keep = (d >= lo) & (d < hi)  # stable: global input order kept
         sg = kd.ShardedGraph.build(torch.from_numpy(s[keep]), torch.from_numpy(d[keep]), bounds,
-                                   backend=OracleBackend(), n_features=F_OUT)
+                                   backend=OracleBackend(), n_features=F_OUT, halo_chunks=chunks)
+        assert len(sg.chunks) == chunks and sg.chunks[-1].hi == sg.n_halo
         h = torch.from_numpy(x[lo:hi]) @ torch.from_numpy(W)
         table = sg.new_table(F_OUT, h)
         table[: sg.n_local] = h
@@ -146,14 +148,18 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(180)
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_equals_unsharded_bitwise(world):
+@pytest.mark.parametrize("world,chunks", [(2, 1), (2, 4), (3, 3)])
+def test_sharded_equals_unsharded_bitwise(world, chunks):
+    """EXACT table path bit-identical to the unsharded graph for any halo
+    chunking (the chunk-major halo table only renames source rows), and the
+    chunk-pipelined GCN layer (own part, then one accumulating part per chunk)
+    within the north-star tolerance."""
     if torch.cuda.is_initialized():
         pytest.skip("never start processes from a process that has initialised the GPU")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, chunks, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     results = {}

@@ -364,3 +364,39 @@ def test_fused_accumulate_own_halo_split(dev, split_len):
     assert_dot_bound(one, aggr, W.astype(np.float64), b.astype(np.float64), k_eps=2e-5)
     with pytest.raises(ValueError):
         kops.aggregate_transform(g_oth, xd[n_own:].contiguous(), Wd, "max", out=out)
+
+
+def test_split_by_source_ranges_accumulate_parts(dev):
+    """The sharded layer's chunk pipeline in miniature: source-range parts
+    (own part with bias, then three accumulate-only parts) equal the one-pass
+    row within the dot-product bound; accumulate-only parts schedule only the
+    rows they touch, so a row no later part touches keeps its first-pass bits."""
+    N, E, F, F_out = 3000, 40000, 128, 64
+    s, d = rmat_edges(11, scale_for(N), N, 0, E)
+    rng = np.random.default_rng(4)
+    x = rng.standard_normal((N, F)).astype(np.float32)
+    W = (rng.standard_normal((F, F_out)) * 0.1).astype(np.float32)
+    b = rng.standard_normal(F_out).astype(np.float32)
+    csr = build(np.stack([s, d]), N, dev, self_loops=True, gcn_norm=True)
+    xd, Wd, bd = T(x).to(dev), T(W).to(dev), T(b).to(dev)
+    cuts = [0, N // 3, N // 2, 2 * N // 3, N]
+    parts = G.split_by_source_ranges(csr, cuts)
+    assert sum(p.kept for p in parts) == csr.kept
+    torch.testing.assert_close(sum(p.deg for p in parts), csr.deg, rtol=0, atol=0)
+    for p in parts[1:]:
+        it = p.items.cpu()
+        assert p.n_items == it.shape[0] and bool((it[:, 2] > it[:, 1]).all())
+        assert int((it[:, 2] - it[:, 1]).sum()) == p.kept  # every edge of the part covered once
+    out = kops.aggregate_transform(parts[0], xd[: cuts[1]].contiguous(), Wd, "sum", weighted=True, bias=bd)
+    first = out.clone()
+    for k in range(1, len(parts)):
+        kops.aggregate_transform(parts[k], xd[cuts[k]: cuts[k + 1]].contiguous(), Wd, "sum", weighted=True, out=out)
+    untouched = (sum(p.deg for p in parts[1:]) == 0).cpu().numpy()
+    assert untouched.any() and not untouched.all()
+    np.testing.assert_array_equal(out.cpu().numpy()[untouched], first.cpu().numpy()[untouched])
+    rows = np.repeat(np.arange(N), csr.deg.cpu().numpy())
+    aggr = np.zeros((N, F))
+    np.add.at(aggr, rows, x[csr.col.cpu().numpy()].astype(np.float64) * csr.w.cpu().numpy()[:, None])
+    assert_dot_bound(out.cpu().numpy(), aggr, W.astype(np.float64), b.astype(np.float64), k_eps=2e-5)
+    with pytest.raises(ValueError):
+        G.split_by_source_ranges(csr, [0, N // 2])  # must end at n_src

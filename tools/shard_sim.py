@@ -1,0 +1,106 @@
+"""One rank's device work of the weak-scaled sharded GCN layer, on one GPU.
+
+  python tools/shard_sim.py [--world 8] [--chunks 1,2,4,8] [--steps 10]
+
+Builds rank 0's shard of the P x 10M-node / P x 100M-edge R-MAT graph as
+bench.py --gpus P does, but with a loopback comm: the peers' requests are
+synthetic (random rows of this rank's range, as many as this rank requests
+from them) and the all-to-all is a device copy.  So the timed step is the
+rank's compute side of ShardedGCNConv -- send-row packing, the own-source
+pass and one accumulating pass per halo chunk -- with the exchange itself
+free.  It prices the chunked pipeline's extra passes against one halo pass
+(DESIGN.md §6); the link time has to be added from the halo bytes.
+A measurement helper, not part of the product.
+"""
+
+import argparse
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "keras-geometric_amd")]
+
+import torch  # noqa: E402
+
+from keras_geometric_amd import distributed as kd  # noqa: E402
+from keras_geometric_amd import ops as kops  # noqa: E402
+
+
+class LoopbackComm(kd.TorchComm):
+    """Rank 0 of a `world`-rank job whose peers mirror it (measurement stand-in)."""
+
+    def __init__(self, world: int, n_local: int):
+        self.w, self.n_local = world, n_local
+        self.gen = torch.Generator(device="cuda").manual_seed(7)
+
+    def rank(self):
+        return 0
+
+    def world(self):
+        return self.w
+
+    def all_to_all_single(self, out, inp, out_splits=None, in_splits=None):
+        if out.dtype == torch.int64 and out_splits is None:  # the count exchange: symmetric peers
+            out.copy_(inp)
+        elif out.dtype == torch.int64:  # peers' requests: random rows of this rank's range
+            out.copy_(torch.randint(0, self.n_local, out.shape, device=out.device, generator=self.gen))
+        elif out.numel():
+            out.copy_(inp.view_as(out))
+
+    def all_to_all_start(self, out, inp, out_splits=None, in_splits=None):
+        self.all_to_all_single(out, inp, out_splits, in_splits)
+        return None
+
+    def broadcast(self, t, src=0):
+        pass
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--chunks", default="1,2,4,8")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--nodes", type=int, default=10_000_000)
+    ap.add_argument("--edges", type=int, default=100_000_000)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    P = args.world
+    for K in [int(v) for v in args.chunks.split(",")]:
+        n_local = kd.equal_bounds(args.nodes * P, P)[1]
+        comm = LoopbackComm(P, n_local)
+        sg = kd.ShardedGraph.rmat(args.nodes * P, args.edges * P, seed=0, device=dev, comm=comm,
+                                  self_loops=True, gcn_norm=True, halo_chunks=K)
+        x = torch.randn(sg.n_local, 128, device=dev)
+        layer = kd.ShardedGCNConv(128, sg)
+        with torch.no_grad():
+            layer(x)
+            g_own, g_chunks = sg.own_halo_parts()
+            for _ in range(2):
+                layer(x)
+            torch.cuda.synchronize()
+            kops.EVENT_SINK = []
+            t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0.record()
+            for _ in range(args.steps):
+                layer(x)
+            t1.record()
+            torch.cuda.synchronize()
+        ev = kops.EVENT_SINK
+        kops.EVENT_SINK = None
+        per = len(ev) // args.steps
+        launch_ms = [sum(ev[i * per + j][0].elapsed_time(ev[i * per + j][1]) for i in range(args.steps)) / args.steps
+                     for j in range(per)]
+        print(json.dumps({
+            "world": P, "chunks": K, "step_ms": round(t0.elapsed_time(t1) / args.steps, 3),
+            "launch_ms": [round(v, 3) for v in launch_ms],
+            "own_edges": g_own.kept, "chunk_edges": [g.kept for g in g_chunks],
+            "halo_rows": sg.n_halo, "chunk_items": [g.n_items for g in g_chunks],
+            "send_rows": sum(sg.send_counts), "n_local": sg.n_local,
+        }), flush=True)
+        del sg, layer, x, g_own, g_chunks
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
