@@ -184,8 +184,11 @@ def main() -> None:
             with torch.no_grad():
                 return layer(x)
 
-        shard_info = {"halo_rows_per_rank": sg.n_halo, "halo_MB_per_layer": sg.n_halo * f_in * 4 / 1e6,
-                      "halo_chunks": len(sg.chunks)}
+        pp = sg._pp  # push-pull halo plan of the default path (None: pull-only or EXACT)
+        n_moved = pp.n_rows if pp is not None else sg.n_halo
+        shard_info = {"halo_rows_pull_only_per_rank": sg.n_halo, "halo_rows_per_rank": n_moved,
+                      "halo_rows_pushed_partials": pp.n_push if pp is not None else 0,
+                      "halo_MB_per_layer": n_moved * f_in * 4 / 1e6, "halo_chunks": len(sg.chunks)}
 
     for _ in range(args.warmup):
         step()

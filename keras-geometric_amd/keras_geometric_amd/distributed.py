@@ -152,6 +152,11 @@ def default_halo_chunks(world: int) -> int:
     return 4 if world > 1 else 1
 
 
+def use_push_pull() -> bool:
+    """The default GCN path exchanges the push-pull halo (KGX_HALO_PUSH=0: pull only)."""
+    return os.environ.get("KGX_HALO_PUSH", "1") not in ("0", "", "false", "False")
+
+
 @dataclass
 class HaloChunk:
     """One exchange step.  Every rank sends each peer the k-th slice of the
@@ -163,6 +168,26 @@ class HaloChunk:
     recv_splits: list
     send_splits: list
     send_rows: torch.Tensor  # int32 local rows to send, grouped by destination rank
+    # push-pull plan: the send rows are one weighted-sum pass over this CSR
+    # (a pulled row = one edge of weight 1, a pushed partial = its edges)
+    send_graph: object = None
+
+
+@dataclass
+class PushPullPlan:
+    """Halo plan of the default GCN path (ShardedGraph.push_pull_plan)."""
+    chunks: list  # HaloChunk per exchange step, send rows packed by send_graph
+    parts: list  # receiver CSR per chunk: sources = that chunk's halo rows (accumulate-only)
+    n_rows: int  # halo rows received per layer
+    n_pull: int  # of which source rows
+    n_push: int  # of which partial sums pushed by the owners
+
+
+def _prefix(v: list) -> list:
+    out = [0]
+    for c in v:
+        out.append(out[-1] + c)
+    return out
 
 
 def _plan_chunks(requested_local: torch.Tensor, send_counts: list, recv_counts: list, n_chunks: int,
@@ -215,6 +240,7 @@ class ShardedGraph:
     _parts: tuple | None = None  # (own-source CSR, [halo-chunk CSRs]), built on first use
     _side: object = None  # HIP stream for the halo exchange
     _halo_buf: dict | None = None
+    _pp: PushPullPlan | None = None
 
     @property
     def lo(self) -> int:
@@ -306,9 +332,135 @@ class ShardedGraph:
         return torch.empty((self.n_local + self.n_halo, features), dtype=torch.float32, device=like.device)
 
     def _pack(self, x_local: torch.Tensor, c: HaloChunk) -> torch.Tensor:
+        if c.send_graph is not None:
+            return self.backend.aggregate(c.send_graph, x_local, "sum", weighted=True)
         if c.send_rows.numel():
             return self.backend.gather_rows(x_local, c.send_rows)
         return x_local.new_empty((0, x_local.shape[1]))
+
+    def push_pull_plan(self) -> PushPullPlan:
+        """A smaller halo for the weighted-sum (GCN) path.  Collective: every
+        rank calls it once (ShardedGCNConv does, on its first forward).
+
+        Pulling a source row serves all of its edges into this rank; an owner
+        pushing the partial sum sum_e w_e x_src of one destination row serves
+        all of that row's edges from the owner.  Per peer the rows moved must
+        cover every halo edge (a vertex cover of the bipartite halo graph);
+        pull-only takes every source, push-only every destination.  Here each
+        edge goes to its endpoint of larger degree in that bipartite graph
+        (ties: pull), and a destination is pushed only for edges whose source is
+        not pulled anyway.  On power-law R-MAT shards that moves ~40 % fewer
+        rows than pulling (1/10-scale probe at 8 shards: 0.72M vs 1.26M rows).
+        A pushed partial enters the receiver's CSR as one edge of weight 1; the
+        owner packs pulled rows and partials in one weighted-sum pass over a
+        send CSR (a pulled row = one edge of weight 1, multiplied exactly).
+        Row sums are re-associated (partials first), so this is a tolerance
+        path like the rest of the overlapped layer; EXACT mode keeps pulling."""
+        if self._pp is not None:
+            return self._pp
+        g, comm, world, lo, n_local = self.graph, self.comm, self.world, self.lo, self.n_local
+        dev = g.col.device
+        if g.w is None:
+            raise ValueError("push_pull_plan needs the shard graph's edge weights (gcn_norm=True)")
+        K = len(self.chunks)
+        rows = torch.repeat_interleave(torch.arange(g.n_dst, device=dev), g.deg.long())
+        col = g.col.long()
+        halo = col >= n_local
+        hs = self.halo_ids.long()[col[halo] - n_local]  # global source id per halo edge
+        hd, hw = rows[halo], g.w[halo]
+        bt = torch.tensor(self.bounds[1:-1], dtype=torch.long, device=dev)
+        us, inv_s, cs = torch.unique(hs, return_inverse=True, return_counts=True)
+        stride = n_local + 1
+        ud, inv_d, cd = torch.unique(torch.bucketize(hs, bt, right=True) * stride + hd, return_inverse=True,
+                                     return_counts=True)
+        push = cd[inv_d] > cs[inv_s]  # the edge is served from its busier endpoint
+        pulled = torch.zeros(us.numel(), dtype=torch.bool, device=dev)
+        pulled[inv_s[~push]] = True
+        via_pull = pulled[inv_s]
+        used = torch.zeros(ud.numel(), dtype=torch.bool, device=dev)
+        used[inv_d[~via_pull]] = True
+        pull_ids = us[pulled]  # sorted -> grouped by owner
+        push_keys = ud[used]  # sorted -> owner-major, then destination row
+        push_owner = push_keys // stride
+        push_row_of_key = torch.cumsum(used.long(), 0) - 1
+        pull_cnt = torch.bincount(torch.bucketize(pull_ids, bt, right=True), minlength=world)
+        push_cnt = torch.bincount(push_owner, minlength=world)
+        pe = ~via_pull  # edges served by a pushed partial, grouped by push row
+        pe_row = push_row_of_key[inv_d[pe]]
+        order = torch.argsort(pe_row, stable=True)
+        pe_row, pe_src, pe_w = pe_row[order], hs[pe][order], hw[pe][order]
+        pe_owner = push_owner[pe_row]
+        pe_cnt = torch.bincount(pe_owner, minlength=world)
+        pe_slot = pe_row - (torch.cumsum(push_cnt, 0) - push_cnt)[pe_owner]  # push row index within its owner
+        counts = torch.stack([pull_cnt, push_cnt, pe_cnt], 1).reshape(-1).contiguous()
+        counts_in = torch.empty_like(counts)
+        comm.all_to_all_single(counts_in, counts)
+        co, ci = counts.view(world, 3).cpu().tolist(), counts_in.view(world, 3).cpu().tolist()
+        r_pull, r_push, r_pe = ([c[i] for c in co] for i in range(3))
+        s_pull, s_push, s_pe = ([c[i] for c in ci] for i in range(3))
+
+        def exchange(t, dtype, s, r):
+            out = torch.empty(sum(s), dtype=dtype, device=dev)
+            comm.all_to_all_single(out, t.contiguous(), s, r)
+            return out
+
+        req_pull = exchange(pull_ids, torch.long, s_pull, r_pull) - lo
+        req_slot = exchange(pe_slot, torch.long, s_pe, r_pe)
+        req_src = exchange(pe_src, torch.long, s_pe, r_pe) - lo
+        req_w = exchange(pe_w, torch.float32, s_pe, r_pe)
+
+        # owner side: per chunk, send CSR rows = [pulled slice k | pushed slice k] per requester
+        sp, spe = _prefix(s_pull), _prefix(s_pe)
+        rp, ru = _prefix(r_pull), _prefix(r_push)
+        pull_pos = torch.empty(rp[-1], dtype=torch.long, device=dev)
+        push_pos = torch.empty(ru[-1], dtype=torch.long, device=dev)
+        chunks, off = [], 0
+        for k in range(K):
+            cols, slots, ws, send_splits, recv_splits = [], [], [], [], []
+            n_slots, lo_k = 0, off
+            for r in range(world):
+                a, b = sp[r] + s_pull[r] * k // K, sp[r] + s_pull[r] * (k + 1) // K
+                cols.append(req_pull[a:b])
+                slots.append(torch.arange(n_slots, n_slots + b - a, device=dev))
+                ws.append(torch.ones(b - a, dtype=torch.float32, device=dev))
+                n_slots += b - a
+                j0, j1 = s_push[r] * k // K, s_push[r] * (k + 1) // K
+                sl = req_slot[spe[r]: spe[r + 1]]
+                m = (sl >= j0) & (sl < j1)
+                cols.append(req_src[spe[r]: spe[r + 1]][m])
+                slots.append(n_slots + sl[m] - j0)
+                ws.append(req_w[spe[r]: spe[r + 1]][m])
+                n_slots += j1 - j0
+                send_splits.append(b - a + j1 - j0)
+            for p in range(world):  # receiver side: where chunk k's rows from p land
+                a, b = r_pull[p] * k // K, r_pull[p] * (k + 1) // K
+                pull_pos[rp[p] + a: rp[p] + b] = torch.arange(off, off + b - a, device=dev)
+                off += b - a
+                j0, j1 = r_push[p] * k // K, r_push[p] * (k + 1) // K
+                push_pos[ru[p] + j0: ru[p] + j1] = torch.arange(off, off + j1 - j0, device=dev)
+                off += j1 - j0
+                recv_splits.append(b - a + j1 - j0)
+            send_graph = None
+            if n_slots:
+                send_graph = self.backend.build_graph(torch.cat(cols).to(torch.int32), torch.cat(slots).to(torch.int32),
+                                                      n_local, n_slots, 128)
+                send_graph.w = torch.cat(ws)[send_graph.eid.long()].contiguous()
+            chunks.append(HaloChunk(lo=lo_k, hi=off, recv_splits=recv_splits, send_splits=send_splits,
+                                    send_rows=torch.empty(0, dtype=torch.int32, device=dev), send_graph=send_graph))
+        # receiver CSR over the received rows: pulled rows keep their edges and
+        # weights; a pushed partial is one edge of weight 1 into its row
+        pidx = torch.searchsorted(pull_ids, hs[via_pull])
+        rcol = torch.cat([pull_pos[pidx], push_pos])
+        rrow = torch.cat([hd[via_pull], push_keys % stride])
+        rw = torch.cat([hw[via_pull], torch.ones(push_keys.numel(), dtype=torch.float32, device=dev)])
+        parts = []
+        if off:
+            rg = self.backend.build_graph(rcol.to(torch.int32), rrow.to(torch.int32), off, n_local, 128)
+            rg.w = rw[rg.eid.long()].contiguous()
+            # a leading empty range makes every chunk part accumulate-only
+            parts = list(self.backend.split_by_source(rg, [0, 0] + [c.hi for c in chunks])[1:])
+        self._pp = PushPullPlan(chunks=chunks, parts=parts, n_rows=off, n_pull=rp[-1], n_push=ru[-1])
+        return self._pp
 
     def halo_exchange(self, table: torch.Tensor) -> None:
         """table[n_local:] <- rows other ranks own (one all-to-all-v over RCCL
@@ -328,26 +480,29 @@ class ShardedGraph:
             self._parts = (parts[0], list(parts[1:]))
         return self._parts
 
-    def halo_buffer(self, features: int, like: torch.Tensor) -> torch.Tensor:
-        """Persistent [n_halo, features] receive buffer (reused every layer call)."""
+    def halo_buffer(self, features: int, like: torch.Tensor, rows: int | None = None) -> torch.Tensor:
+        """Persistent [rows (default n_halo), features] receive buffer (reused every layer call)."""
         if self._halo_buf is None:
             self._halo_buf = {}
-        key = (features, like.device)
+        rows = self.n_halo if rows is None else rows
+        key = (features, like.device, rows)
         buf = self._halo_buf.get(key)
         if buf is None:
-            buf = torch.empty((self.n_halo, features), dtype=torch.float32, device=like.device)
+            buf = torch.empty((rows, features), dtype=torch.float32, device=like.device)
             self._halo_buf[key] = buf
         return buf
 
-    def start_halo_exchange(self, x_local: torch.Tensor, halo: torch.Tensor) -> list:
+    def start_halo_exchange(self, x_local: torch.Tensor, halo: torch.Tensor, chunks: list | None = None) -> list:
         """Per chunk: pack the rows other ranks need and start the all-to-all
         into halo[chunk] on a side stream.  Returns one handle per chunk whose
         wait() orders the then-current stream after that chunk's rows (None:
         the comm ran synchronously and the rows are already ordered)."""
+        chunks = self.chunks if chunks is None else chunks
+
         def run():
             start = getattr(self.comm, "all_to_all_start", None)
             works = []
-            for c in self.chunks:
+            for c in chunks:
                 send = self._pack(x_local, c)
                 if start is None:
                     self.comm.all_to_all_single(halo[c.lo: c.hi], send, c.recv_splits, c.send_splits)
@@ -429,14 +584,18 @@ class ShardedGCNConv(Layer):
         whole halo)."""
         sg = self.sg
         g_own, g_chunks = sg.own_halo_parts()
+        chunks, n_rows = sg.chunks, sg.n_halo
+        if use_push_pull():
+            pp = sg.push_pull_plan()
+            chunks, g_chunks, n_rows = pp.chunks, pp.parts, pp.n_rows
         x_local = x_local.contiguous()
-        halo = sg.halo_buffer(x_local.shape[1], x_local)
+        halo = sg.halo_buffer(x_local.shape[1], x_local, n_rows)
         with torch.no_grad():
-            works = sg.start_halo_exchange(x_local, halo)
+            works = sg.start_halo_exchange(x_local, halo, chunks)
             with kops.sharing_gpu():  # the exchange's RCCL kernels run beside this pass
                 out = sg.backend.aggregate_transform(g_own, x_local, self.kernel, bias=bias)
             last = max((k for k, g in enumerate(g_chunks) if g.kept), default=-1)
-            for k, (c, g) in enumerate(zip(sg.chunks, g_chunks)):
+            for k, (c, g) in enumerate(zip(chunks, g_chunks)):
                 if works[k] is not None:
                     works[k].wait()
                 if not g.kept:

@@ -141,8 +141,15 @@ def _worker(rank, world, chunks, port, q):
         with torch.no_grad():
             layer.kernel.copy_(torch.from_numpy(W))
             layer.bias.copy_(torch.from_numpy(b))
-        y = layer(torch.from_numpy(x[lo:hi])).detach()
-        q.put((rank, gcn.numpy(), mx.numpy(), sg.n_halo, sum(sg.send_counts), y.numpy()))
+        y = layer(torch.from_numpy(x[lo:hi])).detach()  # push-pull halo (the default)
+        pp = sg._pp
+        assert pp is not None and pp.n_rows == pp.n_pull + pp.n_push == pp.chunks[-1].hi
+        os.environ["KGX_HALO_PUSH"] = "0"
+        try:
+            y_pull = layer(torch.from_numpy(x[lo:hi])).detach()  # pull-only halo
+        finally:
+            del os.environ["KGX_HALO_PUSH"]
+        q.put((rank, gcn.numpy(), mx.numpy(), sg.n_halo, sum(sg.send_counts), y.numpy(), y_pull.numpy(), pp.n_push))
     finally:
         dist.destroy_process_group()
 
@@ -164,8 +171,8 @@ def test_sharded_equals_unsharded_bitwise(world, chunks):
         p.start()
     results = {}
     for _ in range(world):
-        rank, gcn, mx, n_halo, n_send, y_split = q.get(timeout=90)
-        results[rank] = (gcn, mx, n_halo, n_send, y_split)
+        rank, gcn, mx, n_halo, n_send, y_split, y_pull, n_push = q.get(timeout=90)
+        results[rank] = (gcn, mx, n_halo, n_send, y_split, y_pull, n_push)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -181,10 +188,13 @@ def test_sharded_equals_unsharded_bitwise(world, chunks):
                       torch.from_numpy(b)).numpy()
     err = np.abs(gcn - y) / np.maximum(1, np.abs(y))
     assert err.max() <= 1e-5
-    # overlapped layer path: own-source part then halo part per row (re-associated sum)
-    y_split = np.concatenate([results[r][4] for r in range(world)])
-    err = np.abs(y_split - y) / np.maximum(1, np.abs(y))
-    assert err.max() <= 1e-5
+    # overlapped layer path, push-pull and pull-only halos: own-source part, then
+    # one part per halo chunk per row (re-associated sums)
+    assert sum(results[r][6] for r in range(world)) > 0  # partial sums were pushed
+    for i in (4, 5):
+        y_split = np.concatenate([results[r][i] for r in range(world)])
+        err = np.abs(y_split - y) / np.maximum(1, np.abs(y))
+        assert err.max() <= 1e-5
 
 
 

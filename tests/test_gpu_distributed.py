@@ -131,22 +131,29 @@ def _run_fused_rank(rank, hub, dev, x, chunks, out):
         torch.cuda.synchronize()
         g_own, g_chunks = sg.own_halo_parts()
         covered = all(bool((g.items[:, 2] > g.items[:, 1]).all()) for g in g_chunks if g.n_items)
-        out[rank] = (y.detach().cpu().numpy(), layer.kernel.detach().cpu().numpy(), len(g_chunks),
-                     g_own.kept + sum(g.kept for g in g_chunks) == sg.graph.kept, covered)
+        whole = g_own.kept + sum(g.kept for g in g_chunks) == sg.graph.kept
+        if sg._pp is not None:  # push-pull: every halo row is a source row or a pushed partial
+            pp = sg._pp
+            covered = covered and all(bool((g.items[:, 2] > g.items[:, 1]).all()) for g in pp.parts if g.n_items)
+            whole = whole and pp.n_rows == pp.n_pull + pp.n_push == pp.chunks[-1].hi and len(pp.chunks) == chunks
+        out[rank] = (y.detach().cpu().numpy(), layer.kernel.detach().cpu().numpy(), len(g_chunks), whole, covered)
     except BaseException as e:
         out[rank] = e
         hub.barrier.abort()
 
 
-@pytest.mark.parametrize("world,chunks", [(2, 1), (2, 4), (3, 3)])
-def test_sharded_gcn_chunked_halo_pipeline(world, chunks, dev):
-    """The default multi-GPU GCN path on the HIP kernels: the own-source fused
-    pass, then one accumulating fused pass per halo chunk (only over the rows
-    the chunk touches) equals the single-GPU layer within the north-star
-    tolerance (the row sums are re-associated own-then-chunks)."""
+@pytest.mark.parametrize("world,chunks,push", [(2, 1, "1"), (2, 4, "1"), (3, 3, "1"), (2, 4, "0")])
+def test_sharded_gcn_chunked_halo_pipeline(world, chunks, push, dev, monkeypatch):
+    """The default multi-GPU GCN path on the HIP kernels: owners pack pulled
+    rows and pushed partial sums in one weighted-sum pass (push="1"; "0":
+    pull-only halo), the own-source fused pass runs, then one accumulating
+    fused pass per halo chunk (only over the rows the chunk touches); equals
+    the single-GPU layer within the north-star tolerance (re-associated row
+    sums)."""
     import keras_geometric_amd as kgx
     from keras_geometric_amd import synthetic
 
+    monkeypatch.setenv("KGX_HALO_PUSH", push)
     x = torch.randn(N, F_FUSED, generator=torch.Generator().manual_seed(2)).to(dev)
     hub = ThreadHub(world)
     res = {}

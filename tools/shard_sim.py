@@ -15,6 +15,7 @@ A measurement helper, not part of the product.
 
 import argparse
 import json
+import os
 import sys
 from pathlib import Path
 
@@ -43,8 +44,8 @@ class LoopbackComm(kd.TorchComm):
     def all_to_all_single(self, out, inp, out_splits=None, in_splits=None):
         if out.dtype == torch.int64 and out_splits is None:  # the count exchange: symmetric peers
             out.copy_(inp)
-        elif out.dtype == torch.int64:  # peers' requests: random rows of this rank's range
-            out.copy_(torch.randint(0, self.n_local, out.shape, device=out.device, generator=self.gen))
+        elif out.dtype == torch.int64:  # peers' requests mirror ours, folded into this rank's range
+            out.copy_(inp.view_as(out) % self.n_local)
         elif out.numel():
             out.copy_(inp.view_as(out))
 
@@ -60,13 +61,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--chunks", default="1,2,4,8")
+    ap.add_argument("--push", default="0,1", help="KGX_HALO_PUSH values to run (0: pull-only halo)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--nodes", type=int, default=10_000_000)
     ap.add_argument("--edges", type=int, default=100_000_000)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     P = args.world
-    for K in [int(v) for v in args.chunks.split(",")]:
+    for push, K in [(p, int(v)) for p in args.push.split(",") for v in args.chunks.split(",")]:
+        os.environ["KGX_HALO_PUSH"] = push
         n_local = kd.equal_bounds(args.nodes * P, P)[1]
         comm = LoopbackComm(P, n_local)
         sg = kd.ShardedGraph.rmat(args.nodes * P, args.edges * P, seed=0, device=dev, comm=comm,
@@ -91,12 +94,16 @@ def main():
         per = len(ev) // args.steps
         launch_ms = [sum(ev[i * per + j][0].elapsed_time(ev[i * per + j][1]) for i in range(args.steps)) / args.steps
                      for j in range(per)]
+        pp = sg._pp
+        if pp is not None:
+            g_chunks = pp.parts
         print(json.dumps({
-            "world": P, "chunks": K, "step_ms": round(t0.elapsed_time(t1) / args.steps, 3),
+            "world": P, "chunks": K, "push_pull": pp is not None, "step_ms": round(t0.elapsed_time(t1) / args.steps, 3),
             "launch_ms": [round(v, 3) for v in launch_ms],
             "own_edges": g_own.kept, "chunk_edges": [g.kept for g in g_chunks],
-            "halo_rows": sg.n_halo, "chunk_items": [g.n_items for g in g_chunks],
-            "send_rows": sum(sg.send_counts), "n_local": sg.n_local,
+            "halo_rows_pull_only": sg.n_halo, "halo_rows": pp.n_rows if pp else sg.n_halo,
+            "pulled": pp.n_pull if pp else sg.n_halo, "pushed": pp.n_push if pp else 0,
+            "chunk_items": [g.n_items for g in g_chunks], "n_local": sg.n_local,
         }), flush=True)
         del sg, layer, x, g_own, g_chunks
         torch.cuda.empty_cache()
