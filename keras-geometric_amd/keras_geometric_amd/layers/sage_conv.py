@@ -115,9 +115,30 @@ class SAGEConv(MessagePassing):
             return torch.zeros((num_nodes, feat), dtype=x.dtype, device=x.device)
         g = graph_for(edge_index_obj if edge_index_obj is not None else edge_index, edge_index,
                       x.shape[0], num_nodes, n_features=x.shape[1])
+        if training and self.dropout_rate > 0:
+            return self._aggregate_dropped(x, edge_index, g)
         if self.actual_aggregator == "pooling":
             return kops.aggregate(g, self.pool_mlp(x).contiguous(), "max", exact=self.exact)
         return kops.aggregate(g, x.contiguous(), self.actual_aggregator, exact=self.exact)
+
+    def _aggregate_dropped(self, x, edge_index, g):
+        """Training-mode message dropout (sage_conv.py:280-298): every message
+        x_j (and, for 'pooling', the pool MLP's input) is its own masked copy,
+        so the messages are materialised per input edge -- x[src_e] times the
+        counter-based kgx mask of (seed, input edge id, column), 0 or 1/(1-p)
+        like keras Dropout -- and reduced by edge (idx = eid), with autograd
+        through the mask multiply and the reduction.  Keras' own RNG cannot be
+        matched bit for bit; the arithmetic given the mask is (tests/test_gpu_dropout.py)."""
+        n_src, E = x.shape[0], edge_index.shape[1]
+        src = edge_index[0].long()
+        src = torch.where(src < 0, src + n_src, src)  # take() wrap; out-of-range ids were rejected by graph_for
+        seed = int(torch.randint(0, 2**62, (1,)).item())
+        keys = torch.arange(E, dtype=torch.int32, device=x.device)
+        msg = x.index_select(0, src) * kops.dropout_mask(seed, self.dropout_rate, keys, x.shape[1])
+        reduce = self.actual_aggregator
+        if reduce == "pooling":
+            msg, reduce = self.pool_mlp(msg), "max"
+        return kops.aggregate(g, msg.contiguous(), reduce, by_edge=True, exact=self.exact)
 
     def call(self, inputs, training=None, mask=None):
         if not isinstance(inputs, (list, tuple)) or len(inputs) < 2:
@@ -125,11 +146,6 @@ class SAGEConv(MessagePassing):
         x = to_device_tensor(inputs[0], torch.float32)
         edge_index = inputs[1]
         ei = edge_index_tensor(edge_index, x.device, allow_transpose=True)
-        if training and self.dropout_rate > 0:
-            raise NotImplementedError(
-                "SAGEConv per-edge dropout in training mode is not implemented by the kgx forward "
-                "engine (sage_conv.py:294-298); use dropout_rate=0 or training=False."
-            )
         num_nodes = x.shape[0]
         aggregated = self.aggregate_neighbors(x, ei, num_nodes, training=training, edge_index_obj=edge_index)
         return self.update_nodes(x, aggregated)

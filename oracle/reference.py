@@ -186,8 +186,9 @@ def gin_forward(x, edge_index, mlp, aggregator="sum", eps: float = 0.0, eps_tens
 
 
 def sage_forward(x, edge_index, w_neigh, w_self=None, bias=None, aggregator="mean", activation="relu",
-                 normalize=False, pool=None):
-    """SAGEConv.call (sage_conv.py:351-439); pool = (kernel, bias, activation) for 'pooling'."""
+                 normalize=False, pool=None, msg_mask=None):
+    """SAGEConv.call (sage_conv.py:351-439); pool = (kernel, bias, activation) for 'pooling';
+    msg_mask [E, F]: training-mode Dropout(x_j) given its mask (sage_conv.py:280-298)."""
     x = K.cast(x, torch.float32)
     ei = _as_2xE(edge_index)
     n = x.shape[0]
@@ -198,6 +199,8 @@ def sage_forward(x, edge_index, w_neigh, w_self=None, bias=None, aggregator="mea
         src, dst = ei[0], ei[1]
         x_j = K.take(x, src, axis=0)
         _x_i = K.take(x, dst, axis=0)
+        if msg_mask is not None:
+            x_j = x_j * msg_mask
         if aggregator == "pooling":
             aggr = pooling_aggregate(x_j, dst, n, *pool)
         else:
