@@ -6,14 +6,14 @@ Every destination row is independent once its source rows are present
 per process/GPU.  Rank r owns nodes [lo, hi): their feature rows and all their
 in-edges (in the global input order, so each row's accumulation order — and
 therefore the result — is bit-identical to the single-GPU EXACT result).
-Sources owned by other ranks ("halo" rows) are fetched once per layer with a
-single all-to-all-v over RCCL (torch.distributed "nccl" = RCCL on ROCm, over
+Sources owned by other ranks ("halo" rows) arrive once per layer through
+all-to-all-v steps over RCCL (torch.distributed "nccl" = RCCL on ROCm, over
 xGMI): the send lists are planned once per graph.
 
-GCN layer, default mode (aggregate-then-transform, exchange pipelined in K
-chunks; chunk k = the k-th slice of every owner's requested rows):
-    side stream:  per chunk k: send_k = gather(x_local, send_rows_k);
-                  RCCL all-to-all -> halo[k]
+GCN layer, default mode (aggregate-then-transform, push-pull halo exchanged in
+K chunks; chunk k = the k-th slice of every owner's pull and push lists):
+    side stream:  per chunk k: send_k = owner's pulled rows and pushed partial
+                  sums (one weighted-sum pass); RCCL all-to-all -> halo[k]
     main stream:  out  = bias + (A_own x_local) W        fused kgx kernel
                   per chunk k: wait for halo[k];
                   out += (A_k halo[k]) W                  same kernel, accumulate
@@ -149,7 +149,10 @@ def default_halo_chunks(world: int) -> int:
     v = os.environ.get("KGX_HALO_CHUNKS")
     if v:
         return max(1, int(v))
-    return 4 if world > 1 else 1
+    # 2: one rank's device work at 8 weak shards (tools/shard_sim.py, exchange
+    # free) is 15.5 / 16.4 / 18.0 ms at K = 1 / 2 / 4, and at an all-to-all rate
+    # near 400 GB/s per GPU K = 2 hides half of the ~9 ms exchange
+    return 2 if world > 1 else 1
 
 
 def use_push_pull() -> bool:

@@ -28,6 +28,14 @@ from keras_geometric_amd import distributed as kd  # noqa: E402
 from keras_geometric_amd import ops as kops  # noqa: E402
 
 
+class _EventWork:
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.ev)
+
+
 class LoopbackComm(kd.TorchComm):
     """Rank 0 of a `world`-rank job whose peers mirror it (measurement stand-in)."""
 
@@ -50,8 +58,12 @@ class LoopbackComm(kd.TorchComm):
             out.copy_(inp.view_as(out))
 
     def all_to_all_start(self, out, inp, out_splits=None, in_splits=None):
+        """Asynchronous like RCCL's: the copy is queued on the current (side)
+        stream and wait() makes the then-current stream wait for it."""
         self.all_to_all_single(out, inp, out_splits, in_splits)
-        return None
+        ev = torch.cuda.Event()
+        ev.record()
+        return _EventWork(ev)
 
     def broadcast(self, t, src=0):
         pass
