@@ -598,10 +598,13 @@ class ShardedGCNConv(Layer):
             with kops.sharing_gpu():  # the exchange's RCCL kernels run beside this pass
                 out = sg.backend.aggregate_transform(g_own, x_local, self.kernel, bias=bias)
             last = max((k for k, g in enumerate(g_chunks) if g.kept), default=-1)
-            for k, (c, g) in enumerate(zip(chunks, g_chunks)):
+            for k, c in enumerate(chunks):
+                # wait for every chunk, used or not: it also orders the side stream's
+                # reads of x_local (the packing) before anything later on this stream
                 if works[k] is not None:
                     works[k].wait()
-                if not g.kept:
+                g = g_chunks[k] if k < len(g_chunks) else None
+                if g is None or not g.kept:
                     continue
                 # leave block slots to the chunks still in flight; the last pass takes the whole GPU
                 with kops.sharing_gpu() if k < last else contextlib.nullcontext():
