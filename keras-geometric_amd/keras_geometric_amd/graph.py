@@ -235,12 +235,20 @@ def split_by_source_ranges(g: CSRGraph, cuts: list[int], accumulate_from: int = 
     -0 into +0 or an inf/NaN weight into NaN where the one-pass row has none."""
     if len(cuts) < 2 or cuts[0] != 0 or cuts[-1] != g.n_src or any(a > b for a, b in zip(cuts, cuts[1:])):
         raise ValueError(f"split_by_source_ranges: cuts must rise from 0 to n_src={g.n_src} (got {cuts})")
-    row_of = row_of_slot(g)
     part_of = torch.bucketize(g.col, torch.tensor(cuts[1:-1], dtype=torch.int32, device=g.device), right=True)
+    return split_by_part(g, part_of, [(cuts[k], cuts[k + 1] - cuts[k]) for k in range(len(cuts) - 1)],
+                         accumulate_from)
+
+
+def split_by_part(g: CSRGraph, part_of: torch.Tensor, sources: list, accumulate_from: int = 1) -> list[CSRGraph]:
+    """Split every CSR row's edges by part_of[slot] in [0, len(sources)): part k
+    keeps its edges in CSR order with sources re-based to sources[k] = (base,
+    n_src) and the edge weights sliced along.  Parts k >= accumulate_from are
+    accumulate-only (see split_by_source_ranges)."""
+    row_of = row_of_slot(g)
     parts = []
-    for k in range(len(cuts) - 1):
+    for k, (base, n_src) in enumerate(sources):
         m = part_of == k
-        base, n_src = cuts[k], cuts[k + 1] - cuts[k]
         deg = torch.bincount(row_of[m], minlength=g.n_dst).to(torch.int32)[: g.n_dst]
         rowptr = torch.zeros(g.n_dst + 1, dtype=torch.int32, device=g.device)
         rowptr[1:] = torch.cumsum(deg, 0)
