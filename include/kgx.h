@@ -49,7 +49,10 @@ enum kgx_reduce { KGX_SUM = 0, KGX_MEAN = 1, KGX_MAX = 2, KGX_MIN = 3, KGX_STD =
  *   RAW : MAX / MIN without the aggregators' isinf -> 0 guard: plain
  *         keras.ops.segment_max semantics (empty segment -> -inf), as
  *         BatchGlobalPooling uses it (global_pooling.py:228-249)            */
-enum kgx_epilogue { KGX_EPI_NONE = 0, KGX_EPI_BIAS = 1, KGX_EPI_GIN = 2, KGX_EPI_RAW = 3 };
+/* KGX_EPI_ACCUM (reduce KGX_SUM only): out[row] += this launch's row sum, read
+ * from and written to `out` in place -- the sharded GIN / SAGE halo-chunk
+ * passes (no reference counterpart; distributed.py). */
+enum kgx_epilogue { KGX_EPI_NONE = 0, KGX_EPI_BIAS = 1, KGX_EPI_GIN = 2, KGX_EPI_RAW = 3, KGX_EPI_ACCUM = 4 };
 
 /* Graph-preparation flags. */
 enum kgx_csr_flags {

@@ -114,6 +114,11 @@ __device__ __forceinline__ void epilogue(const SpmmArgs& a, int32_t row, int f, 
     vload<VEC>(x, a.xroot + int64_t(row) * a.ld_x + f);
 #pragma unroll
     for (int k = 0; k < VEC; ++k) v[k] = __fadd_rn(__fmul_rn(a.gin_scale, x[k]), v[k]);
+  } else if (a.epi == KGX_EPI_ACCUM) {  // out += this part's sum (sharded halo chunks)
+    float o[VEC];
+    vload<VEC>(o, a.out + int64_t(row) * a.ld_o + f);
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) v[k] = __fadd_rn(o[k], v[k]);
   }
 }
 
@@ -433,8 +438,10 @@ extern "C" int kgx_spmm(int reduce, int epilogue, const int32_t* rowptr, const i
                         float* partials, kgx_stream_t stream_) {
   hipStream_t stream = as_stream(stream_);
   KGX_REQUIRE(reduce >= KGX_SUM && reduce <= KGX_STD, KGX_ERR_ARG, "kgx_spmm: unknown reduce %d", reduce);
-  KGX_REQUIRE(epilogue >= KGX_EPI_NONE && epilogue <= KGX_EPI_RAW, KGX_ERR_ARG, "kgx_spmm: unknown epilogue %d",
+  KGX_REQUIRE(epilogue >= KGX_EPI_NONE && epilogue <= KGX_EPI_ACCUM, KGX_ERR_ARG, "kgx_spmm: unknown epilogue %d",
               epilogue);
+  KGX_REQUIRE(epilogue != KGX_EPI_ACCUM || reduce == KGX_SUM, KGX_ERR_ARG,
+              "kgx_spmm: KGX_EPI_ACCUM accumulates plain sums only (got reduce %d)", reduce);
   KGX_REQUIRE(F >= 0 && n_rows >= 0 && n_items >= 0 && n_split >= 0, KGX_ERR_ARG, "kgx_spmm: negative size");
   if (F == 0 || n_rows == 0) return KGX_OK;
   KGX_REQUIRE(out && ld_out >= F && ld_table >= F, KGX_ERR_ARG, "kgx_spmm: bad output / leading dimensions");

@@ -84,6 +84,10 @@ class KgxBackend:
         return kops.aggregate(g, table, reduce, weighted=weighted, epilogue=epilogue, bias=bias, xroot=xroot,
                               gin_scale=gin_scale, exact=exact)
 
+    def aggregate_accumulate(self, g, table, out):
+        """out += the (unweighted) row sums of table over g, in place (KGX_EPI_ACCUM)."""
+        return kops.aggregate_accumulate(g, table, out)
+
 
 class TorchComm:
     """Collectives of the product path: torch.distributed on the process group
@@ -363,14 +367,13 @@ class ShardedGraph:
             return self._pp
         g, comm, world, lo, n_local = self.graph, self.comm, self.world, self.lo, self.n_local
         dev = g.col.device
-        if g.w is None:
-            raise ValueError("push_pull_plan needs the shard graph's edge weights (gcn_norm=True)")
         K = len(self.chunks)
         rows = torch.repeat_interleave(torch.arange(g.n_dst, device=dev), g.deg.long())
         col = g.col.long()
         halo = col >= n_local
         hs = self.halo_ids.long()[col[halo] - n_local]  # global source id per halo edge
-        hd, hw = rows[halo], g.w[halo]
+        hd = rows[halo]
+        hw = g.w[halo] if g.w is not None else torch.ones(hd.numel(), dtype=torch.float32, device=dev)
         bt = torch.tensor(self.bounds[1:-1], dtype=torch.long, device=dev)
         us, inv_s, cs = torch.unique(hs, return_inverse=True, return_counts=True)
         stride = n_local + 1
@@ -526,6 +529,41 @@ class ShardedGraph:
             cur.wait_stream(self._side)
         return works
 
+    def propagate_overlapped(self, x_local: torch.Tensor, reduce: str = "sum", *, gin_scale: float | None = None
+                             ) -> torch.Tensor:
+        """Sum / mean propagation (unweighted shard graph: GIN, SAGE) with the
+        push-pull halo exchanged in chunks on the side stream, as ShardedGCNConv:
+        the own-source pass runs while the halo is in flight, then one
+        accumulating pass (KGX_EPI_ACCUM) per landed chunk over the rows it
+        touches.  gin_scale: GIN's (1+eps) x_i + aggr (gin_conv.py:216-222).
+        Row sums are re-associated (own, then chunks): tolerance-equal to the
+        one-pass result; EXACT mode uses `propagate`."""
+        if reduce not in ("sum", "mean"):
+            raise ValueError(f"propagate_overlapped: sum or mean only (got {reduce!r})")
+        x_local = x_local.contiguous()
+        g_own, _ = self.own_halo_parts()
+        pp = self.push_pull_plan()
+        halo = self.halo_buffer(x_local.shape[1], x_local, pp.n_rows)
+        fold_gin = gin_scale is not None and reduce == "sum"
+        with torch.no_grad():
+            works = self.start_halo_exchange(x_local, halo, pp.chunks)
+            with kops.sharing_gpu():
+                out = self.backend.aggregate(g_own, x_local, "sum", epilogue=nat.EPI_GIN if fold_gin else nat.EPI_NONE,
+                                             xroot=x_local if fold_gin else None,
+                                             gin_scale=float(gin_scale) if fold_gin else 1.0)
+            for k, c in enumerate(pp.chunks):
+                if works[k] is not None:
+                    works[k].wait()
+                g = pp.parts[k] if k < len(pp.parts) else None
+                if g is not None and g.kept:
+                    self.backend.aggregate_accumulate(g, halo[c.lo: c.hi], out)
+            if reduce == "mean":  # aggregators.py:56-85: sum / max(count, 1e-8), count in fp32
+                count = torch.clamp(self.graph.deg[: self.n_local].to(torch.float32), min=1e-8)
+                out = out / count.unsqueeze(1)
+                if gin_scale is not None:
+                    out = torch.tensor(float(gin_scale), dtype=torch.float32, device=out.device) * x_local + out
+        return out
+
     def propagate(self, x_local: torch.Tensor, reduce: str = "sum", **kw) -> torch.Tensor:
         """Sharded MessagePassing.propagate with the default message x_j."""
         table = self.new_table(x_local.shape[1], x_local)
@@ -651,8 +689,11 @@ class ShardedGINConv(_ShardedWrap):
         sg, conv = self.sg, self.conv
         x_local = x_local.contiguous()
         with torch.no_grad():
-            h = sg.propagate(x_local, conv.aggregator, epilogue=nat.EPI_GIN, xroot=x_local,
-                             gin_scale=conv._scale())
+            if not sg.exact and conv.aggregator in ("sum", "mean"):  # halo pipelined under the own-source pass
+                h = sg.propagate_overlapped(x_local, conv.aggregator, gin_scale=float(conv._scale()))
+            else:
+                h = sg.propagate(x_local, conv.aggregator, epilogue=nat.EPI_GIN, xroot=x_local,
+                                 gin_scale=conv._scale())
             return conv.mlp(h, training=training)
 
 
@@ -674,6 +715,8 @@ class ShardedSAGEConv(_ShardedWrap):
         with torch.no_grad():
             if conv.actual_aggregator == "pooling":
                 aggr = sg.propagate(conv.pool_mlp(x_local).contiguous(), "max")
+            elif not sg.exact and conv.actual_aggregator in ("sum", "mean"):
+                aggr = sg.propagate_overlapped(x_local, conv.actual_aggregator)
             else:
                 aggr = sg.propagate(x_local, conv.actual_aggregator)
             return conv.update_nodes(x_local, aggr)

@@ -80,6 +80,62 @@ def _spmm_fake(table, rowptr, rows, items, split, idx, w, n_slots, reduce, epilo
     return table.new_empty((rowptr.shape[0] - 1, table.shape[1]))
 
 
+@torch.library.custom_op("kgx::spmm_acc_", mutates_args=("out",))
+def spmm_acc_(
+    out: torch.Tensor,
+    table: torch.Tensor,
+    rowptr: torch.Tensor,
+    rows: torch.Tensor,
+    items: Optional[torch.Tensor],
+    split: Optional[torch.Tensor],
+    idx: torch.Tensor,
+    w: Optional[torch.Tensor],
+    n_slots: int,
+) -> None:
+    """out[i] += SUM_{e in row i} table[idx[e]] (* w[e]) in place (KGX_EPI_ACCUM)."""
+    table, w = _f32c(table), _f32c(w)
+    dev = nat.require_device(out, table, rowptr, rows, idx, w, items, split)
+    n_dst = rowptr.numel() - 1
+    F = table.shape[1]
+    if out.dtype != torch.float32 or out.shape != (n_dst, F) or out.stride(1) != 1:
+        raise ValueError(f"spmm_acc_: out must be float32 [{n_dst}, {F}] with unit column stride")
+    if n_dst == 0 or F == 0:
+        return
+    n_items = 0 if items is None else items.shape[0]
+    n_split = 0 if split is None else split.shape[0]
+    partials = None
+    if items is not None and n_split > 0:
+        partials = torch.empty((n_slots, F), dtype=torch.float32, device=dev)
+    nat.check(
+        nat.lib().kgx_spmm(
+            nat.SUM, nat.EPI_ACCUM, nat.ptr(rowptr), nat.ptr(rows), n_dst,
+            nat.ptr(items), n_items, nat.ptr(split), n_split,
+            nat.ptr(idx), nat.ptr(w), nat.ptr(table), table.stride(0), F,
+            nat.ptr(out), out.stride(0), None, None, 0, 1.0, None, 0.0, 0, nat.ptr(partials), nat.stream(dev),
+        ),
+        "kgx_spmm",
+    )
+
+
+@spmm_acc_.register_fake
+def _spmm_acc_fake(out, table, rowptr, rows, items, split, idx, w, n_slots):
+    return None
+
+
+def aggregate_accumulate(g: CSRGraph, table: torch.Tensor, out: torch.Tensor, *, weighted: bool = False) -> torch.Tensor:
+    """out += (weighted) row sums of table rows over g, in place; forward only.
+    Meant for accumulate-only graphs (graph.split_by_part), whose schedules skip
+    the rows they add nothing to."""
+    if _needs_grad(table, out):
+        raise NotImplementedError("aggregate_accumulate is a forward-only (no_grad) path")
+    items, _, split, _, n_slots = g.work(False)
+    w = g.w if weighted else None
+    if weighted and w is None:
+        raise ValueError("graph was built without edge weights")
+    _timed(lambda: torch.ops.kgx.spmm_acc_(out, table, g.rowptr, g.rows, items, split, g.col, w, n_slots))
+    return out
+
+
 # Launch hint (results unchanged): while set, fused launches leave 1/8 of the
 # block slots free for a concurrent collective (distributed.py's own-source pass).
 _SHARE_GPU = False
