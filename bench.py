@@ -188,7 +188,9 @@ def main() -> None:
         n_moved = pp.n_rows if pp is not None else sg.n_halo
         shard_info = {"halo_rows_pull_only_per_rank": sg.n_halo, "halo_rows_per_rank": n_moved,
                       "halo_rows_pushed_partials": pp.n_push if pp is not None else 0,
-                      "halo_MB_per_layer": n_moved * f_in * 4 / 1e6, "halo_chunks": len(sg.chunks)}
+                      "halo_MB_per_layer": n_moved * f_in * 4 / 1e6,
+                      "halo_chunks": sg.halo_k if sg.halo_k is not None else len(sg.chunks),
+                      "halo_chunk_tuning_s": sg.tuning}
 
     for _ in range(args.warmup):
         step()

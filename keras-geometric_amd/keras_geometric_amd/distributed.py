@@ -32,6 +32,7 @@ from __future__ import annotations
 
 import contextlib
 import os
+import time
 from dataclasses import dataclass
 
 import torch
@@ -247,7 +248,11 @@ class ShardedGraph:
     _parts: tuple | None = None  # (own-source CSR, [halo-chunk CSRs]), built on first use
     _side: object = None  # HIP stream for the halo exchange
     _halo_buf: dict | None = None
-    _pp: PushPullPlan | None = None
+    _pp: PushPullPlan | None = None  # the push-pull plan last used
+    _pp_by_k: dict | None = None
+    chunks_fixed: bool = False  # K given (halo_chunks= or KGX_HALO_CHUNKS): no tuning
+    halo_k: int | None = None  # push-pull chunk count chosen by tune_halo_chunks
+    tuning: dict | None = None  # K -> slowest rank's forward seconds
 
     @property
     def lo(self) -> int:
@@ -273,6 +278,7 @@ class ShardedGraph:
         comm = comm or TorchComm()
         rank, world = comm.rank(), comm.world()
         n_chunks = default_halo_chunks(world) if halo_chunks is None else max(1, int(halo_chunks))
+        chunks_fixed = halo_chunks is not None or bool(os.environ.get("KGX_HALO_CHUNKS"))
         lo, hi = bounds[rank], bounds[rank + 1]
         n_local = hi - lo
         dev = src.device
@@ -311,7 +317,7 @@ class ShardedGraph:
                                 n_features)
         sg = cls(rank=rank, world=world, n_global=bounds[-1], bounds=list(bounds), graph=g,
                  send_counts=send_counts, recv_counts=recv_counts, halo_ids=halo_table_ids.to(torch.int32),
-                 chunks=chunks, dinv_table=None, backend=backend, comm=comm, exact=exact)
+                 chunks=chunks, dinv_table=None, backend=backend, comm=comm, exact=exact, chunks_fixed=chunks_fixed)
         if gcn_norm:
             dinv_local = backend.dinv(g.deg)
             table = torch.empty((n_src, 1), dtype=torch.float32, device=dev)
@@ -345,7 +351,7 @@ class ShardedGraph:
             return self.backend.gather_rows(x_local, c.send_rows)
         return x_local.new_empty((0, x_local.shape[1]))
 
-    def push_pull_plan(self) -> PushPullPlan:
+    def push_pull_plan(self, n_chunks: int | None = None) -> PushPullPlan:
         """A smaller halo for the weighted-sum (GCN) path.  Collective: every
         rank calls it once (ShardedGCNConv does, on its first forward).
 
@@ -363,11 +369,14 @@ class ShardedGraph:
         send CSR (a pulled row = one edge of weight 1, multiplied exactly).
         Row sums are re-associated (partials first), so this is a tolerance
         path like the rest of the overlapped layer; EXACT mode keeps pulling."""
-        if self._pp is not None:
+        K = n_chunks or self.halo_k or len(self.chunks)
+        if self._pp_by_k is None:
+            self._pp_by_k = {}
+        if K in self._pp_by_k:
+            self._pp = self._pp_by_k[K]
             return self._pp
         g, comm, world, lo, n_local = self.graph, self.comm, self.world, self.lo, self.n_local
         dev = g.col.device
-        K = len(self.chunks)
         rows = torch.repeat_interleave(torch.arange(g.n_dst, device=dev), g.deg.long())
         col = g.col.long()
         halo = col >= n_local
@@ -466,7 +475,35 @@ class ShardedGraph:
             # a leading empty range makes every chunk part accumulate-only
             parts = list(self.backend.split_by_source(rg, [0, 0] + [c.hi for c in chunks])[1:])
         self._pp = PushPullPlan(chunks=chunks, parts=parts, n_rows=off, n_pull=rp[-1], n_push=ru[-1])
+        self._pp_by_k[K] = self._pp
         return self._pp
+
+    def tune_halo_chunks(self, run, candidates=(1, 2, 4)) -> int:
+        """Choose the push-pull chunk count K by timing one forward per
+        candidate (`run(K)`; plans are built before their timed call).  The
+        best K depends on the all-to-all rate of the machine (K = 1
+        has the least device work, more chunks hide more of a slow exchange),
+        so it is measured, like a library autotuner, not assumed.  Collective:
+        every rank times the same candidates and the slowest rank's time counts."""
+        dev = self.graph.col.device
+        times = []
+        for K in candidates:
+            self.push_pull_plan(K)
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            run(K)
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            times.append(time.perf_counter() - t0)
+        t = torch.tensor(times, dtype=torch.float64, device=dev)
+        every = torch.empty(self.world * t.numel(), dtype=torch.float64, device=dev)
+        self.comm.all_to_all_single(every, t.repeat(self.world).contiguous())
+        worst = every.view(self.world, -1).max(0).values.cpu()
+        self.halo_k = int(candidates[int(torch.argmin(worst))])
+        self.tuning = {int(k): float(v) for k, v in zip(candidates, worst)}
+        self.push_pull_plan(self.halo_k)
+        return self.halo_k
 
     def halo_exchange(self, table: torch.Tensor) -> None:
         """table[n_local:] <- rows other ranks own (one all-to-all-v over RCCL
@@ -612,7 +649,21 @@ class ShardedGCNConv(Layer):
                                     epilogue=nat.EPI_BIAS if use_b else nat.EPI_NONE,
                                     bias=self.bias if use_b else None, exact=sg.exact)
 
-    def _forward_overlapped(self, x_local: torch.Tensor, bias) -> torch.Tensor:
+    def tune(self, x_local: torch.Tensor) -> int | None:
+        """Time the push-pull chunk counts once (ShardedGraph.tune_halo_chunks);
+        a no-op when K is fixed, on one rank, or off the default path."""
+        sg = self.sg
+        if not self.built:
+            self._build_device = x_local.device
+            self.build(tuple(x_local.shape))
+        use_b = self.use_bias and self.bias is not None
+        if (sg.exact or sg.chunks_fixed or sg.world < 2 or sg.halo_k is not None or not use_push_pull()
+                or not sg.backend.supports_fused(x_local.shape[1], self.output_dim)):
+            return sg.halo_k
+        with torch.no_grad():
+            return sg.tune_halo_chunks(lambda K: self._forward_overlapped(x_local, self.bias if use_b else None, K))
+
+    def _forward_overlapped(self, x_local: torch.Tensor, bias, n_chunks: int | None = None) -> torch.Tensor:
         """Aggregate-then-transform with the halo exchange pipelined in chunks:
         side stream, per chunk k: pack its send rows of X -> RCCL all-to-all
         into halo[k];
@@ -627,7 +678,9 @@ class ShardedGCNConv(Layer):
         g_own, g_chunks = sg.own_halo_parts()
         chunks, n_rows = sg.chunks, sg.n_halo
         if use_push_pull():
-            pp = sg.push_pull_plan()
+            if n_chunks is None and sg.halo_k is None and not sg.chunks_fixed and sg.world > 1:
+                self.tune(x_local)  # first call: measure K = 1 / 2 / 4 once
+            pp = sg.push_pull_plan(n_chunks)
             chunks, g_chunks, n_rows = pp.chunks, pp.parts, pp.n_rows
         x_local = x_local.contiguous()
         halo = sg.halo_buffer(x_local.shape[1], x_local, n_rows)

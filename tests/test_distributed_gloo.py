@@ -153,7 +153,20 @@ def _worker(rank, world, chunks, port, q):
             y_pull = layer(torch.from_numpy(x[lo:hi])).detach()  # pull-only halo
         finally:
             del os.environ["KGX_HALO_PUSH"]
-        q.put((rank, gcn.numpy(), mx.numpy(), sg.n_halo, sum(sg.send_counts), y.numpy(), y_pull.numpy(), pp.n_push))
+        # K left open: the first forward times K = 1 / 2 / 4 (collective) and keeps the fastest
+        sg2 = kd.ShardedGraph.build(torch.from_numpy(s[keep]), torch.from_numpy(d[keep]), bounds,
+                                    backend=OracleBackend(), n_features=F_OUT)
+        layer2 = kd.ShardedGCNConv(F_OUT, sg2)
+        layer2._build_device = torch.device("cpu")
+        layer2.build((hi - lo, F_IN))
+        with torch.no_grad():
+            layer2.kernel.copy_(torch.from_numpy(W))
+            layer2.bias.copy_(torch.from_numpy(b))
+        y_tuned = layer2(torch.from_numpy(x[lo:hi])).detach()
+        assert sorted(sg2.tuning) == [1, 2, 4] and sg2.halo_k in (1, 2, 4)
+        assert len(sg2._pp.chunks) == sg2.halo_k
+        q.put((rank, gcn.numpy(), mx.numpy(), sg.n_halo, sum(sg.send_counts), y.numpy(), y_pull.numpy(), pp.n_push,
+               y_tuned.numpy()))
     finally:
         dist.destroy_process_group()
 
@@ -175,8 +188,8 @@ def test_sharded_equals_unsharded_bitwise(world, chunks):
         p.start()
     results = {}
     for _ in range(world):
-        rank, gcn, mx, n_halo, n_send, y_split, y_pull, n_push = q.get(timeout=90)
-        results[rank] = (gcn, mx, n_halo, n_send, y_split, y_pull, n_push)
+        rank, gcn, mx, n_halo, n_send, y_split, y_pull, n_push, y_tuned = q.get(timeout=90)
+        results[rank] = (gcn, mx, n_halo, n_send, y_split, y_pull, n_push, y_tuned)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -195,7 +208,7 @@ def test_sharded_equals_unsharded_bitwise(world, chunks):
     # overlapped layer path, push-pull and pull-only halos: own-source part, then
     # one part per halo chunk per row (re-associated sums)
     assert sum(results[r][6] for r in range(world)) > 0  # partial sums were pushed
-    for i in (4, 5):
+    for i in (4, 5, 7):
         y_split = np.concatenate([results[r][i] for r in range(world)])
         err = np.abs(y_split - y) / np.maximum(1, np.abs(y))
         assert err.max() <= 1e-5
