@@ -90,6 +90,22 @@ __device__ __forceinline__ void lds_barrier() {
 typedef short bf16x8_t __attribute__((ext_vector_type(8)));
 typedef short bf16x4_t __attribute__((ext_vector_type(4)));
 
+#ifndef KGX_FUSED_QUAD_IDX
+#define KGX_FUSED_QUAD_IDX 0
+#endif
+
+#if KGX_FUSED_QUAD_IDX
+// value of lane (quad base + u) for every lane of each quad (DPP quad_perm [u,u,u,u])
+__device__ __forceinline__ int32_t quad_bcast(int32_t v, int u) {
+  switch (u) {
+    case 0: return __builtin_amdgcn_mov_dpp(v, 0x00, 0xF, 0xF, false);
+    case 1: return __builtin_amdgcn_mov_dpp(v, 0x55, 0xF, 0xF, false);
+    case 2: return __builtin_amdgcn_mov_dpp(v, 0xAA, 0xF, 0xF, false);
+    default: return __builtin_amdgcn_mov_dpp(v, 0xFF, 0xF, 0xF, false);
+  }
+}
+#endif
+
 template <int RED>
 struct Red {
   static __device__ __forceinline__ float init() {
@@ -233,12 +249,30 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
       const int n = end - e;
       int32_t c[B];
       float wt[B];
+#if KGX_FUSED_QUAD_IDX
+      // one index (and weight) load per lane instead of B: lane l fetches edge
+      // l % B of the block, so every quad of the group holds all B (B <= 4),
+      // and a quad_perm DPP broadcast hands edge u's values to every lane
+      {
+        const int q = lane & (B - 1);
+        const int32_t ee = q < n ? e + q : end - 1;
+        const int32_t cl = a.idx[ee];
+        float wl = 0.0f;
+        if constexpr (WEIGHTED) wl = a.w[ee];
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+          c[u] = quad_bcast(cl, u);
+          if constexpr (WEIGHTED) wt[u] = __builtin_bit_cast(float, quad_bcast(__builtin_bit_cast(int32_t, wl), u));
+        }
+      }
+#else
 #pragma unroll
       for (int u = 0; u < B; ++u) {
         const int32_t ee = u < n ? e + u : end - 1;
         c[u] = a.idx[ee];
         if constexpr (WEIGHTED) wt[u] = a.w[ee];
       }
+#endif
       float v[B][4];
 #pragma unroll
       for (int u = 0; u < B; ++u) vload<4>(v[u], a.x + row_off(c[u], a.ld_x) + f);
