@@ -478,7 +478,7 @@ class ShardedGraph:
         self._pp_by_k[K] = self._pp
         return self._pp
 
-    def tune_halo_chunks(self, run, candidates=(1, 2, 4)) -> int:
+    def tune_halo_chunks(self, run, candidates=(1, 2, 4, 8)) -> int:
         """Choose the push-pull chunk count K by timing one forward per
         candidate (`run(K)`; plans are built before their timed call).  The
         best K depends on the all-to-all rate of the machine (K = 1
@@ -679,7 +679,7 @@ class ShardedGCNConv(Layer):
         chunks, n_rows = sg.chunks, sg.n_halo
         if use_push_pull():
             if n_chunks is None and sg.halo_k is None and not sg.chunks_fixed and sg.world > 1:
-                self.tune(x_local)  # first call: measure K = 1 / 2 / 4 once
+                self.tune(x_local)  # first call: measure K = 1 / 2 / 4 / 8 once
             pp = sg.push_pull_plan(n_chunks)
             chunks, g_chunks, n_rows = pp.chunks, pp.parts, pp.n_rows
         x_local = x_local.contiguous()
