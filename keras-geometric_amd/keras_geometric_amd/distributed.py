@@ -489,13 +489,16 @@ class ShardedGraph:
         times = []
         for K in candidates:
             self.push_pull_plan(K)
-            if dev.type == "cuda":
-                torch.cuda.synchronize(dev)
-            t0 = time.perf_counter()
-            run(K)
-            if dev.type == "cuda":
-                torch.cuda.synchronize(dev)
-            times.append(time.perf_counter() - t0)
+            best = float("inf")
+            for _ in range(2):  # best of two: the first also warms the plan's launches
+                if dev.type == "cuda":
+                    torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+                run(K)
+                if dev.type == "cuda":
+                    torch.cuda.synchronize(dev)
+                best = min(best, time.perf_counter() - t0)
+            times.append(best)
         t = torch.tensor(times, dtype=torch.float64, device=dev)
         every = torch.empty(self.world * t.numel(), dtype=torch.float64, device=dev)
         self.comm.all_to_all_single(every, t.repeat(self.world).contiguous())
