@@ -4,8 +4,9 @@
 
 Builds rank 0's shard of the P x 10M-node / P x 100M-edge R-MAT graph as
 bench.py --gpus P does, but with a loopback comm: the peers' requests are
-synthetic (random rows of this rank's range, as many as this rank requests
-from them) and the all-to-all is a device copy.  So the timed step is the
+synthetic (this rank's own requests mirrored, folded into its range, so as
+many rows as it requests from them) and the all-to-all is an asynchronous
+device copy on the side stream.  So the timed step is the
 rank's compute side of ShardedGCNConv -- send-row packing, the own-source
 pass and one accumulating pass per halo chunk -- with the exchange itself
 free.  It prices the chunked pipeline's extra passes against one halo pass
@@ -41,7 +42,6 @@ class LoopbackComm(kd.TorchComm):
 
     def __init__(self, world: int, n_local: int):
         self.w, self.n_local = world, n_local
-        self.gen = torch.Generator(device="cuda").manual_seed(7)
 
     def rank(self):
         return 0
