@@ -287,3 +287,71 @@ def test_sharded_gin_sage_layers():
         scale = np.maximum(1, np.abs(ref) if scales[i] is None else scales[i])
         errs.append(float((np.abs(got - ref) / scale).max()))
     assert max(errs) <= 1e-5, errs
+
+
+def _local_only_worker(rank, world, port, q):
+    """Every edge stays inside its destination's shard: no halo rows at all."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        s, d, x, W, b = _local_only_graph()
+        bounds = kd.equal_bounds(N, world)
+        lo, hi = bounds[rank], bounds[rank + 1]
+        keep = (d >= lo) & (d < hi)
+        sg = kd.ShardedGraph.build(torch.from_numpy(s[keep]), torch.from_numpy(d[keep]), bounds,
+                                   backend=OracleBackend(), n_features=F_OUT)
+        layer = kd.ShardedGCNConv(F_OUT, sg)
+        layer._build_device = torch.device("cpu")
+        layer.build((hi - lo, F_IN))
+        with torch.no_grad():
+            layer.kernel.copy_(torch.from_numpy(W))
+            layer.bias.copy_(torch.from_numpy(b))
+        y = layer(torch.from_numpy(x[lo:hi])).detach()
+        gsg = kd.ShardedGraph.build(torch.from_numpy(s[keep]), torch.from_numpy(d[keep]), bounds,
+                                    backend=OracleBackend(), n_features=F_IN, self_loops=False, gcn_norm=False)
+        gin = kd.ShardedGINConv(F_OUT, gsg, aggregator="sum", eps_init=0.5)
+        gin._ensure_built(torch.from_numpy(x[lo:hi]))
+        h = gin(torch.from_numpy(x[lo:hi]))
+        q.put((rank, sg.n_halo, sg._pp.n_rows, y.numpy(), h.numpy(), [a for a in gin.conv.get_weights()]))
+    finally:
+        dist.destroy_process_group()
+
+
+def _local_only_graph():
+    s, d, x, W, b = _graph()
+    half = N // 2
+    s = np.where((s < half) == (d < half), s, (s + half) % N).astype(s.dtype)  # source moved into d's half
+    return s, d, x, W, b
+
+
+@pytest.mark.timeout(180)
+def test_sharded_no_halo():
+    """Shards without any remote source: empty halo plans (no pulled rows, no
+    pushed partials, empty chunks), chunk tuning and the pipelined GCN / GIN
+    paths still run and equal the oracle layers."""
+    if torch.cuda.is_initialized():
+        pytest.skip("never start processes from a process that has initialised the GPU")
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_local_only_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r = q.get(timeout=90)
+        res[r[0]] = r[1:]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(res[r][0] == 0 and res[r][1] == 0 for r in range(world))
+    s, d, x, W, b = _local_only_graph()
+    X, EI = torch.from_numpy(x), torch.from_numpy(np.stack([s, d]))
+    y = R.gcn_forward(X, EI, torch.from_numpy(W), torch.from_numpy(b)).numpy()
+    got = np.concatenate([res[r][2] for r in range(world)])
+    assert (np.abs(got - y) / np.maximum(1, np.abs(y))).max() <= 1e-5
+    w = [torch.from_numpy(a) for a in res[0][4]]
+    h = R.gin_forward(X, EI, [(w[0], w[1], None)], "sum", eps=0.5).numpy()
+    got = np.concatenate([res[r][3] for r in range(world)])
+    assert (np.abs(got - h) / np.maximum(1, np.abs(h))).max() <= 1e-5

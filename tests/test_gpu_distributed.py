@@ -283,3 +283,54 @@ def test_sharded_gin_sage_pipelined_hip(dev):
         got = np.concatenate([res[r][0][i][0] for r in range(world)])
         err = np.abs(got - ref) / np.maximum(1.0, scale)
         assert err.max() <= 1e-5, (i, err.max())
+
+
+def _run_no_halo_rank(rank, hub, dev, s, d, x, out):
+    try:
+        comm = ThreadComm(hub, rank)
+        bounds = kd.equal_bounds(N, hub.world)
+        lo, hi = bounds[rank], bounds[rank + 1]
+        keep = (d >= lo) & (d < hi)
+        sg = kd.ShardedGraph.build(torch.from_numpy(s[keep]).to(dev), torch.from_numpy(d[keep]).to(dev), bounds,
+                                   comm=comm, n_features=F_FUSED)
+        layer = kd.ShardedGCNConv(64, sg)
+        y = layer(x[lo:hi])
+        torch.cuda.synchronize()
+        out[rank] = (y.detach().cpu().numpy(), layer.kernel.detach().cpu().numpy(), sg.n_halo, sg._pp.n_rows,
+                     sg.halo_k)
+    except BaseException as e:
+        out[rank] = e
+        hub.barrier.abort()
+
+
+def test_sharded_gcn_no_halo_hip(dev):
+    """Shards with no remote source on the HIP kernels: empty pull and push
+    plans, empty chunk parts and the K tuning still run; the result equals the
+    single-GPU layer."""
+    import keras_geometric_amd as kgx
+    from oracle.rmat import rmat_edges, scale_for
+
+    s, d = rmat_edges(12, scale_for(N), N, 0, E)
+    half = N // 2
+    s = np.where((s < half) == (d < half), s, (s + half) % N).astype(np.int32)
+    d = d.astype(np.int32)
+    x = torch.randn(N, F_FUSED, generator=torch.Generator().manual_seed(4)).to(dev)
+    world = 2
+    hub = ThreadHub(world)
+    res = {}
+    threads = [threading.Thread(target=_run_no_halo_rank, args=(r, hub, dev, s, d, x, res)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=240)
+    for r in range(world):
+        if isinstance(res.get(r), BaseException):
+            raise res[r]
+    assert all(res[r][2] == 0 and res[r][3] == 0 and res[r][4] in (1, 2, 4, 8) for r in range(world))
+    ei = torch.from_numpy(np.stack([s, d])).to(dev)
+    layer = kgx.GCNConv(64)
+    layer([x, ei])
+    layer.set_weights([res[0][1], np.zeros(64, np.float32)])
+    ref = layer([x, ei]).detach().cpu().numpy()
+    got = np.concatenate([res[r][0] for r in range(world)])
+    assert (np.abs(got - ref) / np.maximum(1.0, np.abs(ref))).max() <= 1e-5
