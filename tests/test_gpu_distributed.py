@@ -126,9 +126,10 @@ def _run_fused_rank(rank, hub, dev, x, chunks, out):
         comm = ThreadComm(hub, rank)
         sg = kd.ShardedGraph.rmat(N, E, seed=8, device=dev, comm=comm, n_features=F_FUSED, halo_chunks=chunks)
         xl = x[sg.lo: sg.lo + sg.n_local]
-        layer = kd.ShardedGCNConv(64, sg)
+        layer = kd.ShardedGCNConv(128, sg)  # F_out >= F_in = 128: the fused, chunk-pipelined path
         y = layer(xl)
         torch.cuda.synchronize()
+        assert (sg._pp is not None) == kd.use_push_pull()
         g_own, g_chunks = sg.own_halo_parts()
         covered = all(bool((g.items[:, 2] > g.items[:, 1]).all()) for g in g_chunks if g.n_items)
         whole = g_own.kept + sum(g.kept for g in g_chunks) == sg.graph.kept
@@ -168,9 +169,9 @@ def test_sharded_gcn_chunked_halo_pipeline(world, chunks, push, dev, monkeypatch
     for r in range(world):
         assert res[r][2] == chunks and res[r][3] and res[r][4]
     ei = synthetic.rmat_edge_index(N, E, seed=8, device=dev)
-    layer = kgx.GCNConv(64)
+    layer = kgx.GCNConv(128)
     layer([x, ei])
-    layer.set_weights([res[0][1], np.zeros(64, np.float32)])
+    layer.set_weights([res[0][1], np.zeros(128, np.float32)])
     ref = layer([x, ei]).detach().cpu().numpy()
     got = np.concatenate([res[r][0] for r in range(world)])
     err = np.abs(got - ref) / np.maximum(1.0, np.abs(ref))
@@ -293,7 +294,7 @@ def _run_no_halo_rank(rank, hub, dev, s, d, x, out):
         keep = (d >= lo) & (d < hi)
         sg = kd.ShardedGraph.build(torch.from_numpy(s[keep]).to(dev), torch.from_numpy(d[keep]).to(dev), bounds,
                                    comm=comm, n_features=F_FUSED)
-        layer = kd.ShardedGCNConv(64, sg)
+        layer = kd.ShardedGCNConv(128, sg)
         y = layer(x[lo:hi])
         torch.cuda.synchronize()
         out[rank] = (y.detach().cpu().numpy(), layer.kernel.detach().cpu().numpy(), sg.n_halo, sg._pp.n_rows,
@@ -328,9 +329,9 @@ def test_sharded_gcn_no_halo_hip(dev):
             raise res[r]
     assert all(res[r][2] == 0 and res[r][3] == 0 and res[r][4] in (1, 2, 4, 8) for r in range(world))
     ei = torch.from_numpy(np.stack([s, d])).to(dev)
-    layer = kgx.GCNConv(64)
+    layer = kgx.GCNConv(128)
     layer([x, ei])
-    layer.set_weights([res[0][1], np.zeros(64, np.float32)])
+    layer.set_weights([res[0][1], np.zeros(128, np.float32)])
     ref = layer([x, ei]).detach().cpu().numpy()
     got = np.concatenate([res[r][0] for r in range(world)])
     assert (np.abs(got - ref) / np.maximum(1.0, np.abs(ref))).max() <= 1e-5
