@@ -68,6 +68,10 @@ class KgxBackend:
     def gather_rows(self, table: torch.Tensor, rows: torch.Tensor) -> torch.Tensor:
         return kops.gather_rows(table, rows)
 
+    def transform(self, x: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
+        """Node-level x W (kgx_dense; the library GEMM past its shapes)."""
+        return kops.dense(x, W)
+
     def split_by_source(self, g, cuts: list):
         """Parts of g by source range [cuts[k], cuts[k+1]); every part after the
         first is accumulate-only (graph.split_by_source_ranges)."""
@@ -85,9 +89,9 @@ class KgxBackend:
         return kops.aggregate(g, table, reduce, weighted=weighted, epilogue=epilogue, bias=bias, xroot=xroot,
                               gin_scale=gin_scale, exact=exact)
 
-    def aggregate_accumulate(self, g, table, out):
-        """out += the (unweighted) row sums of table over g, in place (KGX_EPI_ACCUM)."""
-        return kops.aggregate_accumulate(g, table, out)
+    def aggregate_accumulate(self, g, table, out, weighted=False):
+        """out += the (weighted) row sums of table over g, in place (KGX_EPI_ACCUM)."""
+        return kops.aggregate_accumulate(g, table, out, weighted=weighted)
 
 
 class TorchComm:
@@ -569,8 +573,8 @@ class ShardedGraph:
             cur.wait_stream(self._side)
         return works
 
-    def propagate_overlapped(self, x_local: torch.Tensor, reduce: str = "sum", *, gin_scale: float | None = None
-                             ) -> torch.Tensor:
+    def propagate_overlapped(self, x_local: torch.Tensor, reduce: str = "sum", *, gin_scale: float | None = None,
+                             weighted: bool = False, bias: torch.Tensor | None = None) -> torch.Tensor:
         """Sum / mean propagation (unweighted shard graph: GIN, SAGE) with the
         push-pull halo exchanged in chunks on the side stream, as ShardedGCNConv:
         the own-source pass runs while the halo is in flight, then one
@@ -580,6 +584,8 @@ class ShardedGraph:
         one-pass result; EXACT mode uses `propagate`."""
         if reduce not in ("sum", "mean"):
             raise ValueError(f"propagate_overlapped: sum or mean only (got {reduce!r})")
+        if (weighted or bias is not None) and (reduce != "sum" or gin_scale is not None):
+            raise ValueError("propagate_overlapped: weights / bias go with a plain sum (the GCN layer)")
         x_local = x_local.contiguous()
         g_own, _ = self.own_halo_parts()
         pp = self.push_pull_plan()
@@ -587,8 +593,9 @@ class ShardedGraph:
         fold_gin = gin_scale is not None and reduce == "sum"
         with torch.no_grad():
             works = self.start_halo_exchange(x_local, halo, pp.chunks)
+            epi = nat.EPI_GIN if fold_gin else (nat.EPI_BIAS if bias is not None else nat.EPI_NONE)
             with kops.sharing_gpu():
-                out = self.backend.aggregate(g_own, x_local, "sum", epilogue=nat.EPI_GIN if fold_gin else nat.EPI_NONE,
+                out = self.backend.aggregate(g_own, x_local, "sum", weighted=weighted, epilogue=epi, bias=bias,
                                              xroot=x_local if fold_gin else None,
                                              gin_scale=float(gin_scale) if fold_gin else 1.0)
             for k, c in enumerate(pp.chunks):
@@ -596,7 +603,7 @@ class ShardedGraph:
                     works[k].wait()
                 g = pp.parts[k] if k < len(pp.parts) else None
                 if g is not None and g.kept:
-                    self.backend.aggregate_accumulate(g, halo[c.lo: c.hi], out)
+                    self.backend.aggregate_accumulate(g, halo[c.lo: c.hi], out, weighted=weighted)
             if reduce == "mean":  # aggregators.py:56-85: sum / max(count, 1e-8), count in fp32
                 count = torch.clamp(self.graph.deg[: self.n_local].to(torch.float32), min=1e-8)
                 out = out / count.unsqueeze(1)
@@ -644,6 +651,12 @@ class ShardedGCNConv(Layer):
         use_b = self.use_bias and self.bias is not None
         if not sg.exact and sg.backend.supports_fused(x_local.shape[1], self.output_dim):
             return self._forward_overlapped(x_local, self.bias if use_b else None)
+        if not sg.exact and use_push_pull() and sg.graph.w is not None:
+            # transform first (F_out < F_in: narrower rows to exchange), then the
+            # weighted sum with the push-pull halo pipelined under the own-source pass
+            with torch.no_grad():
+                h = sg.backend.transform(x_local.contiguous(), self.kernel)
+                return sg.propagate_overlapped(h, "sum", weighted=True, bias=self.bias if use_b else None)
         table = sg.new_table(self.output_dim, x_local)
         with torch.no_grad():  # forward engine: X W written straight into the table's own-rows slice
             torch.matmul(x_local, self.kernel, out=table[: sg.n_local])

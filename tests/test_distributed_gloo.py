@@ -56,9 +56,12 @@ class OracleBackend:
                                          device=torch.device("cpu")))
         return parts
 
-    def aggregate_accumulate(self, g, table, out):
-        out += self.aggregate(g, table, "sum")
+    def aggregate_accumulate(self, g, table, out, weighted=False):
+        out += self.aggregate(g, table, "sum", weighted=weighted)
         return out
+
+    def transform(self, x, W):
+        return torch.matmul(x, W)
 
     def supports_fused(self, f_in, f_out):
         return True
@@ -84,6 +87,11 @@ class OracleBackend:
         elif epilogue == nat.EPI_GIN:  # (1+eps) x_i + aggr (gin_conv.py:216-222)
             out = torch.tensor(kw["gin_scale"], dtype=torch.float32) * kw["xroot"] + out
         return out
+
+
+class UnfusedOracleBackend(OracleBackend):
+    def supports_fused(self, f_in, f_out):
+        return False
 
 
 def _free_port():
@@ -165,8 +173,19 @@ def _worker(rank, world, chunks, port, q):
         y_tuned = layer2(torch.from_numpy(x[lo:hi])).detach()
         assert sorted(sg2.tuning) == [1, 2, 4, 8] and sg2.halo_k in (1, 2, 4, 8)
         assert len(sg2._pp.chunks) == sg2.halo_k
+        # shapes the fused kernel does not take: X W first, then the pipelined weighted sum
+        sg3 = kd.ShardedGraph.build(torch.from_numpy(s[keep]), torch.from_numpy(d[keep]), bounds,
+                                    backend=UnfusedOracleBackend(), n_features=F_OUT, halo_chunks=chunks)
+        layer3 = kd.ShardedGCNConv(F_OUT, sg3)
+        layer3._build_device = torch.device("cpu")
+        layer3.build((hi - lo, F_IN))
+        with torch.no_grad():
+            layer3.kernel.copy_(torch.from_numpy(W))
+            layer3.bias.copy_(torch.from_numpy(b))
+        y_unfused = layer3(torch.from_numpy(x[lo:hi])).detach()
+        assert sg3._pp is not None
         q.put((rank, gcn.numpy(), mx.numpy(), sg.n_halo, sum(sg.send_counts), y.numpy(), y_pull.numpy(), pp.n_push,
-               y_tuned.numpy()))
+               y_tuned.numpy(), y_unfused.numpy()))
     finally:
         dist.destroy_process_group()
 
@@ -188,8 +207,8 @@ def test_sharded_equals_unsharded_bitwise(world, chunks):
         p.start()
     results = {}
     for _ in range(world):
-        rank, gcn, mx, n_halo, n_send, y_split, y_pull, n_push, y_tuned = q.get(timeout=90)
-        results[rank] = (gcn, mx, n_halo, n_send, y_split, y_pull, n_push, y_tuned)
+        rank, gcn, mx, n_halo, n_send, y_split, y_pull, n_push, y_tuned, y_unfused = q.get(timeout=90)
+        results[rank] = (gcn, mx, n_halo, n_send, y_split, y_pull, n_push, y_tuned, y_unfused)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -208,7 +227,7 @@ def test_sharded_equals_unsharded_bitwise(world, chunks):
     # overlapped layer path, push-pull and pull-only halos: own-source part, then
     # one part per halo chunk per row (re-associated sums)
     assert sum(results[r][6] for r in range(world)) > 0  # partial sums were pushed
-    for i in (4, 5, 7):
+    for i in (4, 5, 7, 8):
         y_split = np.concatenate([results[r][i] for r in range(world)])
         err = np.abs(y_split - y) / np.maximum(1, np.abs(y))
         assert err.max() <= 1e-5
