@@ -72,7 +72,7 @@ def _run_rank(rank, hub, dev, x, out):
         m = sg.propagate(xl, "max")
         layer = kd.ShardedGCNConv(32, sg)
         y = layer(xl)
-        sg.exact = False  # default path: fused own-source part overlapped with the halo exchange
+        sg.exact = False  # default path (F = 64, unfused): X W, then the push-pull halo pipelined under the own pass
         y2 = layer(xl)
         torch.cuda.synchronize()
         out[rank] = (s.cpu().numpy(), m.cpu().numpy(), y.detach().cpu().numpy(), layer.kernel.detach().cpu().numpy(),
