@@ -1,20 +1,28 @@
 """bench.py — GCNConv forward on MI355X: aggregated edges/s + achieved HBM GB/s.
 
 Metric (BASELINE.json): "aggregated edges/sec + achieved HBM GB/s, GCNConv fwd,
-1/2/4/8 MI355X".  A step is one full GCNConv forward (node-level X·W GEMM +
-the fused kgx aggregation with bias epilogue) over a device-resident synthetic
-R-MAT graph.  The graph's CSR/schedule is built once (graph preparation,
-reported separately as graph_build_ms) and reused across steps, as a GNN
-training loop over a fixed graph does.
+1/2/4/8 MI355X".  A step is one full layer forward over a device-resident
+synthetic R-MAT graph.  The graph's CSR/schedule is built once (graph
+preparation, reported separately as graph_build_ms; `cold_layer_ms` is one
+forward from a fresh edge_index, CSR + norm + forward, as the reference pays on
+every call) and reused across steps, as a GNN training loop over a fixed graph does.
 
-N = 1 : north-star workload — R-MAT 10M nodes / 100M edges (+10M self loops),
-        F 128 -> 128, fp32.
-N > 1 : one process per GPU (torchrun), weak scaling — every rank owns a
-        contiguous destination range of 10M nodes and ~100M edges of one global
-        R-MAT graph of N x 10M nodes / N x 100M edges; source rows owned by other
-        ranks arrive by a halo all-to-all over RCCL (xGMI) every layer.
+--config ns (default), c2: GCNConv F 128 -> 128, WEAK scaling
+    N = 1 : R-MAT 10M nodes / 100M edges (+10M self loops)   [ns]
+    N > 1 : every rank owns a contiguous destination range of 10M nodes and
+            ~100M edges of one global R-MAT graph of N x 10M nodes / N x 100M
+            edges; source rows owned by other ranks arrive by a halo all-to-all
+            over RCCL (xGMI), pipelined under the own-source pass.
+--config c4: GINConv sum, F 256, STRONG scaling: one 10M / 100M graph split by
+            destination range over the N GPUs (BASELINE.json configs[3]).
+--config c5: SAGEConv mean, F 100, STRONG scaling: the ogbn-products-shaped
+            2,449,029 / 123,718,280 graph split over the N GPUs (configs[4]).
 
-Prints ONE JSON line on rank 0.
+N > 1 runs one process per GPU.  The driver launches it under
+`torch.distributed.run`; a plain `python bench.py --gpus N` (no WORLD_SIZE in
+the environment) starts that launcher as a child process before touching the
+GPU and relays rank 0's line.  Prints ONE JSON line on stdout (rank 0); every
+other byte any rank or library writes goes to stderr.
 """
 
 from __future__ import annotations
@@ -22,6 +30,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -31,18 +41,21 @@ for _p in (ROOT, ROOT / "keras-geometric_amd"):
     if str(_p) not in sys.path:
         sys.path.insert(0, str(_p))
 
-import torch  # noqa: E402
+import torch  # noqa: E402  (importing torch does not initialise the GPU)
 import torch.distributed as dist  # noqa: E402
 
 METRIC = "aggregated edges/sec + achieved HBM GB/s, GCNConv fwd, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 
+# name: (layer, nodes, edges, F_in, F_out, scaling); weak: nodes/edges per GPU, strong: the whole graph
 CONFIGS = {
-    # name: (nodes per GPU, edges per GPU, F_in, F_out)
-    "ns": (10_000_000, 100_000_000, 128, 128),
-    "c2": (1_000_000, 10_000_000, 128, 128),
-    "tiny": (100_000, 1_000_000, 128, 128),
+    "ns": ("gcn", 10_000_000, 100_000_000, 128, 128, "weak"),
+    "c2": ("gcn", 1_000_000, 10_000_000, 128, 128, "weak"),
+    "tiny": ("gcn", 100_000, 1_000_000, 128, 128, "weak"),
+    "c4": ("gin", 10_000_000, 100_000_000, 256, 256, "strong"),
+    "c5": ("sage", 2_449_029, 123_718_280, 100, 100, "strong"),
 }
+LAYER_NAME = {"gcn": "GCNConv", "gin": "GINConv(sum)", "sage": "SAGEConv(mean)"}
 
 
 def b_alg_spmm(n: int, e_agg: int, f: int, weighted: bool, f_out: int | None = None) -> int:
@@ -74,14 +87,49 @@ def log(msg: str) -> None:
         print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def cpu_baseline(device: torch.device, seconds_hint: str) -> dict:
+def host_cpus() -> dict:
+    """The host's CPU model and counts (lscpu's fields, read from /proc and sysfs)."""
+    model, cores = None, set()
+    try:
+        phys = core = None
+        for line in open("/proc/cpuinfo"):
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "model name" and model is None:
+                model = v
+            elif k == "physical id":
+                phys = v
+            elif k == "core id":
+                core = v
+            elif not k and phys is not None:
+                cores.add((phys, core))
+                phys = core = None
+    except OSError:
+        pass
+    quota = None
+    try:  # cgroup v2 CPU quota ("max" = none)
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    return {"model": model, "os_cpu_count": os.cpu_count(), "physical_cores": len(cores) or None,
+            "affinity_cpus": affinity, "cgroup_cpu_quota": quota}
+
+
+def cpu_baseline(device: torch.device) -> dict:
     """Time the oracle's op-for-op Keras-torch CPU GCNConv forward (the reference's
-    CPU path) on a bounded sample: the C2-shaped 1M-node / 10M-edge R-MAT graph."""
+    CPU path) on a bounded sample: the C2-shaped 1M-node / 10M-edge R-MAT graph,
+    with every CPU this process may run on (os.cpu_count(), limited by its
+    affinity mask and cgroup quota when those are smaller)."""
     from keras_geometric_amd import synthetic
     from oracle import reference as R
 
     n, e, f = 1_000_000, 10_000_000, 128
-    threads = min(16, os.cpu_count() or 1)
+    info = host_cpus()
+    threads = max(1, min(v for v in (info["os_cpu_count"], info["affinity_cpus"],
+                                     int(info["cgroup_cpu_quota"] or 1 << 30)) if v))
     torch.set_num_threads(threads)
     ei = synthetic.rmat_edge_index(n, e, seed=0, device=device).cpu()
     g = torch.Generator().manual_seed(1)
@@ -97,10 +145,73 @@ def cpu_baseline(device: torch.device, seconds_hint: str) -> dict:
         "unit": "edges/s",
         "cores": threads,
         "kind": "port",
+        "host": info,
         "sample": f"oracle GCNConv fwd (Keras-torch CPU lowering, op for op) on R-MAT N={n} E={e} "
-                  f"(+{n} self loops) F {f}->{f}, 1 timed forward = {dt:.2f} s, torch threads={threads}"
-                  f"{seconds_hint}",
+                  f"(+{n} self loops) F {f}->{f}, 1 timed forward = {dt:.2f} s, torch threads={threads}",
     }
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(n_gpus: int) -> int:
+    """`python bench.py --gpus N` without a launcher: start torch.distributed.run
+    as a CHILD process (no GPU has been touched here), one rank per GPU, and
+    relay rank 0's JSON line to stdout."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n_gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(Path(__file__).resolve()),
+           *sys.argv[1:]]
+    print(f"[bench] launching {n_gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    proc = subprocess.run(cmd, stdout=subprocess.PIPE, env=env)
+    out = proc.stdout.decode(errors="replace").splitlines()
+    lines = [ln for ln in out if ln.startswith('{"metric"')]
+    for ln in out:
+        if ln not in lines:
+            print(ln, file=sys.stderr)
+    if lines:
+        print(lines[-1], flush=True)
+    elif proc.returncode == 0:
+        print("[bench] no result line from rank 0", file=sys.stderr)
+        return 1
+    return proc.returncode
+
+
+def _build_single(kind: str, n: int, e: int, f_in: int, f_out: int, seed: int, exact: bool, dev):
+    import keras_geometric_amd as kgx
+    from keras_geometric_amd import synthetic
+
+    log(f"generating R-MAT N={n} E={e}")
+    ei = synthetic.rmat_edge_index(n, e, seed=seed, device=dev)
+    x = torch.randn(n, f_in, device=dev)
+    if kind == "gcn":
+        layer = kgx.GCNConv(f_out, exact=exact)
+    elif kind == "gin":
+        layer = kgx.GINConv(f_out, aggregator="sum", exact=exact)
+    else:
+        layer = kgx.SAGEConv(f_out, aggregator="mean", exact=exact)
+    return ei, x, layer
+
+
+def _build_sharded(kind: str, n_global: int, e_global: int, f_in: int, f_out: int, seed: int, exact: bool,
+                   dev, comm):
+    from keras_geometric_amd import distributed as kd
+
+    gcn = kind == "gcn"
+    sg = kd.ShardedGraph.rmat(n_global, e_global, seed=seed, device=dev, comm=comm, self_loops=gcn,
+                              gcn_norm=gcn, exact=exact, n_features=f_in)
+    x = torch.randn(sg.n_local, f_in, device=dev)
+    if kind == "gcn":
+        layer = kd.ShardedGCNConv(f_out, sg)
+    elif kind == "gin":
+        layer = kd.ShardedGINConv(f_out, sg, aggregator="sum")
+    else:
+        layer = kd.ShardedSAGEConv(f_out, sg, aggregator="mean")
+    return sg, x, layer
 
 
 def main() -> None:
@@ -111,14 +222,24 @@ def main() -> None:
     ap.add_argument("--config", default="ns", choices=sorted(CONFIGS))
     ap.add_argument("--exact", action="store_true", help="EXACT mode (no hub split)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cold", action="store_true", help="skip the cold-graph layer timing")
     ap.add_argument("--seed", type=int, default=0)
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args.gpus))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}; launch N>1 with torch.distributed.run")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # stdout discipline: the one JSON line goes to the original stdout; anything
+    # a library prints (gloo/RCCL banners, warnings) lands on stderr
+    result_fd = os.dup(1) if rank == 0 else None
+    sys.stdout.flush()
+    os.dup2(2, 1)
+
     # KGX_BENCH_REHEARSAL=1 (test only, one-GPU box): all ranks share cuda:0 and
     # the exchange is staged through host memory over gloo -- exercises the N>1
     # control flow and halo plumbing where RCCL cannot run (one GPU); never a
@@ -136,60 +257,62 @@ def main() -> None:
             comm = HostStagedComm()
         else:
             dist.init_process_group("nccl", device_id=dev)
+        log(f"process group: backend={dist.get_backend()} world_size={dist.get_world_size()}")
 
     import keras_geometric_amd as kgx
     from keras_geometric_amd import ops as kops
-    from keras_geometric_amd import synthetic
 
-    n_local, e_local, f_in, f_out = CONFIGS[args.config]
+    kind, n_cfg, e_cfg, f_in, f_out, scaling = CONFIGS[args.config]
+    n_global, e_global = (n_cfg * world, e_cfg * world) if scaling == "weak" else (n_cfg, e_cfg)
     torch.manual_seed(args.seed + 17 * rank)
+    cold_ms = None
+    shard_info = {}
 
     if world == 1:
-        log(f"generating R-MAT N={n_local} E={e_local}")
-        ei = synthetic.rmat_edge_index(n_local, e_local, seed=args.seed, device=dev)
-        x = torch.randn(n_local, f_in, device=dev)
-        layer = kgx.GCNConv(f_out, exact=args.exact)
+        ei, x, layer = _build_single(kind, n_global, e_global, f_in, f_out, args.seed, args.exact, dev)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        layer([x, ei])  # build: weights + CSR + schedule (cached)
+        with torch.no_grad():
+            layer([x, ei])  # build: weights + CSR + schedule (cached)
         torch.cuda.synchronize()
         first_call_ms = (time.perf_counter() - t0) * 1e3
+        g = next(reversed(kgx.graph._CACHE.values()))[1]
         # steady-state graph preparation (CSR + schedule), timed warm: once per graph, not per step
         t0 = time.perf_counter()
-        kgx.graph.build_csr(ei[0].contiguous(), ei[1].contiguous(), n_local, n_local, self_loops=True,
-                            gcn_norm=True, n_features=f_out)
+        kgx.graph.build_csr(ei[0].contiguous(), ei[1].contiguous(), n_global, n_global, self_loops=kind == "gcn",
+                            gcn_norm=kind == "gcn", n_features=f_in)
         torch.cuda.synchronize()
         graph_build_ms = (time.perf_counter() - t0) * 1e3
-        g = next(iter(kgx.graph._CACHE.values()))[1]
         e_agg, n_rows, max_deg = g.kept, g.n_dst, g.max_degree
+
         def step():  # the forward (inference) pass: no autograd state kept
             with torch.no_grad():
                 return layer([x, ei])
-
-        shard_info = {}
     else:
-        from keras_geometric_amd import distributed as kd
-
-        log(f"world={world}: generating shards of R-MAT N={n_local * world} E={e_local * world}")
+        log(f"world={world}: generating shards of R-MAT N={n_global} E={e_global}")
         t0 = time.perf_counter()
-        sg = kd.ShardedGraph.rmat(n_local * world, e_local * world, seed=args.seed, device=dev, comm=comm,
-                                  self_loops=True, gcn_norm=True, exact=args.exact)
-        x = torch.randn(sg.n_local, f_in, device=dev)
-        layer = kd.ShardedGCNConv(f_out, sg)
-        layer(x)
+        sg, x, layer = _build_sharded(kind, n_global, e_global, f_in, f_out, args.seed, args.exact, dev, comm)
+        with torch.no_grad():
+            layer(x)  # build, plans, and (GCN) the halo chunk count measured at the first forward
         torch.cuda.synchronize()
         graph_build_ms = first_call_ms = (time.perf_counter() - t0) * 1e3  # incl. shard generation + halo plan
         e_agg, n_rows, max_deg = sg.graph.kept, sg.n_local, sg.graph.max_degree
+
         def step():
             with torch.no_grad():
                 return layer(x)
 
         pp = sg._pp  # push-pull halo plan of the default path (None: pull-only or EXACT)
         n_moved = pp.n_rows if pp is not None else sg.n_halo
-        shard_info = {"halo_rows_pull_only_per_rank": sg.n_halo, "halo_rows_per_rank": n_moved,
+        # exchanged row width: X rows (F_in) on the aggregate-first paths, X W rows
+        # (F_out) when the GCN layer transforms first (shapes the fused kernel does not take)
+        transform_first = kind == "gcn" and (args.exact or not kops.fused_transform_supported(f_in, f_out)
+                                             and f_out < f_in)
+        f_x = f_out if transform_first else f_in
+        shard_info = {"halo_rows_pull_only": sg.n_halo, "halo_rows": n_moved,
                       "halo_rows_pushed_partials": pp.n_push if pp is not None else 0,
-                      "halo_MB_per_layer": n_moved * f_in * 4 / 1e6,
-                      "halo_chunks": sg.halo_k if sg.halo_k is not None else len(sg.chunks),
+                      "halo_MB_per_layer": n_moved * f_x * 4 / 1e6,
+                      "halo_chunks": sg.halo_k if sg.halo_k is not None else (len(pp.chunks) if pp else len(sg.chunks)),
                       "halo_chunk_tuning_s": sg.tuning}
 
     for _ in range(args.warmup):
@@ -210,35 +333,60 @@ def main() -> None:
     elapsed = time.perf_counter() - t0
     events = kops.EVENT_SINK
     kops.EVENT_SINK = None
-    # kernel time per step (N>1 default path: own-source + halo-source launches)
+    # aggregation-kernel time per step (N>1: own-source + halo launches, which overlap)
     kern_ms = sum(s.elapsed_time(e) for s, e in events) / args.steps
     launches = len(events) // args.steps
 
+    fused = kind == "gcn" and not args.exact and kops.fused_transform_supported(f_in, f_out)
+    if kind == "gcn":
+        # SURVEY.md §8d per rank; at N>1 the accumulating halo-chunk passes' re-reads
+        # of the rows they add to are implementation overhead, not algorithmic bytes
+        balg = b_alg_spmm(n_rows, e_agg, f_in if fused else f_out, weighted=True, f_out=f_out)
+        kernel = "spmm_gemm_kernel" if fused else "spmm_kernel"
+    else:  # GIN: + the x_i root row of the (1+eps) x_i + aggr epilogue; SAGE mean: plain gather-sum
+        balg = b_alg_spmm(n_rows, e_agg, f_in, weighted=False) + (4 * n_rows * f_in if kind == "gin" else 0)
+        kernel = "spmm_kernel"
+    achieved = balg / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
+    mine = {"rank": rank, "e_agg": e_agg, "rows": n_rows, "ms_per_step": elapsed / args.steps * 1e3,
+            "aggregation_ms": kern_ms, "launches_per_step": launches, "roofline_achieved_GBps": achieved,
+            "roofline_frac": achieved / HBM_PEAK_GBS, **shard_info}
+
     if world > 1:
-        rdev = torch.device("cpu") if rehearsal else dev
-        t = torch.tensor([elapsed, kern_ms], device=rdev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
-        tot = torch.tensor([e_agg], device=rdev, dtype=torch.float64)
-        dist.all_reduce(tot)
-        e_total = float(tot[0])
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
+        elapsed = max(r["ms_per_step"] for r in ranks) * args.steps / 1e3
+        e_total = float(sum(r["e_agg"] for r in ranks))
     else:
+        ranks = None
         e_total = float(e_agg)
 
     ms_per_step = elapsed / args.steps * 1e3
     value = e_total * args.steps / elapsed
-    from keras_geometric_amd import ops as _ops
-
-    fused = not args.exact and _ops.fused_transform_supported(f_in, f_out)
-    # SURVEY.md §8d per rank; at N>1 the accumulating halo-chunk passes' re-reads
-    # of the rows they add to are implementation overhead, not algorithmic bytes
-    balg = b_alg_spmm(n_rows, e_agg, f_in if fused else f_out, weighted=True, f_out=f_out)
-    achieved = balg / (kern_ms * 1e-3) / 1e9
     traffic, traffic_src = (None, None)
     if world == 1:
-        traffic, traffic_src = pmc_traffic(args.config, "spmm_gemm_kernel" if fused else "spmm_kernel")
+        traffic, traffic_src = pmc_traffic(args.config, kernel)
+        if not args.no_cold:
+            # cold layer: CSR + (GCN) norm + schedule + forward from a fresh edge_index,
+            # what the reference pays on every call (utils/main.py:8-33 per call)
+            colds = []
+            for _ in range(3):
+                kgx.clear_cache()
+                ei_c = ei.clone()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                with torch.no_grad():
+                    layer([x, ei_c])
+                torch.cuda.synchronize()
+                colds.append((time.perf_counter() - t0) * 1e3)
+                del ei_c
+            cold_ms = sorted(colds)[1]
+    wl = f"{LAYER_NAME[kind]} fwd, R-MAT {n_global} nodes / {e_global} edges"
+    wl += " (+self loops), normalized, bias" if kind == "gcn" else ""
+    wl += f", F {f_in}->{f_out}"
+    if world > 1:
+        wl += ", dst-range shards, RCCL halo all-to-all pipelined under the own-source pass"
     result = {
-        "metric": METRIC,
+        "metric": METRIC if kind == "gcn" else f"aggregated edges/sec + achieved HBM GB/s, {LAYER_NAME[kind]} fwd",
         "value": value,
         "unit": "edges/s",
         "n_gpus": world,
@@ -246,31 +394,32 @@ def main() -> None:
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "fp32",
         "data": f"synthetic R-MAT (a,b,c=.57,.19,.19, seed {args.seed}), x~N(0,1), glorot weights",
         "config": {
-            "workload": f"GCNConv fwd (normalized, self loops, bias), R-MAT "
-                        f"{n_local * world} nodes / {e_local * world} edges (+self loops), "
-                        f"F {f_in}->{f_out}" + (", dst-range shards, RCCL halo all-to-all overlapped with the own-source part"
-                                                 if world > 1 else ""),
-            "nodes_per_gpu": n_local,
-            "edges_per_gpu": e_local,
+            "workload": wl,
+            "name": args.config,
+            "nodes": n_global,
+            "edges": e_global,
+            "nodes_per_gpu": n_rows,
             "e_agg_per_gpu": e_agg,
             "max_in_degree": max_deg,
             "features": [f_in, f_out],
-            "mode": ("exact" if args.exact else "split-hub") + (", fused aggregate->transform (W on bf16x3-split MFMA, f32-accurate)"
-                                                                 if fused else ", X.W GEMM then aggregate"),
+            "mode": ("exact" if args.exact else "split-hub")
+                    + (", fused aggregate->transform (W on bf16x3-split MFMA, f32-accurate)" if fused else ""),
             "parallelism": f"dst-shard{world}" if world > 1 else "single",
         },
-        "edges_per_s_aggregation_kernel": e_agg * world / (kern_ms * 1e-3),
+        "edges_per_s_aggregation_kernel": e_total / (kern_ms * 1e-3) if kern_ms > 0 else None,
         "aggregation_ms": kern_ms,
         "aggregation_launches_per_step": launches,
         "graph_build_ms": graph_build_ms,
         "first_call_ms": first_call_ms,
+        "cold_layer_ms": cold_ms,
         "roofline": {
             "bound": "hbm",
+            "kernel": kernel,
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -279,20 +428,20 @@ def main() -> None:
             "traffic_source": traffic_src,
             "algorithmic_bytes_per_launch": balg,
         },
-        **shard_info,
+        **({"per_rank": ranks} if ranks is not None else shard_info),
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "ns":
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and kind == "gcn" and args.config != "tiny":
         log("timing the CPU baseline (oracle, C2-sized sample)")
         del x, layer, ei
         kgx.clear_cache()
         torch.cuda.empty_cache()
-        result["cpu_baseline"] = cpu_baseline(dev, "")
+        result["cpu_baseline"] = cpu_baseline(dev)
     elif rank == 0:
         result["cpu_baseline"] = None
     if rehearsal:
         result["data"] += " [REHEARSAL: ranks share one GPU, host-staged gloo exchange -- not a measurement]"
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        os.write(result_fd, (json.dumps(result) + "\n").encode())
     if world > 1:
         dist.destroy_process_group()
 

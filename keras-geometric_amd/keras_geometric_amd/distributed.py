@@ -68,9 +68,9 @@ class KgxBackend:
     def gather_rows(self, table: torch.Tensor, rows: torch.Tensor) -> torch.Tensor:
         return kops.gather_rows(table, rows)
 
-    def transform(self, x: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
-        """Node-level x W (kgx_dense; the library GEMM past its shapes)."""
-        return kops.dense(x, W)
+    def transform(self, x: torch.Tensor, W: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
+        """Node-level x W (+ bias) (kgx_dense; the library GEMM past its shapes)."""
+        return kops.dense(x, W, bias)
 
     def split_by_source(self, g, cuts: list):
         """Parts of g by source range [cuts[k], cuts[k+1]); every part after the
@@ -138,6 +138,15 @@ class HostStagedComm(TorchComm):
         h = t.detach().cpu()
         dist.broadcast(h, src=src, group=self.group)
         t.copy_(h)
+
+
+def _inference_only(layer: Layer, weights) -> None:
+    """The sharded layers are a forward (inference) engine: their kernels run
+    under no_grad, so an output would carry no gradient to the weights."""
+    if torch.is_grad_enabled() and any(p.requires_grad for p in weights):
+        raise NotImplementedError(
+            f"{type(layer).__name__} is inference-only: call it under torch.no_grad() (or freeze its weights); "
+            "training runs on the single-GPU layers")
 
 
 def equal_bounds(n_global: int, world: int) -> list[int]:
@@ -355,7 +364,7 @@ class ShardedGraph:
             return self.backend.gather_rows(x_local, c.send_rows)
         return x_local.new_empty((0, x_local.shape[1]))
 
-    def push_pull_plan(self, n_chunks: int | None = None) -> PushPullPlan:
+    def push_pull_plan(self, n_chunks: int | None = None, weighted: bool | None = None) -> PushPullPlan:
         """A smaller halo for the weighted-sum (GCN) path.  Collective: every
         rank calls it once (ShardedGCNConv does, on its first forward).
 
@@ -372,12 +381,21 @@ class ShardedGraph:
         owner packs pulled rows and partials in one weighted-sum pass over a
         send CSR (a pulled row = one edge of weight 1, multiplied exactly).
         Row sums are re-associated (partials first), so this is a tolerance
-        path like the rest of the overlapped layer; EXACT mode keeps pulling."""
+        path like the rest of the overlapped layer; EXACT mode keeps pulling.
+
+        weighted (default: the graph carries edge weights) says whether the
+        receiver's pass multiplies by them: an unweighted plan (GIN / SAGE sums
+        on a graph that also has GCN norms) pushes plain partial sums and gives
+        every receiver edge weight 1, so the plans are kept per (K, weighted)."""
         K = n_chunks or self.halo_k or len(self.chunks)
+        if weighted is None:
+            weighted = self.graph.w is not None
+        if weighted and self.graph.w is None:
+            raise ValueError("push_pull_plan(weighted=True): the shard graph has no edge weights")
         if self._pp_by_k is None:
             self._pp_by_k = {}
-        if K in self._pp_by_k:
-            self._pp = self._pp_by_k[K]
+        if (K, weighted) in self._pp_by_k:
+            self._pp = self._pp_by_k[(K, weighted)]
             return self._pp
         g, comm, world, lo, n_local = self.graph, self.comm, self.world, self.lo, self.n_local
         dev = g.col.device
@@ -386,7 +404,7 @@ class ShardedGraph:
         halo = col >= n_local
         hs = self.halo_ids.long()[col[halo] - n_local]  # global source id per halo edge
         hd = rows[halo]
-        hw = g.w[halo] if g.w is not None else torch.ones(hd.numel(), dtype=torch.float32, device=dev)
+        hw = g.w[halo] if weighted else torch.ones(hd.numel(), dtype=torch.float32, device=dev)
         bt = torch.tensor(self.bounds[1:-1], dtype=torch.long, device=dev)
         us, inv_s, cs = torch.unique(hs, return_inverse=True, return_counts=True)
         stride = n_local + 1
@@ -479,7 +497,7 @@ class ShardedGraph:
             # a leading empty range makes every chunk part accumulate-only
             parts = list(self.backend.split_by_source(rg, [0, 0] + [c.hi for c in chunks])[1:])
         self._pp = PushPullPlan(chunks=chunks, parts=parts, n_rows=off, n_pull=rp[-1], n_push=ru[-1])
-        self._pp_by_k[K] = self._pp
+        self._pp_by_k[(K, weighted)] = self._pp
         return self._pp
 
     def tune_halo_chunks(self, run, candidates=(1, 2, 4, 8)) -> int:
@@ -588,7 +606,7 @@ class ShardedGraph:
             raise ValueError("propagate_overlapped: weights / bias go with a plain sum (the GCN layer)")
         x_local = x_local.contiguous()
         g_own, _ = self.own_halo_parts()
-        pp = self.push_pull_plan()
+        pp = self.push_pull_plan(weighted=weighted)
         halo = self.halo_buffer(x_local.shape[1], x_local, pp.n_rows)
         fold_gin = gin_scale is not None and reduce == "sum"
         with torch.no_grad():
@@ -647,16 +665,22 @@ class ShardedGCNConv(Layer):
         if not self.built:
             self._build_device = x_local.device
             self.build(tuple(x_local.shape))
+        _inference_only(self, self.weights)
         sg = self.sg
         use_b = self.use_bias and self.bias is not None
         if not sg.exact and sg.backend.supports_fused(x_local.shape[1], self.output_dim):
             return self._forward_overlapped(x_local, self.bias if use_b else None)
         if not sg.exact and use_push_pull() and sg.graph.w is not None:
-            # transform first (F_out < F_in: narrower rows to exchange), then the
-            # weighted sum with the push-pull halo pipelined under the own-source pass
+            # the weighted sum with the push-pull halo pipelined under the own-source
+            # pass, over the narrower of X (aggregate, then transform) and X W
+            # (transform first): those are the rows exchanged and gathered
             with torch.no_grad():
-                h = sg.backend.transform(x_local.contiguous(), self.kernel)
-                return sg.propagate_overlapped(h, "sum", weighted=True, bias=self.bias if use_b else None)
+                x_local = x_local.contiguous()
+                if self.output_dim < x_local.shape[1]:
+                    h = sg.backend.transform(x_local, self.kernel)
+                    return sg.propagate_overlapped(h, "sum", weighted=True, bias=self.bias if use_b else None)
+                agg = sg.propagate_overlapped(x_local, "sum", weighted=True)
+                return sg.backend.transform(agg, self.kernel, self.bias if use_b else None)
         table = sg.new_table(self.output_dim, x_local)
         with torch.no_grad():  # forward engine: X W written straight into the table's own-rows slice
             torch.matmul(x_local, self.kernel, out=table[: sg.n_local])
@@ -755,6 +779,7 @@ class ShardedGINConv(_ShardedWrap):
 
     def forward(self, x_local: torch.Tensor, training=None) -> torch.Tensor:
         self._ensure_built(x_local)
+        _inference_only(self, self.conv.weights)
         sg, conv = self.sg, self.conv
         x_local = x_local.contiguous()
         with torch.no_grad():
@@ -779,6 +804,7 @@ class ShardedSAGEConv(_ShardedWrap):
 
     def forward(self, x_local: torch.Tensor, training=None) -> torch.Tensor:
         self._ensure_built(x_local)
+        _inference_only(self, self.conv.weights)
         sg, conv = self.sg, self.conv
         x_local = x_local.contiguous()
         with torch.no_grad():

@@ -60,8 +60,9 @@ class OracleBackend:
         out += self.aggregate(g, table, "sum", weighted=weighted)
         return out
 
-    def transform(self, x, W):
-        return torch.matmul(x, W)
+    def transform(self, x, W, bias=None):
+        y = torch.matmul(x, W)
+        return y if bias is None else K.add(y, bias)
 
     def supports_fused(self, f_in, f_out):
         return True
@@ -101,6 +102,15 @@ def _free_port():
 
 
 N, E, F_IN, F_OUT = 1000, 12000, 16, 8
+
+
+F_WIDE = 24  # F_out > F_in: the unfused sharded GCN aggregates X first
+
+
+def _wide_weights():
+    rng = np.random.default_rng(7)
+    return (rng.standard_normal((F_IN, F_WIDE)) * 0.3).astype(np.float32), \
+        rng.standard_normal(F_WIDE).astype(np.float32)
 
 
 def _graph():
@@ -153,12 +163,16 @@ def _worker(rank, world, chunks, port, q):
         with torch.no_grad():
             layer.kernel.copy_(torch.from_numpy(W))
             layer.bias.copy_(torch.from_numpy(b))
-        y = layer(torch.from_numpy(x[lo:hi])).detach()  # push-pull halo (the default)
+        with pytest.raises(NotImplementedError):  # inference-only: grad mode with trainable weights
+            layer(torch.from_numpy(x[lo:hi]))
+        with torch.no_grad():
+            y = layer(torch.from_numpy(x[lo:hi]))  # push-pull halo (the default)
         pp = sg._pp
         assert pp is not None and pp.n_rows == pp.n_pull + pp.n_push == pp.chunks[-1].hi
         os.environ["KGX_HALO_PUSH"] = "0"
         try:
-            y_pull = layer(torch.from_numpy(x[lo:hi])).detach()  # pull-only halo
+            with torch.no_grad():
+                y_pull = layer(torch.from_numpy(x[lo:hi]))  # pull-only halo
         finally:
             del os.environ["KGX_HALO_PUSH"]
         # K left open: the first forward times K = 1 / 2 / 4 / 8 (collective) and keeps the fastest
@@ -170,7 +184,8 @@ def _worker(rank, world, chunks, port, q):
         with torch.no_grad():
             layer2.kernel.copy_(torch.from_numpy(W))
             layer2.bias.copy_(torch.from_numpy(b))
-        y_tuned = layer2(torch.from_numpy(x[lo:hi])).detach()
+        with torch.no_grad():
+            y_tuned = layer2(torch.from_numpy(x[lo:hi]))
         assert sorted(sg2.tuning) == [1, 2, 4, 8] and sg2.halo_k in (1, 2, 4, 8)
         assert len(sg2._pp.chunks) == sg2.halo_k
         # shapes the fused kernel does not take: X W first, then the pipelined weighted sum
@@ -182,10 +197,32 @@ def _worker(rank, world, chunks, port, q):
         with torch.no_grad():
             layer3.kernel.copy_(torch.from_numpy(W))
             layer3.bias.copy_(torch.from_numpy(b))
-        y_unfused = layer3(torch.from_numpy(x[lo:hi])).detach()
+        with torch.no_grad():
+            y_unfused = layer3(torch.from_numpy(x[lo:hi]))
         assert sg3._pp is not None
+        # F_out > F_in on the unfused path: aggregate X first (narrower rows), then X W + b
+        W2, b2 = _wide_weights()
+        layer4 = kd.ShardedGCNConv(F_WIDE, sg3)
+        layer4._build_device = torch.device("cpu")
+        layer4.build((hi - lo, F_IN))
+        with torch.no_grad():
+            layer4.kernel.copy_(torch.from_numpy(W2))
+            layer4.bias.copy_(torch.from_numpy(b2))
+            y_wide = layer4(torch.from_numpy(x[lo:hi]))
+        # an unweighted sum / mean over a GCN-normed shard graph: the push-pull plan
+        # must push plain partial sums (plans are kept per (K, weighted))
+        xl = torch.from_numpy(x[lo:hi])
+        mean_pp = sg.propagate_overlapped(xl, "mean")
+        sum_pp = sg.propagate_overlapped(xl, "sum")
+        mean_tab, sum_tab = sg.propagate(xl, "mean"), sg.propagate(xl, "sum")
+        scale = sg.propagate(xl.abs(), "sum")
+        assert (mean_pp - mean_tab).abs().max() <= 1e-5 * max(1.0, float(scale.max()))
+        assert ((sum_pp - sum_tab).abs() <= 1e-5 * scale.clamp_min(1)).all()
+        with torch.no_grad():
+            y_again = layer(xl)  # the weighted plan is still the one the GCN layer uses
+        assert torch.equal(y_again, y)
         q.put((rank, gcn.numpy(), mx.numpy(), sg.n_halo, sum(sg.send_counts), y.numpy(), y_pull.numpy(), pp.n_push,
-               y_tuned.numpy(), y_unfused.numpy()))
+               y_tuned.numpy(), y_unfused.numpy(), y_wide.numpy()))
     finally:
         dist.destroy_process_group()
 
@@ -207,8 +244,8 @@ def test_sharded_equals_unsharded_bitwise(world, chunks):
         p.start()
     results = {}
     for _ in range(world):
-        rank, gcn, mx, n_halo, n_send, y_split, y_pull, n_push, y_tuned, y_unfused = q.get(timeout=90)
-        results[rank] = (gcn, mx, n_halo, n_send, y_split, y_pull, n_push, y_tuned, y_unfused)
+        rank, *res = q.get(timeout=90)
+        results[rank] = res
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -231,6 +268,11 @@ def test_sharded_equals_unsharded_bitwise(world, chunks):
         y_split = np.concatenate([results[r][i] for r in range(world)])
         err = np.abs(y_split - y) / np.maximum(1, np.abs(y))
         assert err.max() <= 1e-5
+    W2, b2 = _wide_weights()
+    y2 = R.gcn_forward(torch.from_numpy(x), torch.from_numpy(np.stack([s, d])), torch.from_numpy(W2),
+                       torch.from_numpy(b2)).numpy()
+    got = np.concatenate([results[r][9] for r in range(world)])
+    assert (np.abs(got - y2) / np.maximum(1, np.abs(y2))).max() <= 1e-5
 
 
 
@@ -252,7 +294,8 @@ def _conv_worker(rank, world, port, q):
                       kd.ShardedSAGEConv(F_OUT, sg, aggregator="mean", normalize=True),
                       kd.ShardedSAGEConv(F_OUT, sg, aggregator="pooling", pool_hidden_dim=10)):
             layer._ensure_built(xl)  # weights drawn per rank, then broadcast from rank 0
-            outs.append((layer(xl).numpy(), list(layer.conv.get_weights())))
+            with torch.no_grad():
+                outs.append((layer(xl).numpy(), list(layer.conv.get_weights())))
         q.put((rank, outs))
     finally:
         dist.destroy_process_group()
@@ -325,12 +368,14 @@ def _local_only_worker(rank, world, port, q):
         with torch.no_grad():
             layer.kernel.copy_(torch.from_numpy(W))
             layer.bias.copy_(torch.from_numpy(b))
-        y = layer(torch.from_numpy(x[lo:hi])).detach()
+        with torch.no_grad():
+            y = layer(torch.from_numpy(x[lo:hi]))
         gsg = kd.ShardedGraph.build(torch.from_numpy(s[keep]), torch.from_numpy(d[keep]), bounds,
                                     backend=OracleBackend(), n_features=F_IN, self_loops=False, gcn_norm=False)
         gin = kd.ShardedGINConv(F_OUT, gsg, aggregator="sum", eps_init=0.5)
         gin._ensure_built(torch.from_numpy(x[lo:hi]))
-        h = gin(torch.from_numpy(x[lo:hi]))
+        with torch.no_grad():
+            h = gin(torch.from_numpy(x[lo:hi]))
         q.put((rank, sg.n_halo, sg._pp.n_rows, y.numpy(), h.numpy(), [a for a in gin.conv.get_weights()]))
     finally:
         dist.destroy_process_group()

@@ -63,6 +63,63 @@ class ThreadComm(kd.TorchComm):
         self.hub.barrier.wait()
 
 
+class AsyncThreadComm(ThreadComm):
+    """all_to_all_start with RCCL's stream semantics: the copy runs on this
+    rank's own copy stream after the send rows are ready (an event on every
+    rank's calling stream), the peers' send buffers are recorded on that stream
+    (as ProcessGroupNCCL does) and wait() makes the then-current stream wait for
+    the copy.  delay_cycles > 0 spins the copy stream first, so a missing
+    wait(), a missing wait_stream or a reused send / halo buffer reads rows
+    that have not landed and the result comes out wrong."""
+
+    def __init__(self, hub, rank, delay_cycles=0):
+        super().__init__(hub, rank)
+        self.delay = delay_cycles
+        self.copy_stream = None
+        self.started = 0
+
+    def all_to_all_start(self, out, inp, out_splits=None, in_splits=None):
+        w = self.hub.world
+        if self.copy_stream is None:
+            self.copy_stream = torch.cuda.Stream(device=inp.device)
+        in_splits = list(in_splits or [inp.shape[0] // w] * w)
+        out_splits = list(out_splits or [out.shape[0] // w] * w)
+        ready = torch.cuda.Event()
+        ready.record()  # on the caller's current stream: the packed send rows
+        self.hub.slots[self.r] = (torch.split(inp, in_splits), ready)
+        self.hub.barrier.wait()
+        peers = list(self.hub.slots)
+        self.hub.barrier.wait()
+        cs = self.copy_stream
+        for _, ev in peers:
+            cs.wait_event(ev)
+        with torch.cuda.stream(cs):
+            if self.delay:
+                torch.cuda._sleep(self.delay)
+            off = 0
+            for p, (parts, _) in enumerate(peers):
+                src = parts[self.r]
+                src.record_stream(cs)
+                if src.numel():
+                    out[off: off + out_splits[p]].copy_(src)
+                off += out_splits[p]
+        out.record_stream(cs)
+        done = torch.cuda.Event()
+        done.record(cs)
+        self.started += 1
+
+        class Work:
+            def wait(self_inner):
+                torch.cuda.current_stream().wait_event(done)
+
+        return Work()
+
+
+COMMS = {"sync": lambda hub, r: ThreadComm(hub, r),
+         "async": lambda hub, r: AsyncThreadComm(hub, r),
+         "async_delayed": lambda hub, r: AsyncThreadComm(hub, r, delay_cycles=20_000_000)}
+
+
 def _run_rank(rank, hub, dev, x, out):
     try:
         comm = ThreadComm(hub, rank)
@@ -71,9 +128,10 @@ def _run_rank(rank, hub, dev, x, out):
         s = sg.propagate(xl, "sum")
         m = sg.propagate(xl, "max")
         layer = kd.ShardedGCNConv(32, sg)
-        y = layer(xl)
-        sg.exact = False  # default path (F = 64, unfused): X W, then the push-pull halo pipelined under the own pass
-        y2 = layer(xl)
+        with torch.no_grad():
+            y = layer(xl)
+            sg.exact = False  # default path (F = 64, unfused): X W, then the push-pull halo pipelined under the own pass
+            y2 = layer(xl)
         torch.cuda.synchronize()
         out[rank] = (s.cpu().numpy(), m.cpu().numpy(), y.detach().cpu().numpy(), layer.kernel.detach().cpu().numpy(),
                      sg.n_halo, y2.detach().cpu().numpy())
@@ -121,13 +179,22 @@ def test_sharded_hip_equals_single_gpu(world, dev):
 F_FUSED = 128  # the fused aggregate->transform kernel's F_in: the default (chunk-pipelined) GCN path
 
 
-def _run_fused_rank(rank, hub, dev, x, chunks, out):
+def _run_fused_rank(rank, hub, dev, x, chunks, out, comm_kind="sync"):
     try:
-        comm = ThreadComm(hub, rank)
+        comm = COMMS[comm_kind](hub, rank)
         sg = kd.ShardedGraph.rmat(N, E, seed=8, device=dev, comm=comm, n_features=F_FUSED, halo_chunks=chunks)
         xl = x[sg.lo: sg.lo + sg.n_local]
         layer = kd.ShardedGCNConv(128, sg)  # F_out >= F_in = 128: the fused, chunk-pipelined path
-        y = layer(xl)
+        with torch.no_grad():
+            y = layer(xl)
+            if comm_kind != "sync":  # forwards back to back reuse the persistent halo buffer
+                y_next = layer(xl)
+                x_other = torch.randn_like(xl)
+                layer(x_other)  # different rows in flight through the same buffers
+                y_last = layer(xl)
+                torch.cuda.synchronize()
+                assert torch.equal(y_next, y) and torch.equal(y_last, y), "halo buffer reuse across forwards"
+                assert comm.started > 0
         torch.cuda.synchronize()
         assert (sg._pp is not None) == kd.use_push_pull()
         g_own, g_chunks = sg.own_halo_parts()
@@ -143,8 +210,11 @@ def _run_fused_rank(rank, hub, dev, x, chunks, out):
         hub.barrier.abort()
 
 
-@pytest.mark.parametrize("world,chunks,push", [(2, 1, "1"), (2, 4, "1"), (3, 3, "1"), (2, 4, "0")])
-def test_sharded_gcn_chunked_halo_pipeline(world, chunks, push, dev, monkeypatch):
+@pytest.mark.parametrize("world,chunks,push,comm", [(2, 1, "1", "sync"), (2, 4, "1", "sync"), (3, 3, "1", "sync"),
+                                                    (2, 4, "0", "sync"), (2, 1, "1", "async_delayed"),
+                                                    (2, 4, "1", "async_delayed"), (3, 3, "1", "async"),
+                                                    (2, 4, "0", "async_delayed")])
+def test_sharded_gcn_chunked_halo_pipeline(world, chunks, push, comm, dev, monkeypatch):
     """The default multi-GPU GCN path on the HIP kernels: owners pack pulled
     rows and pushed partial sums in one weighted-sum pass (push="1"; "0":
     pull-only halo), the own-source fused pass runs, then one accumulating
@@ -158,7 +228,8 @@ def test_sharded_gcn_chunked_halo_pipeline(world, chunks, push, dev, monkeypatch
     x = torch.randn(N, F_FUSED, generator=torch.Generator().manual_seed(2)).to(dev)
     hub = ThreadHub(world)
     res = {}
-    threads = [threading.Thread(target=_run_fused_rank, args=(r, hub, dev, x, chunks, res)) for r in range(world)]
+    threads = [threading.Thread(target=_run_fused_rank, args=(r, hub, dev, x, chunks, res, comm))
+               for r in range(world)]
     for t in threads:
         t.start()
     for t in threads:
@@ -188,7 +259,8 @@ def _run_conv_rank(rank, hub, dev, x, out):
         for layer in (kd.ShardedGINConv(32, sg, mlp_hidden=[48], aggregator="sum", eps_init=0.5),
                       kd.ShardedSAGEConv(32, sg, aggregator="mean"),
                       kd.ShardedSAGEConv(32, sg, aggregator="max", normalize=True)):
-            y = layer(xl)
+            with torch.no_grad():
+                y = layer(xl)
             torch.cuda.synchronize()
             res.append((y.cpu().numpy(), layer.conv.get_weights()))
         out[rank] = res
@@ -228,9 +300,9 @@ def test_sharded_gin_sage_hip(dev):
         assert err.max() <= 1e-5, (i, err.max())
 
 
-def _run_pipelined_rank(rank, hub, dev, x, out):
+def _run_pipelined_rank(rank, hub, dev, x, out, comm_kind="sync"):
     try:
-        comm = ThreadComm(hub, rank)
+        comm = COMMS[comm_kind](hub, rank)
         sg = kd.ShardedGraph.rmat(N, E, seed=9, device=dev, comm=comm, n_features=F, self_loops=False,
                                   gcn_norm=False)
         xl = x[sg.lo: sg.lo + sg.n_local]
@@ -238,7 +310,11 @@ def _run_pipelined_rank(rank, hub, dev, x, out):
         for layer in (kd.ShardedGINConv(32, sg, mlp_hidden=[48], aggregator="sum", eps_init=0.5),
                       kd.ShardedGINConv(32, sg, aggregator="mean", eps_init=0.25),
                       kd.ShardedSAGEConv(32, sg, aggregator="mean")):
-            y = layer(xl)
+            with torch.no_grad():
+                y = layer(xl)
+                if comm_kind != "sync":
+                    layer(torch.randn_like(xl))  # other rows through the same halo buffer
+                    assert torch.equal(layer(xl), y), "halo buffer reuse across forwards"
             torch.cuda.synchronize()
             res.append((y.cpu().numpy(), layer.conv.get_weights()))
         out[rank] = (res, sg._pp.n_push, len(sg._pp.chunks))
@@ -247,7 +323,8 @@ def _run_pipelined_rank(rank, hub, dev, x, out):
         hub.barrier.abort()
 
 
-def test_sharded_gin_sage_pipelined_hip(dev):
+@pytest.mark.parametrize("comm", ["sync", "async_delayed"])
+def test_sharded_gin_sage_pipelined_hip(comm, dev):
     """Sharded GIN (sum, mean) and SAGE (mean) on the default path: push-pull
     halo in chunks, own-source kgx_spmm pass, then KGX_EPI_ACCUM passes per
     landed chunk.  Equal to the single-GPU layers within the forward-error
@@ -259,7 +336,7 @@ def test_sharded_gin_sage_pipelined_hip(dev):
     x = torch.randn(N, F, generator=torch.Generator().manual_seed(3)).to(dev)
     hub = ThreadHub(world)
     res = {}
-    threads = [threading.Thread(target=_run_pipelined_rank, args=(r, hub, dev, x, res)) for r in range(world)]
+    threads = [threading.Thread(target=_run_pipelined_rank, args=(r, hub, dev, x, res, comm)) for r in range(world)]
     for t in threads:
         t.start()
     for t in threads:
@@ -295,7 +372,8 @@ def _run_no_halo_rank(rank, hub, dev, s, d, x, out):
         sg = kd.ShardedGraph.build(torch.from_numpy(s[keep]).to(dev), torch.from_numpy(d[keep]).to(dev), bounds,
                                    comm=comm, n_features=F_FUSED)
         layer = kd.ShardedGCNConv(128, sg)
-        y = layer(x[lo:hi])
+        with torch.no_grad():
+            y = layer(x[lo:hi])
         torch.cuda.synchronize()
         out[rank] = (y.detach().cpu().numpy(), layer.kernel.detach().cpu().numpy(), sg.n_halo, sg._pp.n_rows,
                      sg.halo_k)
