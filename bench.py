@@ -52,10 +52,12 @@ CONFIGS = {
     "ns": ("gcn", 10_000_000, 100_000_000, 128, 128, "weak"),
     "c2": ("gcn", 1_000_000, 10_000_000, 128, 128, "weak"),
     "tiny": ("gcn", 100_000, 1_000_000, 128, 128, "weak"),
+    "c3": ("gat", 1_000_000, 10_000_000, 128, 128, "weak"),
     "c4": ("gin", 10_000_000, 100_000_000, 256, 256, "strong"),
     "c5": ("sage", 2_449_029, 123_718_280, 100, 100, "strong"),
 }
-LAYER_NAME = {"gcn": "GCNConv", "gin": "GINConv(sum)", "sage": "SAGEConv(mean)"}
+LAYER_NAME = {"gcn": "GCNConv", "gin": "GINConv(sum)", "sage": "SAGEConv(mean)", "gat": "GATv2Conv(8 heads x 16)"}
+GAT_HEADS = 8
 
 
 def b_alg_spmm(n: int, e_agg: int, f: int, weighted: bool, f_out: int | None = None) -> int:
@@ -192,6 +194,8 @@ def _build_single(kind: str, n: int, e: int, f_in: int, f_out: int, seed: int, e
         layer = kgx.GCNConv(f_out, exact=exact)
     elif kind == "gin":
         layer = kgx.GINConv(f_out, aggregator="sum", exact=exact)
+    elif kind == "gat":
+        layer = kgx.GATv2Conv(f_out // GAT_HEADS, heads=GAT_HEADS, exact=exact)
     else:
         layer = kgx.SAGEConv(f_out, aggregator="mean", exact=exact)
     return ei, x, layer
@@ -201,6 +205,8 @@ def _build_sharded(kind: str, n_global: int, e_global: int, f_in: int, f_out: in
                    dev, comm):
     from keras_geometric_amd import distributed as kd
 
+    if kind == "gat":
+        raise SystemExit("--config c3 (GATv2) is a one-GPU config (BASELINE.json configs[2])")
     gcn = kind == "gcn"
     sg = kd.ShardedGraph.rmat(n_global, e_global, seed=seed, device=dev, comm=comm, self_loops=gcn,
                               gcn_norm=gcn, exact=exact, n_features=f_in)
@@ -279,8 +285,8 @@ def main() -> None:
         g = next(reversed(kgx.graph._CACHE.values()))[1]
         # steady-state graph preparation (CSR + schedule), timed warm: once per graph, not per step
         t0 = time.perf_counter()
-        kgx.graph.build_csr(ei[0].contiguous(), ei[1].contiguous(), n_global, n_global, self_loops=kind == "gcn",
-                            gcn_norm=kind == "gcn", n_features=f_in)
+        kgx.graph.build_csr(ei[0].contiguous(), ei[1].contiguous(), n_global, n_global,
+                            self_loops=kind in ("gcn", "gat"), gcn_norm=kind == "gcn", n_features=f_in)
         torch.cuda.synchronize()
         graph_build_ms = (time.perf_counter() - t0) * 1e3
         e_agg, n_rows, max_deg = g.kept, g.n_dst, g.max_degree
@@ -343,6 +349,9 @@ def main() -> None:
         # of the rows they add to are implementation overhead, not algorithmic bytes
         balg = b_alg_spmm(n_rows, e_agg, f_in if fused else f_out, weighted=True, f_out=f_out)
         kernel = "spmm_gemm_kernel" if fused else "spmm_kernel"
+    elif kind == "gat":  # one pass: h_src row per edge, h_dst row + output row per node
+        balg = 4 * (n_rows + 1) + e_agg * (4 + 4 * f_out) + 8 * n_rows * f_out
+        kernel = "gatv2_kernel"
     else:  # GIN: + the x_i root row of the (1+eps) x_i + aggr epilogue; SAGE mean: plain gather-sum
         balg = b_alg_spmm(n_rows, e_agg, f_in, weighted=False) + (4 * n_rows * f_in if kind == "gin" else 0)
         kernel = "spmm_kernel"

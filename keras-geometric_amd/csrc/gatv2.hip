@@ -218,20 +218,42 @@ __global__ __launch_bounds__(kBlock) void gatv2_fixup_kernel(GatArgs a) {
     if (!valid) continue;
     const int4 sp = a.split[it];
     const int32_t row = sp.x, slot0 = sp.y, nc = sp.z;
+    // One pass over the chunk partials, B chunks' loads in flight per step
+    // (clamped, unconditional), the running max rescaled online as in the main
+    // kernel: a hub row's ~160 partials cost ~10 load latencies, not ~320.
+    constexpr int B = 16;
+    const int64_t ld_p = HC + 2 * a.H;
     float M = -__builtin_inff();
-    for (int32_t c = 0; c < nc; ++c)
-      M = fmaxf(M, a.partials[int64_t(slot0 + c) * (HC + 2 * a.H) + HC + head]);
     double L = 0.0, acc[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) acc[k] = 0.0;
-    for (int32_t c = 0; c < nc; ++c) {
-      const float* p = a.partials + int64_t(slot0 + c) * (HC + 2 * a.H);
-      const double sc = double(expf(p[HC + head] - M));
-      L += double(p[HC + a.H + head]) * sc;
-      float v[K];
-      vload<K>(v, p + f);
+    for (int32_t c0 = 0; c0 < nc; c0 += B) {
+      float mv[B], lv[B], v[B][K];
 #pragma unroll
-      for (int k = 0; k < K; ++k) acc[k] += double(v[k]) * sc;
+      for (int u = 0; u < B; ++u) {
+        const float* p = a.partials + int64_t(slot0 + (c0 + u < nc ? c0 + u : nc - 1)) * ld_p;
+        mv[u] = p[HC + head];
+        lv[u] = p[HC + a.H + head];
+        vload<K>(v[u], p + f);
+      }
+      float mb = M;
+#pragma unroll
+      for (int u = 0; u < B; ++u) mb = fmaxf(mb, mv[u]);  // clamped repeats leave the max unchanged
+      if (mb > M) {
+        const double r = double(expf(M - mb));
+        L *= r;
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc[k] *= r;
+        M = mb;
+      }
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const bool in = c0 + u < nc;  // clamped repeats add nothing (selected, not multiplied by 0: inf rows stay inf)
+        const double sc = double(expf(mv[u] - M));
+        L = in ? L + double(lv[u]) * sc : L;
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc[k] = in ? acc[k] + double(v[u][k]) * sc : acc[k];
+      }
     }
     const double den = L + 1e-10;
     if (a.stats && sub == 0) {
@@ -603,7 +625,14 @@ __global__ __launch_bounds__(kBlock) void gatv2_bwd_fixup_kernel(const int4* __r
     const int4 sp = split[it];
     for (int f = lane; f < HC; f += G) {
       float acc = 0.0f;
-      for (int32_t c = 0; c < sp.z; ++c) acc += partials[int64_t(sp.y + c) * HC + f];
+      constexpr int B = 8;  // chunk loads in flight, then the in-order sum
+      for (int32_t c0 = 0; c0 < sp.z; c0 += B) {
+        float v[B];
+#pragma unroll
+        for (int u = 0; u < B; ++u) v[u] = partials[int64_t(sp.y + (c0 + u < sp.z ? c0 + u : sp.z - 1)) * HC + f];
+#pragma unroll
+        for (int u = 0; u < B; ++u) acc = c0 + u < sp.z ? acc + v[u] : acc;
+      }
       out[int64_t(sp.x) * ld_out + f] = acc;
     }
   }

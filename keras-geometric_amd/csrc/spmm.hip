@@ -66,6 +66,8 @@ struct SpmmArgs {
 // row of 10^5 edges is a latency chain; rows this long get their own kernel
 // with 32 gathers in flight per group instead of 6.
 constexpr int kLongRow = 2048;
+// split-row partials loaded together by the fix-up kernels
+constexpr int kFixB = 8;
 
 template <int RED>
 struct Reducer {
@@ -293,11 +295,17 @@ __global__ __launch_bounds__(kBlock) void spmm_fixup_kernel(SpmmArgs a) {
       float acc[VEC];
 #pragma unroll
       for (int k = 0; k < VEC; ++k) acc[k] = R::init();
-      for (int32_t c = 0; c < nc; ++c) {
-        float p[VEC];
-        vload<VEC>(p, a.partials + int64_t(slot0 + c) * a.ld_p + f);
+      // kFixB chunk loads in flight (clamped, unconditional), then the in-order
+      // combine: a hub row's chain of ~100 partials is not ~100 serial latencies
+      for (int32_t c0 = 0; c0 < nc; c0 += kFixB) {
+        float p[kFixB][VEC];
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) acc[k] = R::combine(acc[k], p[k]);
+        for (int u = 0; u < kFixB; ++u)
+          vload<VEC>(p[u], a.partials + int64_t(slot0 + (c0 + u < nc ? c0 + u : nc - 1)) * a.ld_p + f);
+#pragma unroll
+        for (int u = 0; u < kFixB; ++u)
+#pragma unroll
+          for (int k = 0; k < VEC; ++k) acc[k] = c0 + u < nc ? R::combine(acc[k], p[u][k]) : acc[k];
       }
 #pragma unroll
       for (int k = 0; k < VEC; ++k) acc[k] = a.epi == KGX_EPI_RAW ? R::finish_raw(acc[k], deg) : R::finish(acc[k], deg);

@@ -401,11 +401,15 @@ __global__ __launch_bounds__(256) void spmm_gemm_fixup_kernel(FusedArgs a) {
       float acc[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) acc[k] = R::init();
-      for (int32_t c = 0; c < s.z; ++c) {
-        float p[4];
-        vload<4>(p, a.partials + int64_t(s.y + c) * kFin + lane * 4);
+      constexpr int B = 8;  // chunk loads in flight, then the in-order combine
+      for (int32_t c0 = 0; c0 < s.z; c0 += B) {
+        float p[B][4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) acc[k] = R::combine(acc[k], p[k]);
+        for (int u = 0; u < B; ++u) vload<4>(p[u], a.partials + int64_t(s.y + (c0 + u < s.z ? c0 + u : s.z - 1)) * kFin + lane * 4);
+#pragma unroll
+        for (int u = 0; u < B; ++u)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) acc[k] = c0 + u < s.z ? R::combine(acc[k], p[u][k]) : acc[k];
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) acc[k] = R::finish(acc[k], s.w);
