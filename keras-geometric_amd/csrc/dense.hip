@@ -65,7 +65,8 @@ struct DenseArgs {
   int relu;
   int accumulate;
   int cg_count;  // column groups of 16 WAVES columns (1 or 2)
-  int debug;     // experiment builds only (-DKGX_EXPERIMENTS, env KGX_DENSE_DEBUG): 1 skip MFMA, 2 skip stores
+  int vec_out;   // N, ld_out multiples of 4 and out 16-byte aligned: dwordx4 output stores
+  int debug;     // experiment builds only (-DKGX_EXPERIMENTS, env KGX_DENSE_DEBUG): 1 skip MFMA, 2 skip stores, 4 skip loads + split
 };
 
 template <int KS>
@@ -140,7 +141,12 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
     // K 256, 8 x 16 KB at K 128; half with two operands, whose sets take
     // twice the registers).  The loads are latency-bound, not bandwidth-bound,
     // below that: 64 KB per CU measured 3 TB/s.
-    constexpr int NSETS_ = (32 / KS < 2 ? 2 : (32 / KS > 8 ? 8 : 32 / KS));
+#ifdef KGX_DENSE_NSETS  // experiment knob
+    constexpr int NSETS_ = KS == 8 ? KGX_DENSE_NSETS : (32 / KS < 2 ? 2 : (32 / KS > 8 ? 8 : 32 / KS));
+#else
+    // K 256: three sets (four spilled address registers once the split took fewer VALU but more live values)
+    constexpr int NSETS_ = KS == 8 ? 3 : (32 / KS < 2 ? 2 : (32 / KS > 8 ? 8 : 32 / KS));
+#endif
     constexpr int NSETS = TWO ? (NSETS_ / 2 < 2 ? 2 : NSETS_ / 2) : NSETS_;
     const int ptid = tid - 64 * WAVES;
     const int kk = 4 * (ptid % G::F4_PER_ROW);
@@ -190,6 +196,35 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
       }
     };
     auto stage = [&](const f32x4(&p)[NL], const f32x4(&q)[NL], int buf) {
+#ifndef KGX_DENSE_OLD_SPLIT
+      // fast path: paired conversions (split3_pair_rn, ~4.5 VALU per element:
+      // the producer's split must fit in the issue slots the consumers' MFMAs
+      // leave free on its SIMD).  chk = sum of 2x over the thread's slots is
+      // finite iff no element is inf / NaN or >= 2^127 (where bf16(x) could
+      // round to inf); otherwise the slots are redone with split3_a_lo below.
+      float chk0 = 0.0f, chk1 = 0.0f;
+#pragma unroll
+      for (int j = 0; j < NL; ++j) {
+        const int row = srow0 + j * RSTEP;
+        f32x4 x = p[j];
+        if constexpr (TWO)
+          x = __builtin_bit_cast(f32x4, __builtin_bit_cast(u32x4, p[j]) | __builtin_bit_cast(u32x4, q[j]));
+        chk0 = fmaf(x[0], 2.0f, chk0);
+        chk1 = fmaf(x[1], 2.0f, chk1);
+        chk0 = fmaf(x[2], 2.0f, chk0);
+        chk1 = fmaf(x[3], 2.0f, chk1);
+        uint32_t h0, m0, l0, h1, m1, l1;
+        split3_pair_rn(x[0], x[1], h0, m0, l0);
+        split3_pair_rn(x[2], x[3], h1, m1, l1);
+        *reinterpret_cast<uint2*>(&As[buf][0][row][kk]) = make_uint2(h0, h1);
+        *reinterpret_cast<uint2*>(&As[buf][1][row][kk]) = make_uint2(m0, m1);
+        *reinterpret_cast<uint2*>(&As[buf][2][row][kk]) = make_uint2(l0, l1);
+      }
+#ifdef KGX_DENSE_NO_SLOW  // experiment only: no inf/NaN path (wrong for non-finite inputs)
+      return;
+#endif
+      if (__builtin_expect(__builtin_isfinite(chk0 + chk1), 1)) return;
+#endif
 #pragma unroll
       for (int j = 0; j < NL; ++j) {
         const int row = srow0 + j * RSTEP;
@@ -224,6 +259,10 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
     using Zero = std::integral_constant<int, 0>;
     using Others = std::integral_constant<int, (NSETS - 1) * LPS>;
     static_assert((NSETS - 1) * LPS <= 63, "vmcnt immediate");
+    if (a.debug & 4) {  // experiment: no loads, no split -- the consumers' time alone
+      for (int64_t i = 0; i <= my_tiles; ++i) lds_barrier();
+      return;
+    }
     int64_t t = pid;
     load_tile(P[0], Q[0], t);
     wait_set(P[0], Q[0], Zero{});
@@ -271,10 +310,18 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
       wm[s][j] = m;
       wl[s][j] = lo;
     }
+#ifndef KGX_DENSE_TRANSPOSED
   const float bcol = (a.bias && n_col < a.N) ? a.bias[n_col] : 0.0f;
   // byte offset of this lane's first output element within a tile (row 4 lq, column n_col);
   // out-of-range for columns past N, so their stores are dropped
   const uint32_t out_lane = n_col < a.N ? uint32_t((4 * lq * a.ld_out + n_col) * 4) : 0x80000000u;
+#else
+  // output-transposed form: lane holds row lr, columns col4 .. col4 + 3
+  const int col4 = cg * 16 * WAVES + wave * 16 + 4 * lq;
+  // byte offset of (row lr, column col4) within a tile; a whole 4-column group past N
+  // is out of range (vec_out: N % 4 == 0, so no group straddles N)
+  const uint32_t out_row = col4 < a.N ? uint32_t((lr * a.ld_out + col4) * 4) : 0x80000000u;
+#endif
   lds_barrier();
 
   int64_t t = pid;
@@ -325,29 +372,40 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
         } else {
           wait_frags(cur, acc, std::integral_constant<int, 0>{});
         }
-        // small terms first; two independent accumulator chains (row tiles)
+        // small terms first; two independent accumulator chains (row tiles).
+        // Experiment KGX_DENSE_TRANSPOSED: D = W^T x^T, so a lane ends with 4
+        // consecutive output columns of one row (one dwordx4 store per block)
+        // instead of one column of 4 rows (four dword stores); the A and B
+        // fragment layouts of 16x16x32 are mirror images, so the same register /
+        // LDS fragments serve with the operands swapped.  Measured 1-6 % slower
+        // (C4 7.12 vs 7.02 ms, NS 2.24 vs 2.12): the stores' bytes, not their
+        // instruction count, are what the consumers pay for.
+#ifndef KGX_DENSE_TRANSPOSED
+#define KGX_MF(X, W, ACC_) __builtin_amdgcn_mfma_f32_16x16x32_bf16(X, W, ACC_, 0, 0, 0)
+#else
+#define KGX_MF(X, W, ACC_) __builtin_amdgcn_mfma_f32_16x16x32_bf16(W, X, ACC_, 0, 0, 0)
+#endif
 #pragma unroll
-        for (int r = 0; r < 2; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.l[r], wh[s], acc[r], 0, 0, 0);
+        for (int r = 0; r < 2; ++r) acc[r] = KGX_MF(cur.l[r], wh[s], acc[r]);
 #pragma unroll
-        for (int r = 0; r < 2; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.h[r], wl[s], acc[r], 0, 0, 0);
+        for (int r = 0; r < 2; ++r) acc[r] = KGX_MF(cur.h[r], wl[s], acc[r]);
 #pragma unroll
-        for (int r = 0; r < 2; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.m[r], wm[s], acc[r], 0, 0, 0);
+        for (int r = 0; r < 2; ++r) acc[r] = KGX_MF(cur.m[r], wm[s], acc[r]);
 #pragma unroll
-        for (int r = 0; r < 2; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.m[r], wh[s], acc[r], 0, 0, 0);
+        for (int r = 0; r < 2; ++r) acc[r] = KGX_MF(cur.m[r], wh[s], acc[r]);
 #pragma unroll
-        for (int r = 0; r < 2; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.h[r], wm[s], acc[r], 0, 0, 0);
+        for (int r = 0; r < 2; ++r) acc[r] = KGX_MF(cur.h[r], wm[s], acc[r]);
 #pragma unroll
-        for (int r = 0; r < 2; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.h[r], wh[s], acc[r], 0, 0, 0);
+        for (int r = 0; r < 2; ++r) acc[r] = KGX_MF(cur.h[r], wh[s], acc[r]);
+#undef KGX_MF
       };
       [&]<int... S>(std::integer_sequence<int, S...>) {
         (step(std::integral_constant<int, S>{}), ...);
       }(std::make_integer_sequence<int, KS>{});
     }
-    // epilogue: lane holds rows 4 lq + j of column lr of each 16x16 block.
     // Raw buffer stores through a per-tile descriptor: rows past M fall
     // outside its record count and columns past N carry an out-of-range
-    // offset, so both are dropped by the range check (no branches); the
-    // per-row part of the offset is wave-uniform (soffset).
+    // offset, so both are dropped by the range check (no branches).
     if (!(a.debug & 2)) {
       const int64_t r0 = t * kBM;
       int64_t rows = a.M - r0;
@@ -358,6 +416,8 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
       const int bytes = __builtin_amdgcn_readfirstlane(int(rows * a.ld_out * 4));
       const auto rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((uint64_t(hi) << 32) | lo), 0,
                                                         bytes, 0x00020000);
+#ifndef KGX_DENSE_TRANSPOSED
+      // lane holds rows 4 lq + j of column lr of each 16x16 block (soffset = the row)
 #pragma unroll
       for (int r = 0; r < 2; ++r)
 #pragma unroll
@@ -369,6 +429,42 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
           if (a.relu) v = fmaxf(v, 0.0f);
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rs, out_lane, soff, 0);
         }
+#else
+      // lane holds columns col4 + j (j < 4) of row lr of each 16x16 block (soffset = 16 r rows);
+      // the bias is re-read per tile (an L1 hit) rather than held in 4 more registers
+      float b4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b4[j] = (a.bias && col4 + j < a.N) ? a.bias[col4 + j] : 0.0f;
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int soff = int(16 * r * a.ld_out * 4);
+        f32x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = acc[r][j] + b4[j];
+        if (a.vec_out) {
+          if constexpr (ACC) {
+            const f32x4 o = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, out_row, soff, 0));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = __fadd_rn(o[j], v[j]);
+          }
+          if (a.relu) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.0f);
+          }
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, out_row, soff, 0);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint32_t off = col4 + j < a.N ? out_row + 4u * j : 0x80000000u;
+            float e = v[j];
+            if constexpr (ACC)
+              e = __fadd_rn(__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, soff, 0)), e);
+            if (a.relu) e = fmaxf(e, 0.0f);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, e), rs, off, soff, 0);
+          }
+        }
+      }
+#endif
     }
     lds_barrier();  // buffer `buf` free for the producers; the stores stay in flight
   }
@@ -450,6 +546,7 @@ extern "C" int kgx_dense(int64_t M, const float* x0, int64_t ld_x0, int64_t K0, 
   a.accumulate = (flags & KGX_DENSE_ACCUMULATE) != 0;
   const int K = int(K0 + K1);
   a.cg_count = N <= 128 ? 1 : 2;
+  a.vec_out = N % 4 == 0 && ld_out % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0;
 #ifdef KGX_EXPERIMENTS  // cost-decomposition knob; never in a product build (it changes results)
   static const int dbg = [] {
     const char* h = getenv("KGX_DENSE_DEBUG");

@@ -160,6 +160,25 @@ __global__ __launch_bounds__(kBlock) void gatv2_kernel(GatArgs a) {
       l *= scale;
 #pragma unroll
       for (int k = 0; k < K; ++k) acc[k] *= scale;
+#ifdef KGX_GAT_F32BLOCK
+      // experiment: the U-edge block summed in fp32 (<= U terms), added to the fp64 running sums once
+      float bl = 0.0f, bacc[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) bacc[k] = 0.0f;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (u < n) {
+          const float pu = expf(s[u] - m_new);
+          bl += pu;
+          const float pd = pu * dm[u];
+#pragma unroll
+          for (int k = 0; k < K; ++k) bacc[k] = fmaf(pd, hs[u][k], bacc[k]);
+        }
+      }
+      l += double(bl);
+#pragma unroll
+      for (int k = 0; k < K; ++k) acc[k] += double(bacc[k]);
+#else
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (u < n) {
@@ -170,6 +189,7 @@ __global__ __launch_bounds__(kBlock) void gatv2_kernel(GatArgs a) {
           for (int k = 0; k < K; ++k) acc[k] = fma(pd, double(hs[u][k]), acc[k]);
         }
       }
+#endif
       m = m_new;
     }
 

@@ -61,4 +61,26 @@ __device__ __forceinline__ void split3_pair(float w0, float w1, uint32_t& hi, ui
   lo = uint32_t(uint16_t(l0)) | (uint32_t(uint16_t(l1)) << 16);
 }
 
+typedef float kgx_f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 kgx_bf16x2_t __attribute__((ext_vector_type(2)));
+
+// two RNE bf16 conversions in one v_cvt_pk_bf16_f32 (a in the low half)
+__device__ __forceinline__ uint32_t bf16_pack2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((kgx_f32x2_t{a, b}), kgx_bf16x2_t));
+}
+
+// split3_a of a pair, packed, in 9 VALU ops (three packed conversions; the
+// planes' f32 values are the packed words shifted / masked).  Equal to
+// split3_a element by element whenever bf16(a) and bf16(b) are finite; the
+// caller checks that (dense.hip: a non-finite running sum of 2x sends the
+// thread's slots to split3_a_lo).
+__device__ __forceinline__ void split3_pair_rn(float a, float b, uint32_t& hi, uint32_t& mid, uint32_t& lo) {
+  hi = bf16_pack2(a, b);
+  const float ra = __fsub_rn(a, __builtin_bit_cast(float, hi << 16));
+  const float rb = __fsub_rn(b, __builtin_bit_cast(float, hi & 0xffff0000u));
+  mid = bf16_pack2(ra, rb);
+  lo = bf16_pack2(__fsub_rn(ra, __builtin_bit_cast(float, mid << 16)),
+                  __fsub_rn(rb, __builtin_bit_cast(float, mid & 0xffff0000u)));
+}
+
 }  // namespace kgx
