@@ -262,7 +262,11 @@ def main() -> None:
 
             comm = HostStagedComm()
         else:
-            dist.init_process_group("nccl", device_id=dev)
+            # RCCL on high-priority streams: its all-to-all kernels get block slots
+            # while the own-source pass (a resident grid) holds the rest
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.is_high_priority_stream = True
+            dist.init_process_group("nccl", device_id=dev, pg_options=opts)
         log(f"process group: backend={dist.get_backend()} world_size={dist.get_world_size()}")
 
     import keras_geometric_amd as kgx

@@ -190,8 +190,11 @@ class HaloChunk:
     send_splits: list
     send_rows: torch.Tensor  # int32 local rows to send, grouped by destination rank
     # push-pull plan: the send rows are one weighted-sum pass over this CSR
-    # (a pulled row = one edge of weight 1, a pushed partial = its edges)
+    # (pushed partial sums)
     send_graph: object = None
+    # a push-pull chunk: its exchange steps (pulled rows, then partials), each
+    # landing in its own contiguous slice of [lo, hi)
+    steps: list | None = None
 
 
 @dataclass
@@ -202,6 +205,19 @@ class PushPullPlan:
     n_rows: int  # halo rows received per layer
     n_pull: int  # of which source rows
     n_push: int  # of which partial sums pushed by the owners
+
+
+class _Works:
+    """The handles of one chunk's exchange steps: wait() orders the current
+    stream after all of them."""
+
+    def __init__(self, handles):
+        self.handles = handles
+
+    def wait(self):
+        for h in self.handles:
+            if h is not None:
+                h.wait()
 
 
 def _prefix(v: list) -> list:
@@ -446,21 +462,37 @@ class ShardedGraph:
         req_src = exchange(pe_src, torch.long, s_pe, r_pe) - lo
         req_w = exchange(pe_w, torch.float32, s_pe, r_pe)
 
-        # owner side: per chunk, send CSR rows = [pulled slice k | pushed slice k] per requester
+        # Per chunk k, two exchange steps: the pulled rows (slice k of every
+        # requester's pull list; the owner packs them with kgx_gather_rows, a
+        # plain copy) and the pushed partial sums (slice k of every push list;
+        # one weighted-sum pass over a send CSR).  Packing the pulled rows as
+        # one-edge CSR rows made the pack latency-bound: a dependent chain of
+        # item, index and row loads per row, 6.4 ms for 12.7 GB at 8 shards
+        # (tools/shard_sim.py).  The receiver lands chunk k as [pulled rows from
+        # every peer | partials from every peer].
         sp, spe = _prefix(s_pull), _prefix(s_pe)
         rp, ru = _prefix(r_pull), _prefix(r_push)
         pull_pos = torch.empty(rp[-1], dtype=torch.long, device=dev)
         push_pos = torch.empty(ru[-1], dtype=torch.long, device=dev)
+        none_i32 = torch.empty(0, dtype=torch.int32, device=dev)
         chunks, off = [], 0
         for k in range(K):
-            cols, slots, ws, send_splits, recv_splits = [], [], [], [], []
-            n_slots, lo_k = 0, off
+            lo_k = off
+            rows, pull_send, pull_recv = [], [], []
             for r in range(world):
                 a, b = sp[r] + s_pull[r] * k // K, sp[r] + s_pull[r] * (k + 1) // K
-                cols.append(req_pull[a:b])
-                slots.append(torch.arange(n_slots, n_slots + b - a, device=dev))
-                ws.append(torch.ones(b - a, dtype=torch.float32, device=dev))
-                n_slots += b - a
+                rows.append(req_pull[a:b])
+                pull_send.append(b - a)
+            for p in range(world):  # receiver side: where chunk k's pulled rows from p land
+                a, b = r_pull[p] * k // K, r_pull[p] * (k + 1) // K
+                pull_pos[rp[p] + a: rp[p] + b] = torch.arange(off, off + b - a, device=dev)
+                off += b - a
+                pull_recv.append(b - a)
+            pull_step = HaloChunk(lo=lo_k, hi=off, recv_splits=pull_recv, send_splits=pull_send,
+                                  send_rows=torch.cat(rows).to(torch.int32).contiguous() if rows else none_i32)
+            cols, slots, ws, push_send, push_recv = [], [], [], [], []
+            n_slots, push_lo = 0, off
+            for r in range(world):
                 j0, j1 = s_push[r] * k // K, s_push[r] * (k + 1) // K
                 sl = req_slot[spe[r]: spe[r + 1]]
                 m = (sl >= j0) & (sl < j1)
@@ -468,22 +500,21 @@ class ShardedGraph:
                 slots.append(n_slots + sl[m] - j0)
                 ws.append(req_w[spe[r]: spe[r + 1]][m])
                 n_slots += j1 - j0
-                send_splits.append(b - a + j1 - j0)
-            for p in range(world):  # receiver side: where chunk k's rows from p land
-                a, b = r_pull[p] * k // K, r_pull[p] * (k + 1) // K
-                pull_pos[rp[p] + a: rp[p] + b] = torch.arange(off, off + b - a, device=dev)
-                off += b - a
+                push_send.append(j1 - j0)
+            for p in range(world):  # receiver side: where chunk k's partials from p land
                 j0, j1 = r_push[p] * k // K, r_push[p] * (k + 1) // K
                 push_pos[ru[p] + j0: ru[p] + j1] = torch.arange(off, off + j1 - j0, device=dev)
                 off += j1 - j0
-                recv_splits.append(b - a + j1 - j0)
+                push_recv.append(j1 - j0)
             send_graph = None
             if n_slots:
                 send_graph = self.backend.build_graph(torch.cat(cols).to(torch.int32), torch.cat(slots).to(torch.int32),
                                                       n_local, n_slots, 128)
                 send_graph.w = torch.cat(ws)[send_graph.eid.long()].contiguous()
-            chunks.append(HaloChunk(lo=lo_k, hi=off, recv_splits=recv_splits, send_splits=send_splits,
-                                    send_rows=torch.empty(0, dtype=torch.int32, device=dev), send_graph=send_graph))
+            push_step = HaloChunk(lo=push_lo, hi=off, recv_splits=push_recv, send_splits=push_send,
+                                  send_rows=none_i32, send_graph=send_graph)
+            chunks.append(HaloChunk(lo=lo_k, hi=off, recv_splits=[], send_splits=[], send_rows=none_i32,
+                                    steps=[pull_step, push_step]))
         # receiver CSR over the received rows: pulled rows keep their edges and
         # weights; a pushed partial is one edge of weight 1 into its row
         pidx = torch.searchsorted(pull_ids, hs[via_pull])
@@ -571,18 +602,25 @@ class ShardedGraph:
             start = getattr(self.comm, "all_to_all_start", None)
             works = []
             for c in chunks:
-                send = self._pack(x_local, c)
-                if start is None:
-                    self.comm.all_to_all_single(halo[c.lo: c.hi], send, c.recv_splits, c.send_splits)
-                    works.append(None)
-                else:
-                    works.append(start(halo[c.lo: c.hi], send, c.recv_splits, c.send_splits))
+                handles = []
+                for st in c.steps or [c]:
+                    send = self._pack(x_local, st)
+                    if start is None:
+                        self.comm.all_to_all_single(halo[st.lo: st.hi], send, st.recv_splits, st.send_splits)
+                    else:
+                        handles.append(start(halo[st.lo: st.hi], send, st.recv_splits, st.send_splits))
+                works.append(_Works(handles) if start is not None else None)
             return works
 
         if not x_local.is_cuda:
             return run()
         if self._side is None:
-            self._side = torch.cuda.Stream(device=x_local.device)
+            # high priority: the packing kernels are the exchange's critical path
+            # start; at normal priority the resident own-source pass launched
+            # right after them holds all but the block slots it leaves free and
+            # the packing crawls on those (tools/shard_sim.py: 6.8 ms for 12.7 GB)
+            prio = 0 if os.environ.get("KGX_SIDE_PRIORITY", "1") == "0" else -1  # 0: measurement A/B only
+            self._side = torch.cuda.Stream(device=x_local.device, priority=prio)
         cur = torch.cuda.current_stream(x_local.device)
         self._side.wait_stream(cur)
         with torch.cuda.stream(self._side):

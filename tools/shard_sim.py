@@ -38,10 +38,17 @@ class _EventWork:
 
 
 class LoopbackComm(kd.TorchComm):
-    """Rank 0 of a `world`-rank job whose peers mirror it (measurement stand-in)."""
+    """Rank 0 of a `world`-rank job whose peers mirror it (measurement stand-in).
 
-    def __init__(self, world: int, n_local: int):
+    link_gbps > 0 models the links: each started all-to-all runs on one "link"
+    stream (chunks in order, as RCCL's own stream does) after the send rows are
+    ready, and occupies it for bytes / link_gbps (a spin of one wave, so the
+    modelled transfer takes time but no HBM bandwidth) before its copy lands."""
+
+    def __init__(self, world: int, n_local: int, link_gbps: float = 0.0, cycles_per_ms: float = 0.0):
         self.w, self.n_local = world, n_local
+        self.link_gbps, self.cycles_per_ms = link_gbps, cycles_per_ms
+        self.link = None
 
     def rank(self):
         return 0
@@ -60,9 +67,25 @@ class LoopbackComm(kd.TorchComm):
     def all_to_all_start(self, out, inp, out_splits=None, in_splits=None):
         """Asynchronous like RCCL's: the copy is queued on the current (side)
         stream and wait() makes the then-current stream wait for it."""
-        self.all_to_all_single(out, inp, out_splits, in_splits)
-        ev = torch.cuda.Event()
-        ev.record()
+        if self.link_gbps <= 0:
+            self.all_to_all_single(out, inp, out_splits, in_splits)
+            ev = torch.cuda.Event()
+            ev.record()
+            return _EventWork(ev)
+        if self.link is None:
+            self.link = torch.cuda.Stream(priority=-1)
+        ready = torch.cuda.Event()
+        ready.record()
+        self.link.wait_event(ready)
+        with torch.cuda.stream(self.link):
+            ms = out.numel() * out.element_size() / (self.link_gbps * 1e6)
+            if ms > 0:
+                torch.cuda._sleep(int(ms * self.cycles_per_ms))
+            self.all_to_all_single(out, inp, out_splits, in_splits)
+            inp.record_stream(self.link)
+            out.record_stream(self.link)
+            ev = torch.cuda.Event()
+            ev.record()
         return _EventWork(ev)
 
     def broadcast(self, t, src=0):
@@ -77,13 +100,24 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--nodes", type=int, default=10_000_000)
     ap.add_argument("--edges", type=int, default=100_000_000)
+    ap.add_argument("--link-gbps", type=float, default=0.0,
+                    help="model the exchange: per-GPU receive rate in GB/s (0: the exchange is free)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     P = args.world
+    cycles_per_ms = 0.0
+    if args.link_gbps > 0:  # calibrate torch.cuda._sleep's cycles against events
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(10_000_000)
+        t0.record()
+        torch.cuda._sleep(100_000_000)
+        t1.record()
+        torch.cuda.synchronize()
+        cycles_per_ms = 100_000_000 / t0.elapsed_time(t1)
     for push, K in [(p, int(v)) for p in args.push.split(",") for v in args.chunks.split(",")]:
         os.environ["KGX_HALO_PUSH"] = push
         n_local = kd.equal_bounds(args.nodes * P, P)[1]
-        comm = LoopbackComm(P, n_local)
+        comm = LoopbackComm(P, n_local, args.link_gbps, cycles_per_ms)
         sg = kd.ShardedGraph.rmat(args.nodes * P, args.edges * P, seed=0, device=dev, comm=comm,
                                   self_loops=True, gcn_norm=True, halo_chunks=K)
         x = torch.randn(sg.n_local, 128, device=dev)
@@ -110,7 +144,7 @@ def main():
         if pp is not None:
             g_chunks = pp.parts
         print(json.dumps({
-            "world": P, "chunks": K, "push_pull": pp is not None, "step_ms": round(t0.elapsed_time(t1) / args.steps, 3),
+            "world": P, "chunks": K, "push_pull": pp is not None, "link_gbps": args.link_gbps, "step_ms": round(t0.elapsed_time(t1) / args.steps, 3),
             "launch_ms": [round(v, 3) for v in launch_ms],
             "own_edges": g_own.kept, "chunk_edges": [g.kept for g in g_chunks],
             "halo_rows_pull_only": sg.n_halo, "halo_rows": pp.n_rows if pp else sg.n_halo,
