@@ -24,6 +24,7 @@
 // ds_read_b128 A-fragment reads are conflict-free), then every wave runs
 // v_mfma_f32_16x16x32_bf16 over K for its columns and stores its 16x16 blocks
 // with the bias / ReLU / accumulate epilogue.  One LDS barrier per tile.
+#include <cstdlib>
 #include <type_traits>
 #include <utility>
 
@@ -66,6 +67,7 @@ struct DenseArgs {
   int accumulate;
   int cg_count;  // column groups of 16 WAVES columns (1 or 2)
   int vec_out;   // N, ld_out multiples of 4 and out 16-byte aligned: dwordx4 output stores
+  int pstore;    // experiment KGX_DENSE_PSTORE=1: the producers store the output (vec_out, no accumulate, one operand)
   int debug;     // experiment builds only (-DKGX_EXPERIMENTS, env KGX_DENSE_DEBUG): 1 skip MFMA, 2 skip stores, 4 skip loads + split
 };
 
@@ -105,6 +107,10 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
   constexpr int NL = G::F4_PER_TILE / TP;  // float4 loads per producer thread per tile
   constexpr int RSTEP = TP / G::F4_PER_ROW;
   __shared__ short As[2][3][kBM][G::STRIDE];
+  // output tile staged for the producers' stores (a.pstore), double-buffered by step parity
+  constexpr int OCOLS = 16 * WAVES;
+  constexpr int OSTRIDE = OCOLS + 4;  // floats; 4 mod 32 dwords between rows
+  __shared__ float Os[2][kBM][OSTRIDE];
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
@@ -256,19 +262,67 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
         *reinterpret_cast<bf16x4_t*>(&As[buf][2][row][kk]) = pl;
       }
     };
+    // Producer-side output stores (a.pstore): the consumers leave each finished
+    // 32-row tile in LDS (Os) and the producers store it during the next step
+    // as whole-row dwordx4 runs with the bias / ReLU epilogue, so the MFMA waves
+    // issue no global stores (their stores at the tile end did not overlap the
+    // MFMAs: 1.3 ms of the C4 shape's 7.1).  Every step issues NST stores
+    // (out-of-range, so dropped, where there is no tile to store yet), which
+    // keeps the vmcnt count of the prefetch waits a constant.
+    constexpr int OC4 = OCOLS / 4;         // float4 per out-tile row
+    constexpr int NST = kBM * OC4 / TP;    // out-tile float4 per producer thread
+    constexpr int PRSTEP = TP / OC4;       // out-tile rows between a thread's float4s
+    static_assert(NST * TP == kBM * OC4, "producer store slots must tile the out tile");
+    const int pc4 = ptid % OC4;
+    const int prow0 = ptid / OC4;
+    const int ocol = cg * OCOLS + 4 * pc4;
+    float ob4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ob4[j] = (!TWO && !ACC && a.pstore && a.bias && ocol + j < a.N) ? a.bias[ocol + j] : 0.0f;
+    auto store_out = [&](int64_t step) {  // step < 0: dummy stores (dropped)
+      const int64_t tile = pid + (step < 0 ? 0 : step) * n_pairs;
+      const int64_t r0 = tile * kBM;
+      int64_t rows = a.M - r0;
+      rows = step < 0 ? 0 : (rows < 0 ? 0 : (rows > kBM ? kBM : rows));
+      const uint64_t addr = reinterpret_cast<uint64_t>(a.out) + uint64_t(r0 * a.ld_out * 4);
+      const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(addr));
+      const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(addr >> 32));
+      const int bytes = __builtin_amdgcn_readfirstlane(int(rows * a.ld_out * 4));
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((uint64_t(hi) << 32) | lo), 0,
+                                                        bytes, 0x00020000);
+      const int ob = int((step < 0 ? 0 : step) & 1);
+#pragma unroll
+      for (int m = 0; m < NST; ++m) {
+        const int row = prow0 + m * PRSTEP;
+        f32x4 v = *reinterpret_cast<const f32x4*>(&Os[ob][row][4 * pc4]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[j] = v[j] + ob4[j];
+          if (a.relu) v[j] = fmaxf(v[j], 0.0f);
+        }
+        const uint32_t off = ocol < a.N ? uint32_t((row * a.ld_out + ocol) * 4) : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, off, 0, 0);
+      }
+    };
     using Zero = std::integral_constant<int, 0>;
     using Others = std::integral_constant<int, (NSETS - 1) * LPS>;
-    static_assert((NSETS - 1) * LPS <= 63, "vmcnt immediate");
+    using OthersP = std::integral_constant<int, (NSETS - 1) * (LPS + NST)>;
+    static_assert((NSETS - 1) * (LPS + NST) <= 63, "vmcnt immediate");
     if (a.debug & 4) {  // experiment: no loads, no split -- the consumers' time alone
       for (int64_t i = 0; i <= my_tiles; ++i) lds_barrier();
       return;
     }
+    // two operands hold two register sets per slot: no registers left for the store path
+    const bool pstore = !TWO && !ACC && a.pstore;
     int64_t t = pid;
     load_tile(P[0], Q[0], t);
     wait_set(P[0], Q[0], Zero{});
     stage(P[0], Q[0], 0);
 #pragma unroll
-    for (int k = 0; k < NSETS; ++k) load_tile(P[k], Q[k], t + (k + 1) * n_pairs);
+    for (int k = 0; k < NSETS; ++k) {
+      if (pstore) store_out(-1);
+      load_tile(P[k], Q[k], t + (k + 1) * n_pairs);
+    }
     lds_barrier();
     // step i (tile i of this block): consumers run tile i from buffer i & 1;
     // producers stage tile i + 1 (register set i % NSETS) into the other
@@ -280,14 +334,17 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
 #pragma unroll
       for (int k = 0; k < NSETS; ++k) {
         if (!done) {
-          wait_set(P[k], Q[k], Others{});
+          if (pstore) wait_set(P[k], Q[k], OthersP{});
+          else wait_set(P[k], Q[k], Others{});
           stage(P[k], Q[k], int((i + k + 1) & 1));
+          if (pstore) store_out(i + k - 1);  // the tile the consumers finished at the last barrier
           load_tile(P[k], Q[k], t + (k + 1 + NSETS) * n_pairs);
           lds_barrier();
           done = i + k + 1 >= my_tiles;
         }
       }
     }
+    if (pstore) store_out(my_tiles - 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no loads in flight at exit
     return;
   }
@@ -406,7 +463,14 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
     // Raw buffer stores through a per-tile descriptor: rows past M fall
     // outside its record count and columns past N carry an out-of-range
     // offset, so both are dropped by the range check (no branches).
-    if (!(a.debug & 2)) {
+    if (!TWO && !ACC && a.pstore) {
+      // lane holds rows 4 lq + j of column lr of each 16x16 block: into the LDS
+      // out tile for the producers' stores (bias / ReLU applied there)
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) Os[buf][16 * r + 4 * lq + j][wave * 16 + lr] = acc[r][j];
+    } else if (!(a.debug & 2)) {
       const int64_t r0 = t * kBM;
       int64_t rows = a.M - r0;
       rows = rows > kBM ? kBM : rows;
@@ -547,6 +611,13 @@ extern "C" int kgx_dense(int64_t M, const float* x0, int64_t ld_x0, int64_t K0, 
   const int K = int(K0 + K1);
   a.cg_count = N <= 128 ? 1 : 2;
   a.vec_out = N % 4 == 0 && ld_out % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0;
+  // producer-side output stores: measured slower (C4 7.7 vs 7.1 ms, NS xW 2.4 vs 2.2):
+  // the producers, not the consumers' stores, bound the kernel; opt-in experiment
+  static const bool pstore_on = [] {
+    const char* h = getenv("KGX_DENSE_PSTORE");
+    return h && atoi(h) != 0;
+  }();
+  a.pstore = a.vec_out && !a.accumulate && pstore_on;
 #ifdef KGX_EXPERIMENTS  // cost-decomposition knob; never in a product build (it changes results)
   static const int dbg = [] {
     const char* h = getenv("KGX_DENSE_DEBUG");
