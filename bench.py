@@ -67,20 +67,23 @@ def b_alg_spmm(n: int, e_agg: int, f: int, weighted: bool, f_out: int | None = N
     return 4 * (n + 1) + e_agg * (4 + (4 if weighted else 0) + 4 * f) + 4 * n * f_out
 
 
-def pmc_traffic(config: str, kernel: str) -> tuple[float | None, str | None]:
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC
-    summary (profiles/r*/pmc_<config>.json, written by tools/pmc_summary.py),
-    used only if it was profiled from the kernel sources being run."""
+def pmc_traffic(config: str, kernels) -> tuple[float | None, str | None]:
+    """HBM bytes per step of the launches in `kernels` (summed: one op may be
+    several kernels) from the newest committed rocprofv3 PMC summary
+    (profiles/r*/pmc_<config>.json, written by tools/pmc_summary.py), used only
+    if it was profiled from the kernel sources being run."""
     import importlib.util
 
     spec = importlib.util.spec_from_file_location("pmc_summary", ROOT / "tools" / "pmc_summary.py")
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
+    kernels = [kernels] if isinstance(kernels, str) else list(kernels)
     for path in sorted(ROOT.glob(f"profiles/r*/pmc_{config}.json"), reverse=True):
         d = json.loads(path.read_text())
-        if d.get("source_hash") != mod.source_hash() or kernel not in d.get("kernels", {}):
+        if d.get("source_hash") != mod.source_hash() or kernels[0] not in d.get("kernels", {}):
             continue
-        return d["kernels"][kernel]["traffic_bytes_per_launch"], str(path.relative_to(ROOT))
+        have = d["kernels"]
+        return sum(have[k]["traffic_bytes_per_launch"] for k in kernels if k in have), str(path.relative_to(ROOT))
     return None, None
 
 
@@ -352,13 +355,15 @@ def main() -> None:
         # SURVEY.md §8d per rank; at N>1 the accumulating halo-chunk passes' re-reads
         # of the rows they add to are implementation overhead, not algorithmic bytes
         balg = b_alg_spmm(n_rows, e_agg, f_in if fused else f_out, weighted=True, f_out=f_out)
-        kernel = "spmm_gemm_kernel" if fused else "spmm_kernel"
+        # the fused op: long rows, the short-row suffix (degree <= 7) and the hub fix-up
+        kernel = ("spmm_gemm_kernel", "spmm_gemm_short_kernel", "spmm_gemm_fixup_kernel") if fused \
+            else ("spmm_kernel", "spmm_fixup_kernel")
     elif kind == "gat":  # one pass: h_src row per edge, h_dst row + output row per node
         balg = 4 * (n_rows + 1) + e_agg * (4 + 4 * f_out) + 8 * n_rows * f_out
-        kernel = "gatv2_kernel"
+        kernel = ("gatv2_kernel", "gatv2_fixup_kernel")
     else:  # GIN: + the x_i root row of the (1+eps) x_i + aggr epilogue; SAGE mean: plain gather-sum
         balg = b_alg_spmm(n_rows, e_agg, f_in, weighted=False) + (4 * n_rows * f_in if kind == "gin" else 0)
-        kernel = "spmm_kernel"
+        kernel = ("spmm_kernel", "spmm_fixup_kernel")
     achieved = balg / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
     mine = {"rank": rank, "e_agg": e_agg, "rows": n_rows, "ms_per_step": elapsed / args.steps * 1e3,
             "aggregation_ms": kern_ms, "launches_per_step": launches, "roofline_achieved_GBps": achieved,
@@ -432,7 +437,7 @@ def main() -> None:
         "cold_layer_ms": cold_ms,
         "roofline": {
             "bound": "hbm",
-            "kernel": kernel,
+            "kernel": "+".join(kernel),
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

@@ -197,6 +197,17 @@ int kgx_spmm_gemm(int reduce, const int32_t* rowptr, const int32_t* rows, int64_
                   const float* W, int64_t F_out, const float* bias, int flags, float gin_scale,
                   float* out, int64_t ld_out, float* partials, float* agg_out, int64_t ld_agg,
                   kgx_stream_t stream);
+/* kgx_spmm_gemm with the schedule's short-row suffix named: items
+ * [n_long_items, n_items) are rows of degree <= KGX_SHORT_ROW_MAX (the degree-ordered
+ * schedule's tail, never split), reduced 64 rows per block iteration by a
+ * second kernel.  n_long_items = n_items is kgx_spmm_gemm. */
+enum { KGX_SHORT_ROW_MAX = 7 };
+int kgx_spmm_gemm_ex(int reduce, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
+                     const int32_t* items, int64_t n_items, int64_t n_long_items, const int32_t* split,
+                     int64_t n_split, const int32_t* idx, const float* w, const float* x, int64_t ld_x,
+                     int64_t F_in, const float* W, int64_t F_out, const float* bias, int flags,
+                     float gin_scale, float* out, int64_t ld_out, float* partials, float* agg_out,
+                     int64_t ld_agg, kgx_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Backward of the segment max / min reduction (autograd of kgx_spmm MAX/MIN).

@@ -50,6 +50,7 @@ struct FusedArgs {
   int64_t n_rows;
   const int4* items;
   int64_t n_items;
+  int64_t n_long;  // items [0, n_long): spmm_gemm_kernel; [n_long, n_items): rows of degree <= kShortMax
   const int4* split;
   int64_t n_split;
   const int32_t* idx;
@@ -188,7 +189,7 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
 #endif
   const float bcol = (mfma_wave && a.bias) ? a.bias[n_col] : 0.0f;
 
-  const int64_t n_work = a.items ? a.n_items : a.n_rows;
+  const int64_t n_work = a.items ? a.n_long : a.n_rows;
   const int64_t stride = int64_t(gridDim.x) * kGroups;
 
   // software pipeline: the next item's descriptor and its first U neighbour rows
@@ -386,6 +387,229 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
   }
 }
 
+// Rows of degree <= KGX_SHORT_ROW_MAX (the schedule's suffix; 78 % of an R-MAT graph's
+// rows, 11 % of its edges).  spmm_gemm_kernel gives each row-group ONE row per
+// 16-row tile, so on these rows a group has one or two gathers in flight and
+// the tile's fixed chain (item, index, row, split, MFMA, store) dominates:
+// NS rows of degree <= 7 ran at 3.4 TB/s against 7.7 TB/s for the rest
+// (tools/exp_lowdeg.py).  Here a block iteration takes 64 rows, 4 per group,
+// whose first two edges are all gathered together, and the MFMA phase runs
+// four 16-row blocks per wave.
+static_assert(KGX_SHORT_ROW_MAX == 7, "the short kernel gathers two edges per row up front, then pairs");
+#ifndef KGX_SHORT_RPG
+#define KGX_SHORT_RPG 2
+#endif
+#ifndef KGX_SHORT_PF
+#define KGX_SHORT_PF 3
+#endif
+constexpr int kRPG = KGX_SHORT_RPG;        // rows per group per tile
+constexpr int kSPF = KGX_SHORT_PF;         // edges per row gathered up front (all rows together)
+constexpr int kShortRows = kGroups * kRPG;
+
+template <int RED, bool WEIGHTED>
+__global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs a) {  // 4 waves per SIMD: two blocks per CU
+  using R = Red<RED>;
+  // split planes of the 64 aggregated rows; after the MFMAs the same bytes hold the f32 results
+  __shared__ __attribute__((aligned(16))) short tile3[3][kShortRows][kFin + 8];
+  __shared__ int32_t tile_row[kShortRows];
+  static_assert(sizeof(tile3) >= sizeof(float) * kShortRows * kTileLd, "output tile must fit the plane buffer");
+  float(*otile)[kTileLd] = reinterpret_cast<float(*)[kTileLd]>(&tile3[0][0][0]);
+
+  const int tid = threadIdx.x;
+  const int g = tid >> 5;
+  const int lane = tid & 31;
+  const int f = lane * 4;
+  const int wave = tid >> 6;
+  const int wl = tid & 63;
+  const int n_col = wave * 16 + (wl & 15);
+  const int q = wl >> 4;
+  const bool mfma_wave = wave * 16 < a.F_out;
+
+  bf16x8_t wfh[4], wfm[4], wfl[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+    u32x4_t ph, pm, pl;
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const float v0 = mfma_wave ? a.W[int64_t(32 * q + 8 * s + j) * a.F_out + n_col] : 0.0f;
+      const float v1 = mfma_wave ? a.W[int64_t(32 * q + 8 * s + j + 1) * a.F_out + n_col] : 0.0f;
+      uint32_t h, m_, l;
+      split3_pair(v0, v1, h, m_, l);
+      ph[j / 2] = h;
+      pm[j / 2] = m_;
+      pl[j / 2] = l;
+    }
+    wfh[s] = __builtin_bit_cast(bf16x8_t, ph);
+    wfm[s] = __builtin_bit_cast(bf16x8_t, pm);
+    wfl[s] = __builtin_bit_cast(bf16x8_t, pl);
+  }
+  const float bcol = (mfma_wave && a.bias) ? a.bias[n_col] : 0.0f;
+
+  for (int64_t base = a.n_long + int64_t(blockIdx.x) * kShortRows; base < a.n_items;
+       base += int64_t(gridDim.x) * kShortRows) {
+    int32_t row[kRPG], beg[kRPG], deg[kRPG];
+#pragma unroll
+    for (int r = 0; r < kRPG; ++r) {
+      const int64_t it = base + g + kGroups * r;
+      row[r] = -1;
+      beg[r] = 0;
+      deg[r] = 0;
+      if (it < a.n_items) {
+        const int4 v = a.items[it];
+        row[r] = v.x;
+        beg[r] = v.y;
+        deg[r] = v.z - v.y;
+      }
+    }
+    // the first kSPF edges of all the group's rows in flight together
+    // (unconditional index loads from clamped slots; row gathers exec-masked
+    // by degree)
+    float acc[kRPG][4];
+    {
+      int32_t c[kRPG][kSPF];
+      float wt[kRPG][kSPF];
+#pragma unroll
+      for (int r = 0; r < kRPG; ++r)
+#pragma unroll
+        for (int u = 0; u < kSPF; ++u) {
+          const int32_t ee = deg[r] > 0 ? beg[r] + (u < deg[r] ? u : deg[r] - 1) : 0;
+          c[r][u] = a.idx[ee];
+          if constexpr (WEIGHTED) wt[r][u] = a.w[ee];
+        }
+      float v[kRPG][kSPF][4];
+#pragma unroll
+      for (int r = 0; r < kRPG; ++r)
+#pragma unroll
+        for (int u = 0; u < kSPF; ++u)
+          if (u < deg[r]) vload<4>(v[r][u], a.x + row_off(c[r][u], a.ld_x) + f);
+#pragma unroll
+      for (int r = 0; r < kRPG; ++r)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float t = R::init();
+#pragma unroll
+          for (int u = 0; u < kSPF; ++u) {
+            const float m = WEIGHTED ? __fmul_rn(v[r][u][k], wt[r][u]) : v[r][u][k];
+            t = R::combine(t, u < deg[r] ? R::msg(m) : R::init());
+          }
+          acc[r][k] = t;
+        }
+    }
+    // edges kSPF .. deg-1, two at a time, in order
+#pragma unroll
+    for (int r = 0; r < kRPG; ++r) {
+      for (int32_t e = kSPF; e < deg[r]; e += 2) {
+        const int n = deg[r] - e;
+        int32_t c[2];
+        float wt[2], v[2][4];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int32_t ee = beg[r] + e + (u < n ? u : n - 1);
+          c[u] = a.idx[ee];
+          if constexpr (WEIGHTED) wt[u] = a.w[ee];
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) vload<4>(v[u], a.x + row_off(c[u], a.ld_x) + f);
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float m = WEIGHTED ? __fmul_rn(v[u][k], wt[u]) : v[u][k];
+            acc[r][k] = R::combine(acc[r][k], u < n ? R::msg(m) : R::init());
+          }
+      }
+    }
+    lds_barrier();  // the previous tile's output rows (same LDS bytes) have been stored
+#pragma unroll
+    for (int r = 0; r < kRPG; ++r) {
+      const bool ok = row[r] >= 0;
+      float v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = ok ? R::finish(acc[r][k], deg[r]) : 0.0f;
+      if (ok && a.pre_gin) {
+        float xv[4];
+        vload<4>(xv, a.x + int64_t(row[r]) * a.ld_x + f);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = __fadd_rn(__fmul_rn(a.gin_scale, xv[k]), v[k]);
+      }
+      if (ok && a.agg_out) vstore<4>(a.agg_out + int64_t(row[r]) * a.ld_agg + f, v);
+      bf16x4_t ph, pm, pl;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        short h, m_, l;
+        split3_a(v[k], h, m_, l);
+        ph[k] = h;
+        pm[k] = m_;
+        pl[k] = l;
+      }
+      if (!__builtin_isfinite(__fadd_rn(__fadd_rn(v[0], v[1]), __fadd_rn(v[2], v[3])))) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          short h, m_, l;
+          split3_a_lo(v[k], h, m_, l);
+          ph[k] = h;
+          pm[k] = m_;
+          pl[k] = l;
+        }
+      }
+      const int tr = g + kGroups * r;
+      *reinterpret_cast<bf16x4_t*>(&tile3[0][tr][f]) = ph;
+      *reinterpret_cast<bf16x4_t*>(&tile3[1][tr][f]) = pm;
+      *reinterpret_cast<bf16x4_t*>(&tile3[2][tr][f]) = pl;
+      if (lane == 0) tile_row[tr] = row[r];
+    }
+    lds_barrier();
+    f32x4 d[kRPG];
+    if (mfma_wave && !(a.debug & 1)) {
+      const int m = wl & 15;
+#pragma unroll
+      for (int rb = 0; rb < kRPG; ++rb) d[rb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+#pragma unroll
+        for (int rb = 0; rb < kRPG; ++rb) {
+          const int tr = 16 * rb + m;
+          const bf16x8_t ah = *reinterpret_cast<const bf16x8_t*>(&tile3[0][tr][32 * q + 8 * s4]);
+          const bf16x8_t am = *reinterpret_cast<const bf16x8_t*>(&tile3[1][tr][32 * q + 8 * s4]);
+          const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(&tile3[2][tr][32 * q + 8 * s4]);
+          d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, wfh[s4], d[rb], 0, 0, 0);
+          d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfl[s4], d[rb], 0, 0, 0);
+          d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, wfm[s4], d[rb], 0, 0, 0);
+          d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, wfh[s4], d[rb], 0, 0, 0);
+          d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfm[s4], d[rb], 0, 0, 0);
+          d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfh[s4], d[rb], 0, 0, 0);
+        }
+      }
+    }
+    lds_barrier();  // every wave has read the planes: their bytes now take the f32 results
+    if (mfma_wave) {
+#pragma unroll
+      for (int rb = 0; rb < kRPG; ++rb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) otile[16 * rb + 4 * q + j][n_col] = d[rb][j] + bcol;
+    }
+    lds_barrier();
+    if (!(a.debug & 2)) {
+#pragma unroll
+      for (int r = 0; r < kRPG; ++r) {
+        const int tr = g + kGroups * r;
+        const int rr = tile_row[tr];
+        if (rr >= 0 && f < a.F_out) {
+          float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + f);
+          float4 v = *reinterpret_cast<const float4*>(&otile[tr][f]);
+          if (a.accumulate) {
+            const float4 p = *dst;
+            v = make_float4(__fadd_rn(p.x, v.x), __fadd_rn(p.y, v.y), __fadd_rn(p.z, v.z), __fadd_rn(p.w, v.w));
+          }
+          if (a.relu) v = make_float4(fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f));
+          *dst = v;
+        }
+      }
+    }
+  }
+}
+
 // Split rows: combine chunk partials in order, finish, then out = v @ W + b (VALU).
 template <int RED>
 __global__ __launch_bounds__(256) void spmm_gemm_fixup_kernel(FusedArgs a) {
@@ -440,7 +664,7 @@ __global__ __launch_bounds__(256) void spmm_gemm_fixup_kernel(FusedArgs a) {
 
 template <int RED, bool W>
 int launch(const FusedArgs& a, hipStream_t s) {
-  const int64_t work = a.items ? a.n_items : a.n_rows;
+  const int64_t work = a.items ? a.n_long : a.n_rows;
   if (work > 0) {
     static int cus = 0;
     if (cus == 0) {
@@ -457,6 +681,23 @@ int launch(const FusedArgs& a, hipStream_t s) {
     // KGX_FUSED_SHARE_GPU: leave an eighth of the block slots free so a
     // concurrent collective's kernels (RCCL halo all-to-all) are not starved
     const int64_t cap = a.share_gpu ? int64_t(per_cu) * cus * 7 / 8 : int64_t(per_cu) * cus;
+    hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kThreads), 0, s, a);
+    KGX_CHECK_LAUNCH();
+  }
+  if (a.items && a.n_long < a.n_items) {
+    int per_cu = 0;
+    auto k = spmm_gemm_short_kernel<RED, W>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, 0) != hipSuccess || per_cu <= 0)
+      per_cu = 2;
+    static int cus2 = 0;
+    if (cus2 == 0) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus2, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus2 <= 0)
+        cus2 = 256;
+    }
+    const int64_t need = (a.n_items - a.n_long + kShortRows - 1) / kShortRows;
+    const int64_t cap = a.share_gpu ? int64_t(per_cu) * cus2 * 7 / 8 : int64_t(per_cu) * cus2;
     hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kThreads), 0, s, a);
     KGX_CHECK_LAUNCH();
   }
@@ -480,7 +721,19 @@ extern "C" int kgx_spmm_gemm(int reduce, const int32_t* rowptr, const int32_t* r
                              const float* W, int64_t F_out, const float* bias, int flags, float gin_scale,
                              float* out, int64_t ld_out, float* partials, float* agg_out, int64_t ld_agg,
                              kgx_stream_t stream_) {
+  return kgx_spmm_gemm_ex(reduce, rowptr, rows, n_rows, items, n_items, n_items, split, n_split, idx, w, x, ld_x,
+                          F_in, W, F_out, bias, flags, gin_scale, out, ld_out, partials, agg_out, ld_agg, stream_);
+}
+
+extern "C" int kgx_spmm_gemm_ex(int reduce, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
+                                const int32_t* items, int64_t n_items, int64_t n_long_items, const int32_t* split,
+                                int64_t n_split, const int32_t* idx, const float* w, const float* x, int64_t ld_x,
+                                int64_t F_in, const float* W, int64_t F_out, const float* bias, int flags,
+                                float gin_scale, float* out, int64_t ld_out, float* partials, float* agg_out,
+                                int64_t ld_agg, kgx_stream_t stream_) {
   hipStream_t stream = as_stream(stream_);
+  KGX_REQUIRE(!items || (n_long_items >= 0 && n_long_items <= n_items), KGX_ERR_ARG,
+              "kgx_spmm_gemm: n_long_items must lie in [0, n_items]");
   KGX_REQUIRE(reduce >= KGX_SUM && reduce <= KGX_MIN, KGX_ERR_ARG, "kgx_spmm_gemm: reduce %d unsupported", reduce);
   KGX_REQUIRE(F_in == kFin, KGX_ERR_UNSUPPORTED, "kgx_spmm_gemm: F_in must be %d (got %lld)", kFin,
               (long long)F_in);
@@ -506,6 +759,7 @@ extern "C" int kgx_spmm_gemm(int reduce, const int32_t* rowptr, const int32_t* r
   a.n_rows = n_rows;
   a.items = reinterpret_cast<const int4*>(items);
   a.n_items = items ? n_items : 0;
+  a.n_long = items ? n_long_items : 0;
   a.split = reinterpret_cast<const int4*>(split);
   a.n_split = items ? n_split : 0;
   a.idx = idx;

@@ -66,6 +66,10 @@ class CSRGraph:
     n_split: int = 0
     n_slots: int = 0
     split_len: int = 0
+    # items [n_long, n_items): the schedule's suffix of unsplit rows of degree <=
+    # KGX_SHORT_ROW_MAX, which the fused kernel reduces 32-64 rows per block
+    # iteration (kgx_spmm_gemm_ex); -1: none / not computed
+    n_long: int = -1
     extras: dict = field(default_factory=dict)
 
     @property
@@ -169,6 +173,24 @@ def _build_schedule(g: CSRGraph, split_len: int) -> None:
         raise RuntimeError("kgx schedule: split list overflow")
     g.items = items[: g.n_items]
     g.split = split[: max(g.n_split, 0)]
+    g.n_long = short_suffix_start(g.items)
+
+
+SHORT_ROW_MAX = 7  # KGX_SHORT_ROW_MAX (include/kgx.h)
+
+
+def short_suffix_start(items: torch.Tensor) -> int:
+    """First item of the degree-descending schedule's suffix of unsplit rows of
+    degree <= SHORT_ROW_MAX (split rows' chunks are a prefix; rows come in
+    exactly descending degree after them).  KGX_SHORT_ROWS=0: no suffix."""
+    n = int(items.shape[0])
+    if n == 0 or os.environ.get("KGX_SHORT_ROWS", "1") in ("0", "false", "False"):
+        return n
+    smax = int(os.environ.get("KGX_SHORT_MAX", SHORT_ROW_MAX))  # experiment knob (the kernel takes any degree)
+    short = ((items[:, 2] - items[:, 1]) <= smax) & (items[:, 3] < 0)
+    # the suffix starts after the last item that is NOT short
+    not_short = torch.nonzero(~short)
+    return int(not_short[-1]) + 1 if not_short.numel() else 0
 
 
 def row_of_slot(g: CSRGraph) -> torch.Tensor:
@@ -265,6 +287,7 @@ def split_by_part(g: CSRGraph, part_of: torch.Tensor, sources: list, accumulate_
             empty = int((deg == 0).sum())  # one item each, last in the degree-descending schedule
             sub.n_items -= empty
             sub.items = sub.items[: sub.n_items]
+            sub.n_long = min(sub.n_long, sub.n_items)
             sub.extras["accumulate_only"] = True
         parts.append(sub)
     return parts

@@ -152,7 +152,7 @@ class sharing_gpu:
 
 
 def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale, save_agg,
-                    relu=False):
+                    relu=False, n_long=-1):
     x, w, W, bias = _f32c(x), _f32c(w), _f32c(W), _f32c(bias)
     dev = nat.require_device(x, rowptr, rows, idx, w, W, bias, items, split)
     n_dst = rowptr.numel() - 1
@@ -166,9 +166,10 @@ def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, b
     partials = None
     if items is not None and n_split > 0:
         partials = torch.empty((n_slots, x.shape[1]), dtype=torch.float32, device=dev)
+    n_long = n_items if n_long < 0 or n_long > n_items else n_long
     nat.check(
-        nat.lib().kgx_spmm_gemm(
-            reduce, nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, nat.ptr(split), n_split,
+        nat.lib().kgx_spmm_gemm_ex(
+            reduce, nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, n_long, nat.ptr(split), n_split,
             nat.ptr(idx), nat.ptr(w), nat.ptr(x), x.stride(0), x.shape[1], nat.ptr(W), F_out, nat.ptr(bias),
             int(pre_gin) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0) | (nat.FUSED_RELU if relu else 0),
             float(gin_scale), nat.ptr(out), out.stride(0),
@@ -196,13 +197,15 @@ def spmm_gemm(
     pre_gin: bool,
     gin_scale: float,
     relu: bool = False,
+    n_long: int = -1,
 ) -> torch.Tensor:
     return _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale,
-                           False, relu)[0]
+                           False, relu, n_long)[0]
 
 
 @spmm_gemm.register_fake
-def _spmm_gemm_fake(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale, relu=False):
+def _spmm_gemm_fake(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale, relu=False,
+                    n_long=-1):
     return x.new_empty((rowptr.shape[0] - 1, W.shape[1]))
 
 
@@ -221,13 +224,16 @@ def spmm_gemm_save(
     bias: Optional[torch.Tensor],
     pre_gin: bool,
     gin_scale: float,
+    n_long: int = -1,
 ) -> tuple[torch.Tensor, torch.Tensor]:
     """kgx::spmm_gemm that also returns the aggregated rows before the transform."""
-    return _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale, True)
+    return _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale, True,
+                           False, n_long)
 
 
 @spmm_gemm_save.register_fake
-def _spmm_gemm_save_fake(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale):
+def _spmm_gemm_save_fake(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale,
+                         n_long=-1):
     n = rowptr.shape[0] - 1
     return x.new_empty((n, W.shape[1])), x.new_empty((n, x.shape[1]))
 
@@ -246,6 +252,7 @@ def spmm_gemm_acc_(
     reduce: int,
     W: torch.Tensor,
     bias: Optional[torch.Tensor],
+    n_long: int = -1,
 ) -> None:
     """out += bias + REDUCE(...) @ W (KGX_FUSED_ACCUMULATE), in place."""
     x, w, W, bias = _f32c(x), _f32c(w), _f32c(W), _f32c(bias)
@@ -260,9 +267,10 @@ def spmm_gemm_acc_(
     partials = None
     if items is not None and n_split > 0:
         partials = torch.empty((n_slots, x.shape[1]), dtype=torch.float32, device=dev)
+    n_long = n_items if n_long < 0 or n_long > n_items else n_long
     nat.check(
-        nat.lib().kgx_spmm_gemm(
-            reduce, nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, nat.ptr(split), n_split,
+        nat.lib().kgx_spmm_gemm_ex(
+            reduce, nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, n_long, nat.ptr(split), n_split,
             nat.ptr(idx), nat.ptr(w), nat.ptr(x), x.stride(0), x.shape[1], nat.ptr(W), W.shape[1], nat.ptr(bias),
             nat.FUSED_ACCUMULATE, 1.0, nat.ptr(out), out.stride(0), nat.ptr(partials), None, 0, nat.stream(dev),
         ),
@@ -271,7 +279,7 @@ def spmm_gemm_acc_(
 
 
 @spmm_gemm_acc_.register_fake
-def _spmm_gemm_acc_fake(out, x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias):
+def _spmm_gemm_acc_fake(out, x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, n_long=-1):
     return None
 
 
@@ -595,7 +603,7 @@ def _aggregate_transform_raw(g, x, W, red, weighted, bias, pre_gin, gin_scale, e
         raise ValueError("graph was built without GCN normalisation weights")
     return _timed(lambda: torch.ops.kgx.spmm_gemm(
         x, g.rowptr, g.rows, items, split, g.col, w, n_slots, red, W, bias, bool(pre_gin), float(gin_scale),
-        bool(relu)
+        bool(relu), g.n_long if items is not None else -1
     ))
 
 
@@ -627,7 +635,8 @@ class _AggregateTransformFn(torch.autograd.Function):
         w = g.w if weighted else None
         if ctx.needs_input_grad[1]:  # keep P = PRE(A x) for dW (one extra row store instead of a recompute)
             out, P = _timed(lambda: torch.ops.kgx.spmm_gemm_save(
-                x, g.rowptr, g.rows, items, split, g.col, w, n_slots, red, W, bias, bool(pre_gin), float(gin_scale)))
+                x, g.rowptr, g.rows, items, split, g.col, w, n_slots, red, W, bias, bool(pre_gin), float(gin_scale),
+                g.n_long if items is not None else -1))
         else:
             out = _aggregate_transform_raw(g, x, W, red, weighted, bias, pre_gin, gin_scale, exact)
             P = None
@@ -691,7 +700,7 @@ def aggregate_transform(
         items, _, split, _, n_slots = g.work(exact)
         w = g.w if weighted else None
         _timed(lambda: torch.ops.kgx.spmm_gemm_acc_(out, x, g.rowptr, g.rows, items, split, g.col, w, n_slots, red,
-                                                   W, bias))
+                                                   W, bias, g.n_long if items is not None else -1))
         return out
     if _needs_grad(x, W, bias):
         y = _AggregateTransformFn.apply(x, W, bias, g, red, weighted, pre_gin, float(gin_scale), exact)

@@ -56,6 +56,8 @@ def csr_from_arrays(d: dict[str, np.ndarray], device: torch.device) -> G.CSRGrap
     )
     if g.rowptr.numel() != g.n_dst + 1 or g.col.numel() != g.kept or g.eid.numel() != g.kept:
         raise ValueError("kgx graph file: CSR array sizes do not match its meta row")
+    if g.items is not None:
+        g.n_long = G.short_suffix_start(g.items[: g.n_items])
     return g
 
 
