@@ -158,6 +158,16 @@ int kgx_spmm(int reduce, int epilogue,
              const float* bias, const float* xroot, int64_t ld_x, float gin_scale,
              const int32_t* drop_key, float drop_p, uint64_t drop_seed,
              float* partials, kgx_stream_t stream);
+/* kgx_spmm with the schedule's short-row suffix named: items [n_long_items,
+ * n_items) are unsplit rows of degree <= KGX_SHORT_ROW_MAX (defined below),
+ * taken several per lane group by a second kernel (not with message dropout
+ * or column slices wider than 64 lanes).  n_long_items = n_items is kgx_spmm. */
+int kgx_spmm_ex(int reduce, int epilogue, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
+                const int32_t* items, int64_t n_items, int64_t n_long_items, const int32_t* split,
+                int64_t n_split, const int32_t* idx, const float* w, const float* table, int64_t ld_table,
+                int64_t F, float* out, int64_t ld_out, const float* bias, const float* xroot, int64_t ld_x,
+                float gin_scale, const int32_t* drop_key, float drop_p, uint64_t drop_seed, float* partials,
+                kgx_stream_t stream);
 
 /* Message dropout mask (training; GCNConv.message dropout, gcn_conv.py:237-242;
  * GATv2 attention dropout, gatv2_conv.py:252-253): element (key, f) is kept

@@ -60,6 +60,7 @@ struct SpmmArgs {
   float drop_scale;
   int f_base;  // first column of this launch (column slicing of wide F)
   int long_rows;  // EXACT mode: rows of degree >= kLongRow are reduced by spmm_long_kernel
+  int64_t n_long;  // items [n_long, n_items): short rows (degree <= KGX_SHORT_ROW_MAX) for spmm_short_kernel
 };
 
 // EXACT mode has no hub split (each row is one sequential reduction), so a hub
@@ -184,7 +185,7 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
   const int G = a.G;
   const int lane = threadIdx.x & (G - 1);
   const int64_t ngroups = (int64_t(gridDim.x) * kBlock) >> a.lgG;
-  const int64_t n_work = a.items ? a.n_items : a.n_rows;
+  const int64_t n_work = a.items ? a.n_long : a.n_rows;
 
   // Every global load below is unconditional (clamped to a valid address) and
   // masked work is folded in as the reduction's identity: a load under a
@@ -278,6 +279,118 @@ __global__ __launch_bounds__(kBlock) void spmm_long_kernel(SpmmArgs a) {
   }
 }
 
+// The schedule's suffix of unsplit rows of degree <= KGX_SHORT_ROW_MAX (78 %
+// of an R-MAT graph's rows, 11 % of its edges).  spmm_kernel's groups take one
+// row per item, so on these rows a group has one or two gathers in flight and
+// each row pays a chain of dependent loads (item, index, row) for 0.5-4 KB:
+// NS rows of degree <= 7 ran at 5.1 TB/s against 7.7 TB/s for the rest
+// (tools/exp_lowdeg.py spmm).  Here a group takes kSR consecutive items and
+// gathers the first kSPF edges of all of them together (exec-masked by
+// degree), the rest in pairs, each row still reduced in its CSR order.
+#ifndef KGX_SPMM_SHORT_R
+#define KGX_SPMM_SHORT_R 4
+#endif
+#ifndef KGX_SPMM_SHORT_PF
+#define KGX_SPMM_SHORT_PF 2
+#endif
+constexpr int kSR = KGX_SPMM_SHORT_R;
+constexpr int kSPF = KGX_SPMM_SHORT_PF;
+
+template <int VEC, int RED, bool WEIGHTED>
+__global__ __launch_bounds__(kBlock) void spmm_short_kernel(SpmmArgs a) {
+  using R = Reducer<RED>;
+  const int G = a.G;
+  const int lane = threadIdx.x & (G - 1);
+  const int64_t ngroups = (int64_t(gridDim.x) * kBlock) >> a.lgG;
+  const int fo = lane * VEC;
+  const bool fv = fo < a.F;
+  const int fl = fv ? fo : a.F - VEC;
+  const int64_t n_short = a.n_items - a.n_long;
+  for (int64_t q = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> a.lgG; q * kSR < n_short; q += ngroups) {
+    int32_t row[kSR], beg[kSR], deg[kSR];
+#pragma unroll
+    for (int r = 0; r < kSR; ++r) {
+      const int64_t it = a.n_long + q * kSR + r;
+      row[r] = -1;
+      beg[r] = 0;
+      deg[r] = 0;
+      if (it < a.n_items) {
+        const int4 v = a.items[it];
+        row[r] = v.x;
+        beg[r] = v.y;
+        deg[r] = v.z - v.y;
+      }
+    }
+    float acc[kSR][VEC];
+    {
+      int32_t c[kSR][kSPF];
+      float wt[kSR][kSPF];
+#pragma unroll
+      for (int r = 0; r < kSR; ++r)
+#pragma unroll
+        for (int u = 0; u < kSPF; ++u) {
+          const int32_t ee = deg[r] > 0 ? beg[r] + (u < deg[r] ? u : deg[r] - 1) : 0;
+          c[r][u] = a.idx[ee];
+          if constexpr (WEIGHTED) wt[r][u] = a.w[ee];
+        }
+      float v[kSR][kSPF][VEC];
+#pragma unroll
+      for (int r = 0; r < kSR; ++r)
+#pragma unroll
+        for (int u = 0; u < kSPF; ++u)
+          if (u < deg[r]) vload<VEC>(v[r][u], a.table + row_off(c[r][u], a.ld_t) + fl);
+#pragma unroll
+      for (int r = 0; r < kSR; ++r)
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+          float t = R::init();
+#pragma unroll
+          for (int u = 0; u < kSPF; ++u) {
+            float m = v[r][u][k];
+            if constexpr (WEIGHTED) m = __fmul_rn(m, wt[r][u]);
+            t = R::combine(t, u < deg[r] ? R::msg(m) : R::init());
+          }
+          acc[r][k] = t;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < kSR; ++r) {
+      for (int32_t e = kSPF; e < deg[r]; e += 2) {
+        const int n = deg[r] - e;
+        int32_t c[2];
+        float wt[2], v[2][VEC];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int32_t ee = beg[r] + e + (u < n ? u : n - 1);
+          c[u] = a.idx[ee];
+          if constexpr (WEIGHTED) wt[u] = a.w[ee];
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) vload<VEC>(v[u], a.table + row_off(c[u], a.ld_t) + fl);
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int k = 0; k < VEC; ++k) {
+            float m = v[u][k];
+            if constexpr (WEIGHTED) m = __fmul_rn(m, wt[u]);
+            acc[r][k] = R::combine(acc[r][k], u < n ? R::msg(m) : R::init());
+          }
+      }
+    }
+    if (!fv) continue;
+#pragma unroll
+    for (int r = 0; r < kSR; ++r) {
+      if (row[r] < 0) continue;
+      float o[VEC];
+#pragma unroll
+      for (int k = 0; k < VEC; ++k)
+        o[k] = a.epi == KGX_EPI_RAW ? R::finish_raw(acc[r][k], deg[r]) : R::finish(acc[r][k], deg[r]);
+      epilogue<VEC>(a, row[r], fo, o);
+      vstore<VEC>(a.out + int64_t(row[r]) * a.ld_o + fo, o);
+    }
+  }
+}
+
 // Combine the chunk partials of split rows in chunk order, then finish.
 template <int VEC, int NT, int RED>
 __global__ __launch_bounds__(kBlock) void spmm_fixup_kernel(SpmmArgs a) {
@@ -368,7 +481,6 @@ __global__ __launch_bounds__(kBlock) void spmm_std_kernel(SpmmArgs a) {
 template <int VEC, int NT, int RED, bool W>
 int launch_main(const SpmmArgs& a_in, hipStream_t s) {
   SpmmArgs a = a_in;
-  const int64_t work = a.items ? a.n_items : a.n_rows;
   if constexpr (NT == 1) {
     if (!a.items && a.n_rows > 0) {  // EXACT: long rows first, on their own kernel
       a.long_rows = 1;
@@ -381,12 +493,25 @@ int launch_main(const SpmmArgs& a_in, hipStream_t s) {
       KGX_CHECK_LAUNCH();
     }
   }
-  if (work > 0) {
+  if constexpr (NT == 1) {
+    if (a.items && a.n_long < a.n_items && !a.drop_key) {
+      auto ks = spmm_short_kernel<VEC, RED, W>;
+      hipLaunchKernelGGL(ks, dim3(resident_grid(ks, (a.n_items - a.n_long + kSR - 1) / kSR, a.G)), dim3(kBlock), 0, s,
+                         a);
+      KGX_CHECK_LAUNCH();
+    } else {
+      a.n_long = a.n_items;
+    }
+  } else {
+    a.n_long = a.n_items;
+  }
+  const int64_t work_long = a.items ? a.n_long : a.n_rows;
+  if (work_long > 0) {
     auto k = spmm_kernel<VEC, NT, RED, W>;
     if constexpr (RED == KGX_SUM) {
       if (a.drop_key) k = spmm_kernel<VEC, NT, RED, W, true>;
     }
-    hipLaunchKernelGGL(k, dim3(resident_grid(k, work, a.G)), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(k, dim3(resident_grid(k, work_long, a.G)), dim3(kBlock), 0, s, a);
     KGX_CHECK_LAUNCH();
   }
   if (a.items && a.n_split > 0) {
@@ -444,7 +569,20 @@ extern "C" int kgx_spmm(int reduce, int epilogue, const int32_t* rowptr, const i
                         float* out, int64_t ld_out, const float* bias, const float* xroot, int64_t ld_x,
                         float gin_scale, const int32_t* drop_key, float drop_p, uint64_t drop_seed,
                         float* partials, kgx_stream_t stream_) {
+  return kgx_spmm_ex(reduce, epilogue, rowptr, rows, n_rows, items, n_items, n_items, split, n_split, idx, w, table,
+                     ld_table, F, out, ld_out, bias, xroot, ld_x, gin_scale, drop_key, drop_p, drop_seed, partials,
+                     stream_);
+}
+
+extern "C" int kgx_spmm_ex(int reduce, int epilogue, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
+                           const int32_t* items, int64_t n_items, int64_t n_long_items, const int32_t* split,
+                           int64_t n_split, const int32_t* idx, const float* w, const float* table, int64_t ld_table,
+                           int64_t F, float* out, int64_t ld_out, const float* bias, const float* xroot,
+                           int64_t ld_x, float gin_scale, const int32_t* drop_key, float drop_p, uint64_t drop_seed,
+                           float* partials, kgx_stream_t stream_) {
   hipStream_t stream = as_stream(stream_);
+  KGX_REQUIRE(!items || (n_long_items >= 0 && n_long_items <= n_items), KGX_ERR_ARG,
+              "kgx_spmm: n_long_items must lie in [0, n_items]");
   KGX_REQUIRE(reduce >= KGX_SUM && reduce <= KGX_STD, KGX_ERR_ARG, "kgx_spmm: unknown reduce %d", reduce);
   KGX_REQUIRE(epilogue >= KGX_EPI_NONE && epilogue <= KGX_EPI_ACCUM, KGX_ERR_ARG, "kgx_spmm: unknown epilogue %d",
               epilogue);
@@ -472,6 +610,7 @@ extern "C" int kgx_spmm(int reduce, int epilogue, const int32_t* rowptr, const i
   a.n_items = use_items ? n_items : 0;
   a.split = reinterpret_cast<const int4*>(split);
   a.n_split = use_items ? n_split : 0;
+  a.n_long = use_items ? n_long_items : 0;
   a.idx = idx;
   a.w = w;
   a.epi = epilogue;

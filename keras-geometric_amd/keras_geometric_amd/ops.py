@@ -45,6 +45,7 @@ def spmm(
     drop_key: Optional[torch.Tensor] = None,
     drop_p: float = 0.0,
     drop_seed: int = 0,
+    n_long: int = -1,
 ) -> torch.Tensor:
     table = _f32c(table)
     w, bias, xroot = _f32c(w), _f32c(bias), _f32c(xroot)
@@ -59,10 +60,11 @@ def spmm(
     partials = None
     if items is not None and n_split > 0 and reduce != nat.STD:
         partials = torch.empty((n_slots, F), dtype=torch.float32, device=dev)
+    n_long = n_items if n_long < 0 or n_long > n_items else n_long
     nat.check(
-        nat.lib().kgx_spmm(
+        nat.lib().kgx_spmm_ex(
             reduce, epilogue, nat.ptr(rowptr), nat.ptr(rows), n_dst,
-            nat.ptr(items), n_items, nat.ptr(split), n_split,
+            nat.ptr(items), n_items, n_long, nat.ptr(split), n_split,
             nat.ptr(idx), nat.ptr(w), nat.ptr(table), table.stride(0), F,
             nat.ptr(out), out.stride(0),
             nat.ptr(bias), nat.ptr(xroot), xroot.stride(0) if xroot is not None else 0, float(gin_scale),
@@ -76,7 +78,7 @@ def spmm(
 
 @spmm.register_fake
 def _spmm_fake(table, rowptr, rows, items, split, idx, w, n_slots, reduce, epilogue, bias, xroot, gin_scale,
-               drop_key=None, drop_p=0.0, drop_seed=0):
+               drop_key=None, drop_p=0.0, drop_seed=0, n_long=-1):
     return table.new_empty((rowptr.shape[0] - 1, table.shape[1]))
 
 
@@ -91,6 +93,7 @@ def spmm_acc_(
     idx: torch.Tensor,
     w: Optional[torch.Tensor],
     n_slots: int,
+    n_long: int = -1,
 ) -> None:
     """out[i] += SUM_{e in row i} table[idx[e]] (* w[e]) in place (KGX_EPI_ACCUM)."""
     table, w = _f32c(table), _f32c(w)
@@ -106,10 +109,11 @@ def spmm_acc_(
     partials = None
     if items is not None and n_split > 0:
         partials = torch.empty((n_slots, F), dtype=torch.float32, device=dev)
+    n_long = n_items if n_long < 0 or n_long > n_items else n_long
     nat.check(
-        nat.lib().kgx_spmm(
+        nat.lib().kgx_spmm_ex(
             nat.SUM, nat.EPI_ACCUM, nat.ptr(rowptr), nat.ptr(rows), n_dst,
-            nat.ptr(items), n_items, nat.ptr(split), n_split,
+            nat.ptr(items), n_items, n_long, nat.ptr(split), n_split,
             nat.ptr(idx), nat.ptr(w), nat.ptr(table), table.stride(0), F,
             nat.ptr(out), out.stride(0), None, None, 0, 1.0, None, 0.0, 0, nat.ptr(partials), nat.stream(dev),
         ),
@@ -118,7 +122,7 @@ def spmm_acc_(
 
 
 @spmm_acc_.register_fake
-def _spmm_acc_fake(out, table, rowptr, rows, items, split, idx, w, n_slots):
+def _spmm_acc_fake(out, table, rowptr, rows, items, split, idx, w, n_slots, n_long=-1):
     return None
 
 
@@ -132,7 +136,8 @@ def aggregate_accumulate(g: CSRGraph, table: torch.Tensor, out: torch.Tensor, *,
     w = g.w if weighted else None
     if weighted and w is None:
         raise ValueError("graph was built without edge weights")
-    _timed(lambda: torch.ops.kgx.spmm_acc_(out, table, g.rowptr, g.rows, items, split, g.col, w, n_slots))
+    _timed(lambda: torch.ops.kgx.spmm_acc_(out, table, g.rowptr, g.rows, items, split, g.col, w, n_slots,
+                                           g.n_long if items is not None else -1))
     return out
 
 
@@ -460,7 +465,7 @@ def _aggregate_raw(g, table, red, weighted, by_edge, epilogue, bias, xroot, gin_
         raise ValueError("message dropout is implemented for sum aggregation (GCNConv) only")
     return _timed(lambda: torch.ops.kgx.spmm(
         table, g.rowptr, g.rows, items, split, idx, w, n_slots, red, epilogue, bias, xroot, float(gin_scale),
-        g.eid if drop_p > 0 else None, float(drop_p), int(drop_seed),
+        g.eid if drop_p > 0 else None, float(drop_p), int(drop_seed), g.n_long if items is not None else -1,
     ))
 
 

@@ -49,6 +49,13 @@ def main(n=10_000_000, e=100_000_000, f=128):
         return torch.ops.kgx.spmm_gemm(x, g.rowptr, g.rows, its.contiguous(), g.split if n_split else None,
                                       g.col, g.w, g.n_slots, 0, W, None, False, 1.0, False)
 
+    def run_spmm(its):  # the plain weighted aggregation (kgx_spmm) over the same items
+        n_split = g.n_split if split_items and its.shape[0] and int(its[0, 3]) >= 0 else 0
+        return torch.ops.kgx.spmm(x, g.rowptr, g.rows, its.contiguous(), g.split if n_split else None, g.col, g.w,
+                                  g.n_slots, 0, 0, None, None, 1.0)
+
+    if len(sys.argv) > 1 and sys.argv[1] == "spmm":
+        run = run_spmm  # noqa: F811
     full = timeit(lambda: run(items))
     out = {"full_ms": full, "items": items.shape[0]}
     for d in (1, 3, 7, 15):  # log2-bucket boundaries: rows of degree <= d are a suffix of the schedule
