@@ -54,8 +54,7 @@ inline unsigned grid_for(int64_t work_threads, int64_t cap_blocks = 2048) {
 
 // Grid for a persistent grid-stride launch: as many blocks as are resident at
 // once (occupancy x CUs), never more than the work needs.
-template <typename Kern>
-unsigned resident_grid(Kern kernel, int64_t groups_needed, int G) {
+inline int cu_count() {
   static int cus = 0;
   if (cus == 0) {
     int dev = 0;
@@ -63,6 +62,12 @@ unsigned resident_grid(Kern kernel, int64_t groups_needed, int G) {
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
       cus = 256;
   }
+  return cus;
+}
+
+template <typename Kern>
+unsigned resident_grid(Kern kernel, int64_t groups_needed, int G) {
+  const int cus = cu_count();
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0) != hipSuccess || per_cu <= 0)
     per_cu = 4;

@@ -279,6 +279,215 @@ __global__ __launch_bounds__(kBlock) void spmm_long_kernel(SpmmArgs a) {
   }
 }
 
+// EXACT-mode rows of degree >= kLongRow, one 16-wave block per row.  Such a
+// row is one chain of adds in CSR order that no split may re-associate, and
+// spmm_long_kernel walks it with one 32-lane group (32 gathers in flight): the
+// NS graph's largest row (138k edges) alone took 9.3 ms.  Here producer waves
+// stream the row's messages (neighbour row x weight, rounded as the reference
+// rounds them) into a two-stage LDS ring, kHubD stages of gathers in flight
+// per lane, and CW consumer waves fold each stage in edge order, one feature
+// per lane -- the same per-(row, feature) operation sequence, bit for bit.
+// The gathers and their index / weight loads are inline-asm loads with
+// counted vmcnt waits: the compiler's accounting would wait for the whole
+// queue whenever an index it loaded is used.
+#ifndef KGX_HUB_D
+#define KGX_HUB_D 8
+#endif
+// timing experiments: bit 0 skips the consumers' fold, bit 2 adds a barrier
+// per iteration.  (Never drop the gathers: the batch loads' completion is
+// proved by the gathers issued after them, see the vmcnt comment below.)
+#ifndef KGX_HUB_DEBUG
+#define KGX_HUB_DEBUG 0
+#endif
+constexpr int kHubThreads = 1024;
+constexpr int kHubD = KGX_HUB_D;
+
+__device__ __forceinline__ void hub_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int G, int RED, bool WEIGHTED>
+__global__ __launch_bounds__(kHubThreads, 1) void spmm_hub_kernel(SpmmArgs a) {
+  using R = Reducer<RED>;
+  constexpr int CW = G >= 16 ? G / 16 : 1;  // consumer waves (64 features each)
+  constexpr int NPW = kHubThreads / 64 - CW;  // producer waves
+  constexpr int RPW = 64 / G;                 // rows per producer wave per stage
+  // rows (edges) per stage; a consumer lane holds two stages in registers, so
+  // at most 32 (narrow rows leave producer waves idle)
+  constexpr int S = NPW * RPW < 32 ? NPW * RPW : 32;
+  constexpr int RL = 4 * G;                   // floats per ring row
+  constexpr int D = kHubD;
+  __shared__ __attribute__((aligned(16))) float ring[3][S * RL];
+
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63;
+
+  // Row h of the degree-ordered list; false past the long rows.  Iteration s
+  // of a row: producers write stage s into ring[s % 3]; consumers read stage
+  // s-1 into registers and fold stage s-2 (read one iteration earlier).
+  // Consumers and producers run separate copies of the row loop (same rows,
+  // same iteration counts, one barrier per iteration) so that neither's
+  // loop-invariant values occupy the other's registers.
+  static_assert(D % 2 == 0, "consumer iterations come in pairs");
+#define KGX_HUB_ROW(h)                                                  \
+  const int32_t row = a.rows[h];                                        \
+  const int32_t beg = a.rowptr[row], end = a.rowptr[row + 1];           \
+  if (end - beg < kLongRow) break; /* rows come in descending degree */ \
+  const int32_t n_st = (end - beg + S - 1) / S;                         \
+  const int32_t n_iter = (n_st + 2 + 2 * D - 1) / (2 * D) * (2 * D);
+
+  if (wave < CW) {  // ---- consumers
+    for (int64_t h = blockIdx.x; h < a.n_rows; h += gridDim.x) {
+      KGX_HUB_ROW(h)
+      const int f = wave * 64 + lane;
+      const int fc = f < RL ? f : RL - 1;
+      float acc = R::init();
+      float va[S], vb[S];
+      auto rd = [&](float(&v)[S], int32_t t) {
+        const float* rb = &ring[t % 3][fc];
+#pragma unroll
+        for (int i = 0; i < S; ++i) v[i] = rb[i * RL];
+      };
+      auto fold = [&](const float(&v)[S], int32_t t) {
+        if (t == n_st - 1) {  // the row's last stage: slots past `end` hold clamped duplicates
+          const int32_t n = end - beg - t * S;
+#pragma unroll
+          for (int i = 0; i < S; ++i) acc = R::combine(acc, i < n ? v[i] : R::init());  // init(): exact identity
+        } else {
+#pragma unroll
+          for (int i = 0; i < S; ++i) acc = R::combine(acc, v[i]);
+        }
+      };
+      for (int32_t s = 0; s < n_iter; s += 2) {
+        if (s >= 1 && s - 1 < n_st) rd(va, s - 1);
+        __builtin_amdgcn_sched_barrier(0);  // the reads fly while the previous stage folds
+#if !(KGX_HUB_DEBUG & 1)  // timing experiment: no fold
+        if (s >= 2 && s - 2 < n_st) fold(vb, s - 2);
+#endif
+        hub_barrier();
+        if (s < n_st) rd(vb, s);
+        __builtin_amdgcn_sched_barrier(0);
+#if !(KGX_HUB_DEBUG & 1)
+        if (s >= 1 && s - 1 < n_st) fold(va, s - 1);
+#endif
+        hub_barrier();
+#if KGX_HUB_DEBUG & 4
+        hub_barrier();
+        hub_barrier();
+#endif
+      }
+      if (f < a.F) {
+        float r[1] = {a.epi == KGX_EPI_RAW ? R::finish_raw(acc, end - beg) : R::finish(acc, end - beg)};
+        epilogue<1>(a, row, f, r);
+        vstore<1>(a.out + int64_t(row) * a.ld_o + f, r);
+      }
+    }
+    return;
+  }
+
+  // ---- producers: lane (slot r, features f..f+3) of every stage
+  for (int64_t h = blockIdx.x; h < a.n_rows; h += gridDim.x) {
+    KGX_HUB_ROW(h)
+    const int slot = (wave - CW) * RPW + lane / G;
+    if (__builtin_amdgcn_readfirstlane(slot) >= S) {  // idle producer wave: barriers only
+      for (int32_t s = 0; s < n_iter; ++s) hub_barrier();
+      continue;
+    }
+    const int f = (lane % G) * 4;
+    const int fl = f < a.F ? f : a.F - 4;  // lanes past F load (and write) a valid duplicate
+    const float* tab = a.table + fl;
+    float* lds_row = &ring[0][slot * RL + f];
+    auto edge = [&](int32_t t) {  // stage t's edge of this slot, clamped into the row
+      const int32_t e = beg + t * S + slot;
+      return e < end ? e : end - 1;
+    };
+    int32_t ci[2][D];  // index batches: stages of chunk c in set c & 1
+    f32x4_t gv[D];     // gathers in flight: stage t in gv[t % D]
+    float wr[D];       // ... and their weights, loaded with them
+    auto batch = [&](int set, int32_t chunk) {
+#pragma unroll
+      for (int j = 0; j < D; ++j) {
+        const int32_t* pi = a.idx + edge(chunk * D + j);
+        asm volatile("global_load_dword %0, %1, off" : "=v"(ci[set][j]) : "v"(pi) : "memory");
+      }
+    };
+    auto gather = [&](int j, int32_t t, int32_t c) {  // weight, then row, of stage t
+      if constexpr (WEIGHTED) {
+        const float* pw = a.w + edge(t);
+        asm volatile("global_load_dword %0, %1, off" : "=v"(wr[j]) : "v"(pw) : "memory");
+      }
+      const float* p = tab + row_off(c, a.ld_t);
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(gv[j]) : "v"(p) : "memory");
+    };
+    auto pin_batch = [&](int set) {
+#pragma unroll
+      for (int j = 0; j < D; ++j) asm volatile("" : "+v"(ci[set][j]));
+    };
+    // vector-memory ops per iteration (weight + row) and the vmcnt waits:
+    // stage s's row load is the oldest we need; newer are the D-1 later
+    // iterations' loads, plus (after the chunk's first iteration) its batch
+    constexpr int OPI = WEIGHTED ? 2 : 1;
+    static_assert(OPI * (D - 1) + D <= 63, "vmcnt immediate");
+    // prologue: index batches of chunks 0 and 1, then the loads of stages 0..D-1
+    batch(0, 0);
+    batch(1, 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pin_batch(0);
+    pin_batch(1);
+#pragma unroll
+    for (int j = 0; j < D; ++j) gather(j, j, ci[0][j]);
+    // one chunk = D iterations; during chunk k the set holding chunk k+1's
+    // indices issues the loads of stages (k+1)D.., and the other set is
+    // refilled with chunk k+2 at the chunk's first iteration
+    auto chunk = [&](int32_t k, auto use_c) {
+      constexpr int use = decltype(use_c)::value, fill = 1 - use;
+#pragma unroll
+      for (int j = 0; j < D; ++j) {
+        const int32_t s = k * D + j;
+        if (j == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPI * (D - 1)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPI * (D - 1) + D) : "memory");
+        asm volatile("" : "+v"(gv[j]));
+        if constexpr (WEIGHTED) asm volatile("" : "+v"(wr[j]));
+        {
+          f32x4_t m;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) m[q] = R::msg(WEIGHTED ? __fmul_rn(gv[j][q], wr[j]) : gv[j][q]);
+          *reinterpret_cast<f32x4_t*>(lds_row + (s % 3) * (S * RL)) = m;
+        }
+        if (j == 0) batch(fill, k + 2);
+        gather(j, s + D, ci[use][j]);
+        hub_barrier();
+#if KGX_HUB_DEBUG & 4  // timing experiment: a second barrier per iteration
+        hub_barrier();
+#endif
+      }
+      // the batch issued at j = 0 has landed (only this chunk's loads are
+      // newer): the compiler may copy its registers at the loop's back edge
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPI * D) : "memory");
+      pin_batch(fill);
+    };
+    // one exit, at the bottom, where the in-flight registers are exactly
+    // those of the back edge (an exit between the two chunks made hipcc
+    // shuffle still-loading registers)
+    for (int32_t k = 0; k * D < n_iter; k += 2) {
+      chunk(k, std::integral_constant<int, 1>{});
+      chunk(k + 1, std::integral_constant<int, 0>{});
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no loads in flight past the row
+    // Keep every asm-load destination live up to that wait: the last chunk's
+    // loads are never consumed, and a dead destination register could be
+    // handed to other code while its load is still in flight.
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      asm volatile("" ::"v"(gv[j]), "v"(ci[0][j]), "v"(ci[1][j]));
+      if constexpr (WEIGHTED) asm volatile("" ::"v"(wr[j]));
+    }
+  }
+#undef KGX_HUB_ROW
+}
+
 // The schedule's suffix of unsplit rows of degree <= KGX_SHORT_ROW_MAX (78 %
 // of an R-MAT graph's rows, 11 % of its edges).  spmm_kernel's groups take one
 // row per item, so on these rows a group has one or two gathers in flight and
@@ -482,7 +691,20 @@ template <int VEC, int NT, int RED, bool W>
 int launch_main(const SpmmArgs& a_in, hipStream_t s) {
   SpmmArgs a = a_in;
   if constexpr (NT == 1) {
-    if (!a.items && a.n_rows > 0) {  // EXACT: long rows first, on their own kernel
+    static const bool hub_off = [] {
+      const char* h = getenv("KGX_HUB");
+      return h && atoi(h) == 0;
+    }();
+    if (VEC == 4 && !a.items && a.n_rows > 0 && !a.drop_key && a.G >= 8 && !hub_off) {
+      a.long_rows = 1;  // EXACT: long rows first, one block per row
+      auto kh = spmm_hub_kernel<64, RED, W>;
+      if (a.G == 32) kh = spmm_hub_kernel<32, RED, W>;
+      else if (a.G == 16) kh = spmm_hub_kernel<16, RED, W>;
+      else if (a.G == 8) kh = spmm_hub_kernel<8, RED, W>;
+      const int64_t nb = a.n_rows < cu_count() ? a.n_rows : cu_count();  // one resident block per CU
+      hipLaunchKernelGGL(kh, dim3(unsigned(nb)), dim3(kHubThreads), 0, s, a);
+      KGX_CHECK_LAUNCH();
+    } else if (!a.items && a.n_rows > 0) {  // EXACT: long rows first, on their own kernel
       a.long_rows = 1;
       auto kl = spmm_long_kernel<VEC, RED, W>;
       if constexpr (RED == KGX_SUM) {

@@ -217,6 +217,42 @@ def test_feature_widths(dev, F):
                R.propagate(T(x), R.add_self_loops(T(np.stack([s, d])), N), "mean").numpy())
 
 
+def _hub_graph(N=6000, seed=11):
+    """R-MAT background plus hub rows of degree 2048 .. 40000 (EXACT mode's
+    one-block-per-row kernel, spmm_hub_kernel, takes degree >= 2048)."""
+    rng = np.random.default_rng(seed)
+    s, d = rmat_edges(seed, scale_for(N), N, 0, 20000)
+    hs, hd = [s], [d]
+    for h, deg in zip((5, 17, 400, 2999), (40000, 2048, 9001, 2500)):
+        hs.append(rng.integers(0, N, deg).astype(np.int32))
+        hd.append(np.full(deg, h, np.int32))
+    return np.stack([np.concatenate(hs), np.concatenate(hd)]), N
+
+
+@pytest.mark.parametrize("F", [24, 64, 100, 128, 256])
+def test_exact_hub_rows_bit_identical(dev, F):
+    """Hub rows (one block per row, messages staged through LDS) reduce in CSR
+    order bit for bit: sum / mean / max / min, weighted (GCN norm) and
+    unweighted, with NaN / inf / -0 among the messages."""
+    ei, N = _hub_graph()
+    x = np.random.default_rng(F).standard_normal((N, F)).astype(np.float32)
+    x[7, 0], x[8, 1 % F], x[9, 2 % F], x[10, :] = np.nan, np.inf, -np.inf, -0.0
+    csr = build(ei, N, dev)
+    assert int(csr.deg.max()) >= 40000
+    xt = T(x)
+    xd = xt.to(dev)
+    for aggr in ("sum", "mean", "max", "min"):
+        exact(kops.aggregate(csr, xd, aggr, exact=True).cpu(), R.propagate(xt, T(ei), aggr))
+    gcsr = build(ei, N, dev, self_loops=True, gcn_norm=True)
+    out = kops.aggregate(gcsr, xd, "sum", weighted=True, exact=True).cpu()
+    rows = torch.repeat_interleave(torch.arange(N), gcsr.deg.cpu().long())
+    ref = K.segment_sum(xt[gcsr.col.cpu().long()] * gcsr.w.cpu().unsqueeze(1), rows, N)
+    exact(out, ref)
+    h = kops.aggregate(csr, xd, "max", epilogue=nat.EPI_GIN, xroot=xd, gin_scale=1.25, exact=True).cpu()
+    agg = R.propagate(xt, T(ei), "max")
+    exact(h, torch.tensor(1.25, dtype=torch.float32) * xt + agg)
+
+
 def test_nan_inf_signed_zero(dev, golden):
     e = golden("edge_cases")
     for kind in ("nan", "inf"):
