@@ -299,11 +299,36 @@ __global__ __launch_bounds__(kBlock) void spmm_long_kernel(SpmmArgs a) {
 #ifndef KGX_HUB_DEBUG
 #define KGX_HUB_DEBUG 0
 #endif
+#ifndef KGX_HUB_PRIO
+#define KGX_HUB_PRIO 0
+#endif
+#ifndef KGX_HUB_READER_WAIT
+#define KGX_HUB_READER_WAIT 0
+#endif
+#ifndef KGX_HUB_RPL
+#define KGX_HUB_RPL 2
+#endif
 constexpr int kHubThreads = 1024;
-constexpr int kHubD = KGX_HUB_D;
+constexpr int kHubD = KGX_HUB_D;      // rows in flight per producer lane
+constexpr int kHubRPL = KGX_HUB_RPL;  // rows per producer lane per stage
+constexpr int kHubSMax = 56;
+#ifndef KGX_HUB_G
+#define KGX_HUB_G 16
+#endif
+constexpr int kHubG = KGX_HUB_G;  // hub column group: 4 x kHubG features
 
 __device__ __forceinline__ void hub_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+// The consumers' side: their LDS reads of stage s-1 need not land before the
+// barrier (producers overwrite that buffer two barriers later, and the reads
+// are waited for by the fold one iteration later), so no lgkmcnt(0) here.
+__device__ __forceinline__ void hub_barrier_reader() {
+#if KGX_HUB_READER_WAIT
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }
@@ -313,12 +338,15 @@ __global__ __launch_bounds__(kHubThreads, 1) void spmm_hub_kernel(SpmmArgs a) {
   using R = Reducer<RED>;
   constexpr int CW = G >= 16 ? G / 16 : 1;  // consumer waves (64 features each)
   constexpr int NPW = kHubThreads / 64 - CW;  // producer waves
-  constexpr int RPW = 64 / G;                 // rows per producer wave per stage
-  // rows (edges) per stage; a consumer lane holds two stages in registers, so
-  // at most 32 (narrow rows leave producer waves idle)
-  constexpr int S = NPW * RPW < 32 ? NPW * RPW : 32;
+  constexpr int RPW = 64 / G;                 // rows per producer wave per pass
+  // a consumer lane holds two stages in registers: at most kHubSMax rows per
+  // stage (a multiple of RPW, so narrow rows leave whole producer waves idle)
+  constexpr int SP = NPW * RPW < kHubSMax ? NPW * RPW : kHubSMax;  // producer slots
+  constexpr int RPL = SP * kHubRPL <= kHubSMax ? kHubRPL : 1;       // rows per slot per stage
+  constexpr int S = SP * RPL;                 // rows (edges) per stage
   constexpr int RL = 4 * G;                   // floats per ring row
-  constexpr int D = kHubD;
+  constexpr int D = kHubD / RPL;              // stages of loads in flight (D x RPL rows per lane)
+  static_assert(kHubSMax % 8 == 0 && D >= 2 && D % 2 == 0, "hub pipeline shape");
   __shared__ __attribute__((aligned(16))) float ring[3][S * RL];
 
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
@@ -331,7 +359,15 @@ __global__ __launch_bounds__(kHubThreads, 1) void spmm_hub_kernel(SpmmArgs a) {
   // same iteration counts, one barrier per iteration) so that neither's
   // loop-invariant values occupy the other's registers.
   static_assert(D % 2 == 0, "consumer iterations come in pairs");
-#define KGX_HUB_ROW(h)                                                  \
+  // A row's features are independent chains: the row is split into column
+  // groups of FW features, one block each, so a hub row's bytes spread over
+  // ncg CUs (one CU moves ~50-60 GB/s through this pipeline).
+  constexpr int FW = 4 * G;
+  const int ncg = (a.F + FW - 1) / FW;
+#define KGX_HUB_ROW(p)                                                  \
+  const int64_t h = (p) / ncg;                                          \
+  const int c0 = int((p) % ncg) * FW; /* first column of the group */   \
+  const int fw = a.F - c0 < FW ? a.F - c0 : FW;                         \
   const int32_t row = a.rows[h];                                        \
   const int32_t beg = a.rowptr[row], end = a.rowptr[row + 1];           \
   if (end - beg < kLongRow) break; /* rows come in descending degree */ \
@@ -339,11 +375,19 @@ __global__ __launch_bounds__(kHubThreads, 1) void spmm_hub_kernel(SpmmArgs a) {
   const int32_t n_iter = (n_st + 2 + 2 * D - 1) / (2 * D) * (2 * D);
 
   if (wave < CW) {  // ---- consumers
-    for (int64_t h = blockIdx.x; h < a.n_rows; h += gridDim.x) {
-      KGX_HUB_ROW(h)
+#if KGX_HUB_PRIO
+    __builtin_amdgcn_s_setprio(3);  // the fold chain is the row's critical path
+#endif
+    for (int64_t p = blockIdx.x; p < a.n_rows * ncg; p += gridDim.x) {
+      KGX_HUB_ROW(p)
       const int f = wave * 64 + lane;
       const int fc = f < RL ? f : RL - 1;
       float acc = R::init();
+      // Iteration s reads stage s-1 into registers (one LDS read per two
+      // edges) and folds stage s-2, read one iteration earlier, so the LDS
+      // latency stays behind the add chain.  (Streaming the fold through a
+      // short register ring -- one read per edge -- measured 1.7x slower:
+      // the consumer wave is bound by its LDS instruction issue.)
       float va[S], vb[S];
       auto rd = [&](float(&v)[S], int32_t t) {
         const float* rb = &ring[t % 3][fc];
@@ -366,70 +410,78 @@ __global__ __launch_bounds__(kHubThreads, 1) void spmm_hub_kernel(SpmmArgs a) {
 #if !(KGX_HUB_DEBUG & 1)  // timing experiment: no fold
         if (s >= 2 && s - 2 < n_st) fold(vb, s - 2);
 #endif
-        hub_barrier();
+        hub_barrier_reader();
         if (s < n_st) rd(vb, s);
         __builtin_amdgcn_sched_barrier(0);
 #if !(KGX_HUB_DEBUG & 1)
         if (s >= 1 && s - 1 < n_st) fold(va, s - 1);
 #endif
-        hub_barrier();
+        hub_barrier_reader();
 #if KGX_HUB_DEBUG & 4
-        hub_barrier();
-        hub_barrier();
+        hub_barrier_reader();
+        hub_barrier_reader();
 #endif
       }
-      if (f < a.F) {
+      if (f < fw) {
         float r[1] = {a.epi == KGX_EPI_RAW ? R::finish_raw(acc, end - beg) : R::finish(acc, end - beg)};
-        epilogue<1>(a, row, f, r);
-        vstore<1>(a.out + int64_t(row) * a.ld_o + f, r);
+        epilogue<1>(a, row, c0 + f, r);
+        vstore<1>(a.out + int64_t(row) * a.ld_o + c0 + f, r);
       }
     }
     return;
   }
 
   // ---- producers: lane (slot r, features f..f+3) of every stage
-  for (int64_t h = blockIdx.x; h < a.n_rows; h += gridDim.x) {
-    KGX_HUB_ROW(h)
+  for (int64_t p = blockIdx.x; p < a.n_rows * ncg; p += gridDim.x) {
+    KGX_HUB_ROW(p)
     const int slot = (wave - CW) * RPW + lane / G;
-    if (__builtin_amdgcn_readfirstlane(slot) >= S) {  // idle producer wave: barriers only
+    if (__builtin_amdgcn_readfirstlane(slot) >= SP) {  // idle producer wave: barriers only
       for (int32_t s = 0; s < n_iter; ++s) hub_barrier();
       continue;
     }
     const int f = (lane % G) * 4;
-    const int fl = f < a.F ? f : a.F - 4;  // lanes past F load (and write) a valid duplicate
-    const float* tab = a.table + fl;
+    const int fl = f < fw ? f : fw - 4;  // lanes past the group load (and write) a valid duplicate
+    const float* tab = a.table + c0 + fl;
     float* lds_row = &ring[0][slot * RL + f];
-    auto edge = [&](int32_t t) {  // stage t's edge of this slot, clamped into the row
-      const int32_t e = beg + t * S + slot;
+    auto edge = [&](int32_t t, int r) {  // stage t's edge of row r of this slot, clamped into the row
+      const int32_t e = beg + t * S + r * SP + slot;
       return e < end ? e : end - 1;
     };
-    int32_t ci[2][D];  // index batches: stages of chunk c in set c & 1
-    f32x4_t gv[D];     // gathers in flight: stage t in gv[t % D]
-    float wr[D];       // ... and their weights, loaded with them
+    int32_t ci[2][D][RPL];  // index batches: stages of chunk c in set c & 1
+    f32x4_t gv[D][RPL];     // gathers in flight: stage t in gv[t % D]
+    float wr[D][RPL];       // ... and their weights, loaded with them
     auto batch = [&](int set, int32_t chunk) {
 #pragma unroll
-      for (int j = 0; j < D; ++j) {
-        const int32_t* pi = a.idx + edge(chunk * D + j);
-        asm volatile("global_load_dword %0, %1, off" : "=v"(ci[set][j]) : "v"(pi) : "memory");
-      }
+      for (int j = 0; j < D; ++j)
+#pragma unroll
+        for (int r = 0; r < RPL; ++r) {
+          const int32_t* pi = a.idx + edge(chunk * D + j, r);
+          asm volatile("global_load_dword %0, %1, off" : "=v"(ci[set][j][r]) : "v"(pi) : "memory");
+        }
     };
-    auto gather = [&](int j, int32_t t, int32_t c) {  // weight, then row, of stage t
-      if constexpr (WEIGHTED) {
-        const float* pw = a.w + edge(t);
-        asm volatile("global_load_dword %0, %1, off" : "=v"(wr[j]) : "v"(pw) : "memory");
+    auto gather = [&](int j, int32_t t, const int32_t(&c)[RPL]) {  // weights, then rows, of stage t
+#pragma unroll
+      for (int r = 0; r < RPL; ++r) {
+        if constexpr (WEIGHTED) {
+          const float* pw = a.w + edge(t, r);
+          asm volatile("global_load_dword %0, %1, off" : "=v"(wr[j][r]) : "v"(pw) : "memory");
+        }
+        const float* p = tab + row_off(c[r], a.ld_t);
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(gv[j][r]) : "v"(p) : "memory");
       }
-      const float* p = tab + row_off(c, a.ld_t);
-      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(gv[j]) : "v"(p) : "memory");
     };
     auto pin_batch = [&](int set) {
 #pragma unroll
-      for (int j = 0; j < D; ++j) asm volatile("" : "+v"(ci[set][j]));
+      for (int j = 0; j < D; ++j)
+#pragma unroll
+        for (int r = 0; r < RPL; ++r) asm volatile("" : "+v"(ci[set][j][r]));
     };
-    // vector-memory ops per iteration (weight + row) and the vmcnt waits:
-    // stage s's row load is the oldest we need; newer are the D-1 later
+    // vector-memory ops per iteration (weights + rows) and the vmcnt waits:
+    // stage s's loads are the oldest we need; newer are the D-1 later
     // iterations' loads, plus (after the chunk's first iteration) its batch
-    constexpr int OPI = WEIGHTED ? 2 : 1;
-    static_assert(OPI * (D - 1) + D <= 63, "vmcnt immediate");
+    constexpr int OPI = RPL * (WEIGHTED ? 2 : 1);
+    constexpr int NB = D * RPL;
+    static_assert(OPI * (D - 1) + NB <= 63, "vmcnt immediate");
     // prologue: index batches of chunks 0 and 1, then the loads of stages 0..D-1
     batch(0, 0);
     batch(1, 1);
@@ -447,14 +499,15 @@ __global__ __launch_bounds__(kHubThreads, 1) void spmm_hub_kernel(SpmmArgs a) {
       for (int j = 0; j < D; ++j) {
         const int32_t s = k * D + j;
         if (j == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPI * (D - 1)) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPI * (D - 1) + D) : "memory");
-        asm volatile("" : "+v"(gv[j]));
-        if constexpr (WEIGHTED) asm volatile("" : "+v"(wr[j]));
-        {
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPI * (D - 1) + NB) : "memory");
+#pragma unroll
+        for (int r = 0; r < RPL; ++r) {
+          asm volatile("" : "+v"(gv[j][r]));
+          if constexpr (WEIGHTED) asm volatile("" : "+v"(wr[j][r]));
           f32x4_t m;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) m[q] = R::msg(WEIGHTED ? __fmul_rn(gv[j][q], wr[j]) : gv[j][q]);
-          *reinterpret_cast<f32x4_t*>(lds_row + (s % 3) * (S * RL)) = m;
+          for (int q = 0; q < 4; ++q) m[q] = R::msg(WEIGHTED ? __fmul_rn(gv[j][r][q], wr[j][r]) : gv[j][r][q]);
+          *reinterpret_cast<f32x4_t*>(lds_row + (s % 3) * (S * RL) + r * (SP * RL)) = m;
         }
         if (j == 0) batch(fill, k + 2);
         gather(j, s + D, ci[use][j]);
@@ -480,10 +533,12 @@ __global__ __launch_bounds__(kHubThreads, 1) void spmm_hub_kernel(SpmmArgs a) {
     // loads are never consumed, and a dead destination register could be
     // handed to other code while its load is still in flight.
 #pragma unroll
-    for (int j = 0; j < D; ++j) {
-      asm volatile("" ::"v"(gv[j]), "v"(ci[0][j]), "v"(ci[1][j]));
-      if constexpr (WEIGHTED) asm volatile("" ::"v"(wr[j]));
-    }
+    for (int j = 0; j < D; ++j)
+#pragma unroll
+      for (int r = 0; r < RPL; ++r) {
+        asm volatile("" ::"v"(gv[j][r]), "v"(ci[0][j][r]), "v"(ci[1][j][r]));
+        if constexpr (WEIGHTED) asm volatile("" ::"v"(wr[j][r]));
+      }
   }
 #undef KGX_HUB_ROW
 }
@@ -697,11 +752,13 @@ int launch_main(const SpmmArgs& a_in, hipStream_t s) {
     }();
     if (VEC == 4 && !a.items && a.n_rows > 0 && !a.drop_key && a.G >= 8 && !hub_off) {
       a.long_rows = 1;  // EXACT: long rows first, one block per row
+      const int gh = a.G < kHubG ? a.G : kHubG;  // column group = 4 x gh features
       auto kh = spmm_hub_kernel<64, RED, W>;
-      if (a.G == 32) kh = spmm_hub_kernel<32, RED, W>;
-      else if (a.G == 16) kh = spmm_hub_kernel<16, RED, W>;
-      else if (a.G == 8) kh = spmm_hub_kernel<8, RED, W>;
-      const int64_t nb = a.n_rows < cu_count() ? a.n_rows : cu_count();  // one resident block per CU
+      if (gh == 32) kh = spmm_hub_kernel<32, RED, W>;
+      else if (gh == 16) kh = spmm_hub_kernel<16, RED, W>;
+      else if (gh == 8) kh = spmm_hub_kernel<8, RED, W>;
+      const int64_t work = a.n_rows * ((a.F + 4 * gh - 1) / (4 * gh));
+      const int64_t nb = work < cu_count() ? work : cu_count();  // one resident block per CU
       hipLaunchKernelGGL(kh, dim3(unsigned(nb)), dim3(kHubThreads), 0, s, a);
       KGX_CHECK_LAUNCH();
     } else if (!a.items && a.n_rows > 0) {  // EXACT: long rows first, on their own kernel

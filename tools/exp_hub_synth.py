@@ -43,5 +43,9 @@ def run(n_rows, deg, n=1_000_000, f=128):
 
 
 if __name__ == "__main__":
-    for nr, d in ((1, 138_539), (256, 54_000), (2048, 6_700)):
-        print(json.dumps(run(nr, d)), flush=True)
+    if len(sys.argv) > 1:  # rows deg [n_src] [F]
+        a = [int(v) for v in sys.argv[1:]]
+        print(json.dumps(run(a[0], a[1], *(a[2:4]))), flush=True)
+    else:
+        for nr, d in ((1, 138_539), (256, 54_000), (2048, 6_700)):
+            print(json.dumps(run(nr, d)), flush=True)
