@@ -219,6 +219,23 @@ int kgx_spmm_gemm_ex(int reduce, const int32_t* rowptr, const int32_t* rows, int
                      float gin_scale, float* out, int64_t ld_out, float* partials, float* agg_out,
                      int64_t ld_agg, kgx_stream_t stream);
 
+/* kgx_spmm_gemm_ex2: kgx_spmm_gemm_ex with the schedule's tail of rows of degree
+ * <= 2 ([n_short_end, n_items)) taken from packed records instead of the item
+ * list: tiny_pack[n_items - n_short_end][4] = {row, degree, col0, col1} (col1 =
+ * col0 for degree 1, both any valid source for degree 0) and, when w is given,
+ * tiny_w[..][2] = {w0, w1}; the first n_tiny_deg2 records have degree 2 (the
+ * rest <= 1: degree-descending order).  Built once per graph (tiny.py).  Items
+ * [n_long_items, n_short_end) go to the short-row kernel as before.  tiny_pack
+ * NULL: n_short_end must equal n_items.  Same boundary as kgx_spmm_gemm
+ * (gcn_conv.py:233-272, aggregators.py:56-167). */
+int kgx_spmm_gemm_ex2(int reduce, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
+                      const int32_t* items, int64_t n_items, int64_t n_long_items, int64_t n_short_end,
+                      const int32_t* tiny_pack, const float* tiny_w, int64_t n_tiny_deg2,
+                      const int32_t* split, int64_t n_split,
+                      const int32_t* idx, const float* w, const float* x, int64_t ld_x, int64_t F_in,
+                      const float* W, int64_t F_out, const float* bias, int flags, float gin_scale, float* out,
+                      int64_t ld_out, float* partials, float* agg_out, int64_t ld_agg, kgx_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * Backward of the segment max / min reduction (autograd of kgx_spmm MAX/MIN).
  * torch's scatter_reduce amax/amin backward, under the reference's isinf

@@ -71,6 +71,11 @@ struct FusedArgs {
   int relu;         // out = max(result, 0) (not with accumulate)
   float gin_scale;
   int debug;        // experiment builds only (-DKGX_EXPERIMENTS, env KGX_FUSED_DEBUG): 1 skip MFMA, 2 skip stores
+  int64_t n_short_end;  // items [n_long, n_short_end): spmm_gemm_short_kernel
+  const int4* tpack;    // rows of degree <= 2 as {row, degree, col0, col1} (spmm_gemm_tiny_kernel)
+  const float2* tw;     // their weights {w0, w1} (weighted reductions)
+  int64_t n_tiny;       // rows in tpack
+  int64_t n_tiny2;      // the first n_tiny2 of them have degree 2 (the rest <= 1)
 };
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops
@@ -446,7 +451,7 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
   }
   const float bcol = (mfma_wave && a.bias) ? a.bias[n_col] : 0.0f;
 
-  for (int64_t base = a.n_long + int64_t(blockIdx.x) * kShortRows; base < a.n_items;
+  for (int64_t base = a.n_long + int64_t(blockIdx.x) * kShortRows; base < a.n_short_end;
        base += int64_t(gridDim.x) * kShortRows) {
     int32_t row[kRPG], beg[kRPG], deg[kRPG];
 #pragma unroll
@@ -455,7 +460,7 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
       row[r] = -1;
       beg[r] = 0;
       deg[r] = 0;
-      if (it < a.n_items) {
+      if (it < a.n_short_end) {
         const int4 v = a.items[it];
         row[r] = v.x;
         beg[r] = v.y;
@@ -610,6 +615,228 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
   }
 }
 
+// Rows of degree <= 2 (an R-MAT graph's self-loop-only rows are half of all
+// rows), warp-specialised.  spmm_gemm_short_kernel's waves each gather, split,
+// run the MFMAs and store in turn, and its waves sit in s_waitcnt / barriers
+// 71 % of their cycles: the MFMA phase and the stores add to the gathers
+// instead of hiding behind them, and W's 48 fragment registers per lane leave
+// no room to prefetch.  Here, in a 1024-thread block:
+//  - producer waves 8..15 (16 groups of 32 lanes, 2 rows each per 32-row tile)
+//    read a packed record per row {row, degree, col0, col1} (+ {w0, w1}),
+//    gather both source rows unconditionally (col1 = col0 for degree 1;
+//    absent edges fold in the reduction's identity), split the aggregated
+//    rows into the bf16 planes of one of two LDS tiles.  Their loads run two
+//    tiles ahead: while tile t is folded, tile t+1's rows and tile t+2's
+//    records are in flight (all loads unconditional, so hipcc's vmcnt counts
+//    stay exact and it never drains the queue);
+//  - MFMA waves 0..7 hold W's split fragments (16 output columns each), take
+//    the other tile and store their results straight from the accumulators.
+// One barrier per tile hands a tile from producers to MFMA waves.
+constexpr int kTinyThreads = 1024;
+constexpr int kTinyGroups = 16;  // producer row groups
+#ifndef KGX_TINY_RPG
+#define KGX_TINY_RPG 2
+#endif
+constexpr int kTinyRPG = KGX_TINY_RPG;  // rows per group per tile (= 16-row MFMA blocks per tile)
+constexpr int kTinyRows = kTinyGroups * kTinyRPG;
+
+// NG: edges gathered per row (2 for the degree-2 head of the tail, 1 for the
+// degree <= 1 rest: the schedule is degree-descending, so each is a range).
+template <int RED, bool WEIGHTED, bool EXTRA, int NG>  // EXTRA: pre_gin or agg_out (loads / stores under a row mask)
+__global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedArgs a) {
+  using R = Red<RED>;
+  __shared__ __attribute__((aligned(16))) short planes[2][3][kTinyRows][kFin + 8];
+  __shared__ int32_t trow[2][kTinyRows];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t n_tiles = (a.n_tiny + kTinyRows - 1) / kTinyRows;
+  const int64_t my_tiles = int64_t(blockIdx.x) < n_tiles ? (n_tiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+
+  if (wave < 8) {  // ---- MFMA waves: tile i-1 at iteration i
+    const int wl = tid & 63;
+    const int q = wl >> 4, m = wl & 15;
+    const int n_col = wave * 16 + m;
+    const bool mfma_wave = wave * 16 < a.F_out;
+    bf16x8_t wfh[4], wfm[4], wfl[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+      u32x4_t ph, pm, pl;
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        const float v0 = mfma_wave ? a.W[int64_t(32 * q + 8 * s + j) * a.F_out + n_col] : 0.0f;
+        const float v1 = mfma_wave ? a.W[int64_t(32 * q + 8 * s + j + 1) * a.F_out + n_col] : 0.0f;
+        uint32_t h, m_, l;
+        split3_pair(v0, v1, h, m_, l);
+        ph[j / 2] = h;
+        pm[j / 2] = m_;
+        pl[j / 2] = l;
+      }
+      wfh[s] = __builtin_bit_cast(bf16x8_t, ph);
+      wfm[s] = __builtin_bit_cast(bf16x8_t, pm);
+      wfl[s] = __builtin_bit_cast(bf16x8_t, pl);
+    }
+    const float bcol = (mfma_wave && a.bias) ? a.bias[n_col] : 0.0f;
+    for (int64_t i = 0; i <= my_tiles; ++i) {
+      if (i >= 1 && mfma_wave) {
+        const int b = int((i - 1) & 1);
+        f32x4 d[kTinyRPG];
+#pragma unroll
+        for (int rb = 0; rb < kTinyRPG; ++rb) d[rb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+#pragma unroll
+          for (int rb = 0; rb < kTinyRPG; ++rb) {
+            const int tr = 16 * rb + m;
+            const bf16x8_t ah = *reinterpret_cast<const bf16x8_t*>(&planes[b][0][tr][32 * q + 8 * s4]);
+            const bf16x8_t am = *reinterpret_cast<const bf16x8_t*>(&planes[b][1][tr][32 * q + 8 * s4]);
+            const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(&planes[b][2][tr][32 * q + 8 * s4]);
+            d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, wfh[s4], d[rb], 0, 0, 0);
+            d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfl[s4], d[rb], 0, 0, 0);
+            d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, wfm[s4], d[rb], 0, 0, 0);
+            d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, wfh[s4], d[rb], 0, 0, 0);
+            d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfm[s4], d[rb], 0, 0, 0);
+            d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfh[s4], d[rb], 0, 0, 0);
+          }
+        }
+        // lane (m, q) holds column n_col of rows 16 rb + 4 q + j: four 64-byte
+        // row segments per store instruction (the wave next door writes the
+        // other half of each 128-byte line)
+#pragma unroll
+        for (int rb = 0; rb < kTinyRPG; ++rb)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int rr = trow[b][16 * rb + 4 * q + j];
+            if (rr >= 0) {
+              float* dst = a.out + int64_t(rr) * a.ld_o + n_col;
+              float v = d[rb][j] + bcol;
+              if (a.accumulate) v = __fadd_rn(*dst, v);
+              if (a.relu) v = fmaxf(v, 0.0f);
+              *dst = v;
+            }
+          }
+      }
+      lds_barrier();
+    }
+    return;
+  }
+
+  // ---- producers: tile i at iteration i
+  const int pt = tid - 512;
+  const int g = pt >> 5, lane = pt & 31, f = lane * 4;
+  struct Rec {
+    int4 p[kTinyRPG];
+    float2 w[kTinyRPG];
+  };
+  auto rec = [&](int64_t k, Rec& r) {  // tile k's records (clamped; rows past the end get row -1)
+#pragma unroll
+    for (int j = 0; j < kTinyRPG; ++j) {
+      const int64_t t = int64_t(blockIdx.x) + k * gridDim.x;
+      const int64_t e = t * kTinyRows + g + kTinyGroups * j;
+      const int64_t ec = e < a.n_tiny ? e : a.n_tiny - 1;
+      r.p[j] = a.tpack[ec];
+      if (e >= a.n_tiny) r.p[j].x = -1;
+      if constexpr (WEIGHTED) r.w[j] = a.tw[ec];
+    }
+  };
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  auto gather = [&](const Rec& r, f4 (&v)[kTinyRPG][NG]) {
+#pragma unroll
+    for (int j = 0; j < kTinyRPG; ++j) {
+      v[j][0] = *reinterpret_cast<const f4*>(a.x + row_off(r.p[j].z, a.ld_x) + f);
+      if constexpr (NG == 2) v[j][1] = *reinterpret_cast<const f4*>(a.x + row_off(r.p[j].w, a.ld_x) + f);
+    }
+  };
+  auto produce = [&](int64_t i, const auto& c, const f4 (&v)[kTinyRPG][NG]) {
+    const int b = int(i & 1);
+#pragma unroll
+    for (int j = 0; j < kTinyRPG; ++j) {
+      const int32_t row = c.row[j], deg = c.deg[j];
+      float o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float t = R::init();
+        const float m0 = WEIGHTED ? __fmul_rn(v[j][0][k], c.w[j].x) : v[j][0][k];
+        t = R::combine(t, deg > 0 ? R::msg(m0) : R::init());
+        if constexpr (NG == 2) {
+          const float m1 = WEIGHTED ? __fmul_rn(v[j][1][k], c.w[j].y) : v[j][1][k];
+          t = R::combine(t, deg > 1 ? R::msg(m1) : R::init());
+        }
+        o[k] = row >= 0 ? R::finish(t, deg) : 0.0f;
+      }
+      if constexpr (EXTRA) {
+        if (row >= 0 && a.pre_gin) {
+          float xv[4];
+          vload<4>(xv, a.x + int64_t(row) * a.ld_x + f);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) o[k] = __fadd_rn(__fmul_rn(a.gin_scale, xv[k]), o[k]);
+        }
+        if (row >= 0 && a.agg_out) vstore<4>(a.agg_out + int64_t(row) * a.ld_agg + f, o);
+      }
+      bf16x4_t ph, pm, pl;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        short h, m_, l;
+        split3_a(o[k], h, m_, l);
+        ph[k] = h;
+        pm[k] = m_;
+        pl[k] = l;
+      }
+      if (!__builtin_isfinite(__fadd_rn(__fadd_rn(o[0], o[1]), __fadd_rn(o[2], o[3])))) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          short h, m_, l;
+          split3_a_lo(o[k], h, m_, l);
+          ph[k] = h;
+          pm[k] = m_;
+          pl[k] = l;
+        }
+      }
+      const int tr = g + kTinyGroups * j;
+      *reinterpret_cast<bf16x4_t*>(&planes[b][0][tr][f]) = ph;
+      *reinterpret_cast<bf16x4_t*>(&planes[b][1][tr][f]) = pm;
+      *reinterpret_cast<bf16x4_t*>(&planes[b][2][tr][f]) = pl;
+      if (lane == 0) trow[b][tr] = row;
+    }
+  };
+  // Pipeline, at iteration i: issue tile i+2's records, issue tile i+1's row
+  // gathers (its records arrived a step ago), fold tile i (rows in flight
+  // since i-1).  Every load is unconditional, so when a value is used the
+  // loads issued after it are a known count and hipcc's vmcnt wait leaves
+  // them in flight.  Unrolled by two so register sets rotate by name.
+  struct Cur {
+    int32_t row[kTinyRPG], deg[kTinyRPG];
+    float2 w[kTinyRPG];
+  };
+  auto take = [&](const Rec& r, Cur& c) {
+#pragma unroll
+    for (int j = 0; j < kTinyRPG; ++j) {
+      c.row[j] = r.p[j].x;
+      c.deg[j] = r.p[j].y;
+      c.w[j] = WEIGHTED ? r.w[j] : float2{1.0f, 1.0f};
+    }
+  };
+  Rec ra, rb;
+  Cur cur;
+  f4 v0[kTinyRPG][NG], v1[kTinyRPG][NG];
+  rec(0, rb);
+  take(rb, cur);
+  rec(1, ra);
+  gather(rb, v0);
+  auto step = [&](int64_t i, Rec& rn, Rec& rfree, f4 (&vc)[kTinyRPG][NG], f4 (&vn)[kTinyRPG][NG]) {
+    rec(i + 2, rfree);  // tile i+2's records
+    gather(rn, vn);     // tile i+1's rows
+    produce(i, cur, vc);
+    take(rn, cur);
+    lds_barrier();
+  };
+  for (int64_t i = 0; i <= my_tiles; i += 2) {
+    step(i, ra, rb, v0, v1);
+    if (i + 1 > my_tiles) break;
+    step(i + 1, rb, ra, v1, v0);
+  }
+}
+
 // Split rows: combine chunk partials in order, finish, then out = v @ W + b (VALU).
 template <int RED>
 __global__ __launch_bounds__(256) void spmm_gemm_fixup_kernel(FusedArgs a) {
@@ -684,7 +911,7 @@ int launch(const FusedArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kThreads), 0, s, a);
     KGX_CHECK_LAUNCH();
   }
-  if (a.items && a.n_long < a.n_items) {
+  if (a.items && a.n_long < a.n_short_end) {
     int per_cu = 0;
     auto k = spmm_gemm_short_kernel<RED, W>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, 0) != hipSuccess || per_cu <= 0)
@@ -696,10 +923,26 @@ int launch(const FusedArgs& a, hipStream_t s) {
           hipDeviceGetAttribute(&cus2, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus2 <= 0)
         cus2 = 256;
     }
-    const int64_t need = (a.n_items - a.n_long + kShortRows - 1) / kShortRows;
+    const int64_t need = (a.n_short_end - a.n_long + kShortRows - 1) / kShortRows;
     const int64_t cap = a.share_gpu ? int64_t(per_cu) * cus2 * 7 / 8 : int64_t(per_cu) * cus2;
     hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kThreads), 0, s, a);
     KGX_CHECK_LAUNCH();
+  }
+  if (a.tpack && a.n_tiny > 0) {  // one 1024-thread block per CU; degree-2 head, then the degree <= 1 rest
+    const bool extra = a.pre_gin || a.agg_out;
+    for (int part = 0; part < 2; ++part) {
+      FusedArgs b = a;
+      b.tpack = a.tpack + (part ? a.n_tiny2 : 0);
+      b.tw = a.tw ? a.tw + (part ? a.n_tiny2 : 0) : nullptr;
+      b.n_tiny = part ? a.n_tiny - a.n_tiny2 : a.n_tiny2;
+      if (b.n_tiny <= 0) continue;
+      auto k = part ? (extra ? spmm_gemm_tiny_kernel<RED, W, true, 1> : spmm_gemm_tiny_kernel<RED, W, false, 1>)
+                    : (extra ? spmm_gemm_tiny_kernel<RED, W, true, 2> : spmm_gemm_tiny_kernel<RED, W, false, 2>);
+      const int64_t need = (b.n_tiny + kTinyRows - 1) / kTinyRows;
+      const int64_t cap = a.share_gpu ? int64_t(cu_count()) * 7 / 8 : int64_t(cu_count());
+      hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kTinyThreads), 0, s, b);
+      KGX_CHECK_LAUNCH();
+    }
   }
   if (a.items && a.n_split > 0) {
     const int64_t blocks = (a.n_split + 7) / 8;
@@ -731,9 +974,26 @@ extern "C" int kgx_spmm_gemm_ex(int reduce, const int32_t* rowptr, const int32_t
                                 int64_t F_in, const float* W, int64_t F_out, const float* bias, int flags,
                                 float gin_scale, float* out, int64_t ld_out, float* partials, float* agg_out,
                                 int64_t ld_agg, kgx_stream_t stream_) {
+  return kgx_spmm_gemm_ex2(reduce, rowptr, rows, n_rows, items, n_items, n_long_items, n_items, nullptr, nullptr, 0,
+                           split, n_split, idx, w, x, ld_x, F_in, W, F_out, bias, flags, gin_scale, out, ld_out,
+                           partials, agg_out, ld_agg, stream_);
+}
+
+extern "C" int kgx_spmm_gemm_ex2(int reduce, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
+                                 const int32_t* items, int64_t n_items, int64_t n_long_items, int64_t n_short_end,
+                                 const int32_t* tiny_pack, const float* tiny_w, int64_t n_tiny_deg2,
+                                 const int32_t* split,
+                                 int64_t n_split, const int32_t* idx, const float* w, const float* x, int64_t ld_x,
+                                 int64_t F_in, const float* W, int64_t F_out, const float* bias, int flags,
+                                 float gin_scale, float* out, int64_t ld_out, float* partials, float* agg_out,
+                                 int64_t ld_agg, kgx_stream_t stream_) {
   hipStream_t stream = as_stream(stream_);
-  KGX_REQUIRE(!items || (n_long_items >= 0 && n_long_items <= n_items), KGX_ERR_ARG,
-              "kgx_spmm_gemm: n_long_items must lie in [0, n_items]");
+  KGX_REQUIRE(!items || (n_long_items >= 0 && n_long_items <= n_short_end && n_short_end <= n_items), KGX_ERR_ARG,
+              "kgx_spmm_gemm: need 0 <= n_long_items <= n_short_end <= n_items");
+  KGX_REQUIRE(!tiny_pack || (items && (w == nullptr || tiny_w)), KGX_ERR_ARG,
+              "kgx_spmm_gemm: the tiny-row records need the schedule (and weights when weighted)");
+  KGX_REQUIRE(!tiny_pack || (n_tiny_deg2 >= 0 && n_tiny_deg2 <= n_items - n_short_end), KGX_ERR_ARG,
+              "kgx_spmm_gemm: n_tiny_deg2 must lie in [0, n_items - n_short_end]");
   KGX_REQUIRE(reduce >= KGX_SUM && reduce <= KGX_MIN, KGX_ERR_ARG, "kgx_spmm_gemm: reduce %d unsupported", reduce);
   KGX_REQUIRE(F_in == kFin, KGX_ERR_UNSUPPORTED, "kgx_spmm_gemm: F_in must be %d (got %lld)", kFin,
               (long long)F_in);
@@ -760,6 +1020,11 @@ extern "C" int kgx_spmm_gemm_ex(int reduce, const int32_t* rowptr, const int32_t
   a.items = reinterpret_cast<const int4*>(items);
   a.n_items = items ? n_items : 0;
   a.n_long = items ? n_long_items : 0;
+  a.n_short_end = items ? n_short_end : 0;
+  a.tpack = items ? reinterpret_cast<const int4*>(tiny_pack) : nullptr;
+  a.tw = reinterpret_cast<const float2*>(tiny_w);
+  a.n_tiny = (items && tiny_pack) ? n_items - n_short_end : 0;
+  a.n_tiny2 = a.n_tiny ? n_tiny_deg2 : 0;
   a.split = reinterpret_cast<const int4*>(split);
   a.n_split = items ? n_split : 0;
   a.idx = idx;

@@ -156,8 +156,16 @@ class sharing_gpu:
         _SHARE_GPU = self._old
 
 
+def _tiny_abi(items, n_items, n_long, tpack, tw, n_short_end, n_tiny2):
+    """(n_short_end, tpack, tw, n_tiny2) arguments of kgx_spmm_gemm_ex2."""
+    if items is None or tpack is None or not (n_long <= n_short_end <= n_items) \
+            or tpack.shape[0] != n_items - n_short_end:
+        return n_items, None, None, 0
+    return n_short_end, tpack, tw, n_tiny2
+
+
 def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale, save_agg,
-                    relu=False, n_long=-1):
+                    relu=False, n_long=-1, tpack=None, tw=None, n_short_end=-1, n_tiny2=0):
     x, w, W, bias = _f32c(x), _f32c(w), _f32c(W), _f32c(bias)
     dev = nat.require_device(x, rowptr, rows, idx, w, W, bias, items, split)
     n_dst = rowptr.numel() - 1
@@ -172,9 +180,12 @@ def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, b
     if items is not None and n_split > 0:
         partials = torch.empty((n_slots, x.shape[1]), dtype=torch.float32, device=dev)
     n_long = n_items if n_long < 0 or n_long > n_items else n_long
+    n_se, tpack, tw, n_tiny2 = _tiny_abi(items, n_items, n_long, tpack, tw if w is not None else None, n_short_end,
+                                         n_tiny2)
     nat.check(
-        nat.lib().kgx_spmm_gemm_ex(
-            reduce, nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, n_long, nat.ptr(split), n_split,
+        nat.lib().kgx_spmm_gemm_ex2(
+            reduce, nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, n_long, n_se, nat.ptr(tpack),
+            nat.ptr(tw), n_tiny2, nat.ptr(split), n_split,
             nat.ptr(idx), nat.ptr(w), nat.ptr(x), x.stride(0), x.shape[1], nat.ptr(W), F_out, nat.ptr(bias),
             int(pre_gin) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0) | (nat.FUSED_RELU if relu else 0),
             float(gin_scale), nat.ptr(out), out.stride(0),
@@ -203,14 +214,18 @@ def spmm_gemm(
     gin_scale: float,
     relu: bool = False,
     n_long: int = -1,
+    tpack: Optional[torch.Tensor] = None,
+    tw: Optional[torch.Tensor] = None,
+    n_short_end: int = -1,
+    n_tiny2: int = 0,
 ) -> torch.Tensor:
     return _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale,
-                           False, relu, n_long)[0]
+                           False, relu, n_long, tpack, tw, n_short_end, n_tiny2)[0]
 
 
 @spmm_gemm.register_fake
 def _spmm_gemm_fake(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale, relu=False,
-                    n_long=-1):
+                    n_long=-1, tpack=None, tw=None, n_short_end=-1, n_tiny2=0):
     return x.new_empty((rowptr.shape[0] - 1, W.shape[1]))
 
 
@@ -230,15 +245,19 @@ def spmm_gemm_save(
     pre_gin: bool,
     gin_scale: float,
     n_long: int = -1,
+    tpack: Optional[torch.Tensor] = None,
+    tw: Optional[torch.Tensor] = None,
+    n_short_end: int = -1,
+    n_tiny2: int = 0,
 ) -> tuple[torch.Tensor, torch.Tensor]:
     """kgx::spmm_gemm that also returns the aggregated rows before the transform."""
     return _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale, True,
-                           False, n_long)
+                           False, n_long, tpack, tw, n_short_end, n_tiny2)
 
 
 @spmm_gemm_save.register_fake
 def _spmm_gemm_save_fake(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale,
-                         n_long=-1):
+                         n_long=-1, tpack=None, tw=None, n_short_end=-1, n_tiny2=0):
     n = rowptr.shape[0] - 1
     return x.new_empty((n, W.shape[1])), x.new_empty((n, x.shape[1]))
 
@@ -258,6 +277,10 @@ def spmm_gemm_acc_(
     W: torch.Tensor,
     bias: Optional[torch.Tensor],
     n_long: int = -1,
+    tpack: Optional[torch.Tensor] = None,
+    tw: Optional[torch.Tensor] = None,
+    n_short_end: int = -1,
+    n_tiny2: int = 0,
 ) -> None:
     """out += bias + REDUCE(...) @ W (KGX_FUSED_ACCUMULATE), in place."""
     x, w, W, bias = _f32c(x), _f32c(w), _f32c(W), _f32c(bias)
@@ -273,9 +296,12 @@ def spmm_gemm_acc_(
     if items is not None and n_split > 0:
         partials = torch.empty((n_slots, x.shape[1]), dtype=torch.float32, device=dev)
     n_long = n_items if n_long < 0 or n_long > n_items else n_long
+    n_se, tpack, tw, n_tiny2 = _tiny_abi(items, n_items, n_long, tpack, tw if w is not None else None, n_short_end,
+                                         n_tiny2)
     nat.check(
-        nat.lib().kgx_spmm_gemm_ex(
-            reduce, nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, n_long, nat.ptr(split), n_split,
+        nat.lib().kgx_spmm_gemm_ex2(
+            reduce, nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, n_long, n_se, nat.ptr(tpack),
+            nat.ptr(tw), n_tiny2, nat.ptr(split), n_split,
             nat.ptr(idx), nat.ptr(w), nat.ptr(x), x.stride(0), x.shape[1], nat.ptr(W), W.shape[1], nat.ptr(bias),
             nat.FUSED_ACCUMULATE, 1.0, nat.ptr(out), out.stride(0), nat.ptr(partials), None, 0, nat.stream(dev),
         ),
@@ -284,7 +310,8 @@ def spmm_gemm_acc_(
 
 
 @spmm_gemm_acc_.register_fake
-def _spmm_gemm_acc_fake(out, x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, n_long=-1):
+def _spmm_gemm_acc_fake(out, x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, n_long=-1, tpack=None,
+                        tw=None, n_short_end=-1, n_tiny2=0):
     return None
 
 
@@ -601,6 +628,16 @@ def aggregate(
                           int(seed))
 
 
+def _tiny_of(g, items):
+    """(tpack, tw, n_short_end, n_tiny2) for a fused launch over g's schedule
+    (tiny.py: packed records of the degree <= 2 tail, built once per graph)."""
+    if items is None:
+        return None, None, -1, 0
+    from . import tiny
+
+    return tiny.tiny_pack(g)
+
+
 def _aggregate_transform_raw(g, x, W, red, weighted, bias, pre_gin, gin_scale, exact, relu=False):
     items, _, split, _, n_slots = g.work(exact)
     w = g.w if weighted else None
@@ -608,7 +645,7 @@ def _aggregate_transform_raw(g, x, W, red, weighted, bias, pre_gin, gin_scale, e
         raise ValueError("graph was built without GCN normalisation weights")
     return _timed(lambda: torch.ops.kgx.spmm_gemm(
         x, g.rowptr, g.rows, items, split, g.col, w, n_slots, red, W, bias, bool(pre_gin), float(gin_scale),
-        bool(relu), g.n_long if items is not None else -1
+        bool(relu), g.n_long if items is not None else -1, *_tiny_of(g, items)
     ))
 
 
@@ -641,7 +678,7 @@ class _AggregateTransformFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:  # keep P = PRE(A x) for dW (one extra row store instead of a recompute)
             out, P = _timed(lambda: torch.ops.kgx.spmm_gemm_save(
                 x, g.rowptr, g.rows, items, split, g.col, w, n_slots, red, W, bias, bool(pre_gin), float(gin_scale),
-                g.n_long if items is not None else -1))
+                g.n_long if items is not None else -1, *_tiny_of(g, items)))
         else:
             out = _aggregate_transform_raw(g, x, W, red, weighted, bias, pre_gin, gin_scale, exact)
             P = None
@@ -705,7 +742,8 @@ def aggregate_transform(
         items, _, split, _, n_slots = g.work(exact)
         w = g.w if weighted else None
         _timed(lambda: torch.ops.kgx.spmm_gemm_acc_(out, x, g.rowptr, g.rows, items, split, g.col, w, n_slots, red,
-                                                   W, bias, g.n_long if items is not None else -1))
+                                                   W, bias, g.n_long if items is not None else -1,
+                                                   *_tiny_of(g, items)))
         return out
     if _needs_grad(x, W, bias):
         y = _AggregateTransformFn.apply(x, W, bias, g, red, weighted, pre_gin, float(gin_scale), exact)
