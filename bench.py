@@ -356,7 +356,7 @@ def main() -> None:
         # of the rows they add to are implementation overhead, not algorithmic bytes
         balg = b_alg_spmm(n_rows, e_agg, f_in if fused else f_out, weighted=True, f_out=f_out)
         # the fused op: long rows, the short-row suffix (degree <= 7) and the hub fix-up
-        kernel = ("spmm_gemm_kernel", "spmm_gemm_short_kernel", "spmm_gemm_fixup_kernel") if fused \
+        kernel = ("spmm_gemm_kernel", "spmm_gemm_short_kernel", "spmm_gemm_tiny_kernel", "spmm_gemm_fixup_kernel") if fused \
             else ("spmm_kernel", "spmm_fixup_kernel")
     elif kind == "gat":  # one pass: h_src row per edge, h_dst row + output row per node
         balg = 4 * (n_rows + 1) + e_agg * (4 + 4 * f_out) + 8 * n_rows * f_out

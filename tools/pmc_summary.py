@@ -63,11 +63,17 @@ def main() -> None:
     kernels = {}
     for name in sorted(set(fetch) | set(write)):
         fk, wk = fetch.get(name), write.get(name)
+        t = (2 * fk * 1024 if fk is not None else 0) + (wk * 1024 if wk is not None else 0)
+        k = kernels.get(short(name))
+        if k is not None:  # several instantiations launched per step (e.g. the tiny kernel's two parts): summed
+            k["kernel"] += " + " + name
+            k["traffic_bytes_per_launch"] += t
+            continue
         kernels[short(name)] = {
             "kernel": name,
             "fetch_size_kib_median": fk,
             "write_size_kib_median": wk,
-            "traffic_bytes_per_launch": (2 * fk * 1024 if fk is not None else 0) + (wk * 1024 if wk is not None else 0),
+            "traffic_bytes_per_launch": t,
         }
     json.dump({"config": config, "source_hash": source_hash(), "correction": "FETCH_SIZE x 2 x 1024 + WRITE_SIZE x 1024",
                "kernels": kernels}, open(out, "w"), indent=1)
