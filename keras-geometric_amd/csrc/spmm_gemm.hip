@@ -634,17 +634,23 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
 // One barrier per tile hands a tile from producers to MFMA waves.
 constexpr int kTinyThreads = 1024;
 constexpr int kTinyGroups = 16;  // producer row groups
+// rows per group per tile (= 16-row MFMA blocks per tile): two-edge rows / one-edge rows
 #ifndef KGX_TINY_RPG
 #define KGX_TINY_RPG 2
 #endif
-constexpr int kTinyRPG = KGX_TINY_RPG;  // rows per group per tile (= 16-row MFMA blocks per tile)
-constexpr int kTinyRows = kTinyGroups * kTinyRPG;
+#ifndef KGX_TINY_RPG1
+#define KGX_TINY_RPG1 4
+#endif
+template <int NG>
+constexpr int tiny_rows() { return kTinyGroups * (NG == 1 ? KGX_TINY_RPG1 : KGX_TINY_RPG); }
 
 // NG: edges gathered per row (2 for the degree-2 head of the tail, 1 for the
 // degree <= 1 rest: the schedule is degree-descending, so each is a range).
 template <int RED, bool WEIGHTED, bool EXTRA, int NG>  // EXTRA: pre_gin or agg_out (loads / stores under a row mask)
 __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedArgs a) {
   using R = Red<RED>;
+  constexpr int kTinyRPG = NG == 1 ? KGX_TINY_RPG1 : KGX_TINY_RPG;  // rows per group per tile
+  constexpr int kTinyRows = kTinyGroups * kTinyRPG;
   __shared__ __attribute__((aligned(16))) short planes[2][3][kTinyRows][kFin + 8];
   __shared__ int32_t trow[2][kTinyRows];
   const int tid = threadIdx.x;
@@ -938,7 +944,8 @@ int launch(const FusedArgs& a, hipStream_t s) {
       if (b.n_tiny <= 0) continue;
       auto k = part ? (extra ? spmm_gemm_tiny_kernel<RED, W, true, 1> : spmm_gemm_tiny_kernel<RED, W, false, 1>)
                     : (extra ? spmm_gemm_tiny_kernel<RED, W, true, 2> : spmm_gemm_tiny_kernel<RED, W, false, 2>);
-      const int64_t need = (b.n_tiny + kTinyRows - 1) / kTinyRows;
+      const int rows = part ? tiny_rows<1>() : tiny_rows<2>();
+      const int64_t need = (b.n_tiny + rows - 1) / rows;
       const int64_t cap = a.share_gpu ? int64_t(cu_count()) * 7 / 8 : int64_t(cu_count());
       hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kTinyThreads), 0, s, b);
       KGX_CHECK_LAUNCH();
