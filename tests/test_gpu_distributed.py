@@ -43,6 +43,9 @@ class ThreadComm(kd.TorchComm):
         w = self.hub.world
         in_splits = in_splits or [inp.shape[0] // w] * w
         self.hub.slots[self.r] = [c.clone() for c in torch.split(inp, list(in_splits))]
+        # the clones are queued on this rank's stream: they must have run before
+        # a peer (another thread, another stream) reads them
+        torch.cuda.synchronize()
         self.hub.barrier.wait()
         parts = [self.hub.slots[src][self.r] for src in range(w)]
         if out.numel():
@@ -57,6 +60,7 @@ class ThreadComm(kd.TorchComm):
     def broadcast(self, t, src=0):
         if self.r == src:
             self.hub.slots[src] = t.detach().clone()
+            torch.cuda.synchronize()
         self.hub.barrier.wait()
         t.copy_(self.hub.slots[src])
         torch.cuda.synchronize()
