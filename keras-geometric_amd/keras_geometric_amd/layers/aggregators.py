@@ -36,12 +36,19 @@ class Aggregator(ABC):
             return torch.zeros((dim_size, messages.shape[1]), dtype=messages.dtype, device=messages.device)
         if graph is None:
             tgt = to_device_tensor(target_idx, torch.int32, messages.device).reshape(-1)
-            if self.reduce == "std" and bool((tgt >= dim_size).any()):
-                # StdAggregator gathers mean[target] with take() (aggregators.py:208),
-                # which raises on ids >= dim_size; the segment sums alone would drop them.
-                raise IndexError("index out of range in self")
             ei = torch.stack([torch.zeros_like(tgt), tgt])
             graph = graph_for(target_idx, ei, 0, int(dim_size), segment_only=True, n_features=messages.shape[1])
+            if self.reduce == "std":
+                # StdAggregator gathers mean[target] with take() (aggregators.py:208), which
+                # wraps ids in [-dim_size, 0) and raises outside [-dim_size, dim_size); the
+                # segment sums alone would drop them.  Checked once per cached graph (one host
+                # sync beside the CSR build's own), not on every call.
+                oob = getattr(graph, "_take_oob", None)
+                if oob is None:
+                    oob = bool(((tgt >= dim_size) | (tgt < -dim_size)).any())
+                    graph._take_oob = oob
+                if oob:
+                    raise IndexError("index out of range in self")
         return self._reduce(graph, messages, exact)
 
     def _reduce(self, graph: CSRGraph, messages: torch.Tensor, exact: bool) -> torch.Tensor:

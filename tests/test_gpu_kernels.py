@@ -200,6 +200,13 @@ def test_by_edge_messages_segment_semantics(dev):
     tgt2 = np.minimum(tgt, n - 1)
     out = std.aggregate(T(m).to(dev), T(tgt2).to(dev), n, exact=True)
     exact_or_sqrt_ulp(out.cpu(), R.aggregate("std", T(m), T(tgt2), n), "std")
+    # ... and on ids < -n (take's wrap only covers [-n, 0)); the verdict is cached on the graph
+    tgt3 = tgt2.copy()
+    tgt3[7] = -n - 1
+    t3 = T(tgt3).to(dev)
+    for _ in range(2):
+        with pytest.raises(IndexError):
+            std.aggregate(T(m).to(dev), t3, n)
 
 
 @pytest.mark.parametrize("F", [1, 3, 6, 7, 100, 128, 256, 300, 520, 1100])
