@@ -99,7 +99,15 @@ constexpr int kProducerWaves = 4;
 // vmcnt waits) in waves that issue no MFMA means a wait on a prefetch never
 // stalls the matrix pipe, and the consumers' output stores never delay a
 // prefetch wait.
-template <int KS, int WAVES, bool ACC, bool TWO>
+//
+// LS (non-accumulating form, vec_out): full-line output stores.  The 16x16
+// MFMA result leaves each lane one column of four rows, so a wave's dword
+// stores cover 64 B of a row per 128-B line (its neighbour wave writes the
+// other half).  With LS the consumers park each finished tile in an LDS out
+// tile (Os, double-buffered by tile parity) and, during the next tile's last
+// k-step, every wave reads two whole-row float4 runs back and stores them with
+// dwordx4: one wave instruction = two 512-B rows.
+template <int KS, int WAVES, bool ACC, bool TWO, bool LS = false>
 __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(DenseArgs a) {
   using G = Geom<KS>;
   constexpr int TP = 64 * kProducerWaves;
@@ -111,6 +119,7 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
   constexpr int OCOLS = 16 * WAVES;
   constexpr int OSTRIDE = OCOLS + 4;  // floats; 4 mod 32 dwords between rows
   __shared__ float Os[2][kBM][OSTRIDE];
+  __shared__ float Ob[LS ? OCOLS : 1];  // LS: this block's bias columns (read beside the out rows)
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
@@ -379,7 +388,45 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
   // is out of range (vec_out: N % 4 == 0, so no group straddles N)
   const uint32_t out_row = col4 < a.N ? uint32_t((lr * a.ld_out + col4) * 4) : 0x80000000u;
 #endif
+  if constexpr (LS) {
+    if (wave == 0)
+      for (int c = l; c < OCOLS; c += 64) Ob[c] = (a.bias && cg * OCOLS + c < a.N) ? a.bias[cg * OCOLS + c] : 0.0f;
+  }
   lds_barrier();
+
+  // LS: out-tile float4 q = 128 wave + 64 m + l (m = 0, 1) -> row q / OC4, float4 column l % OC4
+  constexpr int OC4L = OCOLS / 4;
+  const int lc4 = l % OC4L;
+  const int lrow0 = (wave * 128 + l) / OC4L;
+  constexpr int LROWS = 64 / OC4L;  // rows between a lane's two float4
+  const int locol = cg * OCOLS + 4 * lc4;
+  const uint32_t lo_off = locol < a.N ? uint32_t((lrow0 * a.ld_out + locol) * 4) : 0x80000000u;
+  auto tile_rsrc_ls = [&](int64_t tile) {  // rows past M fall outside the record count
+    const int64_t r0 = tile * kBM;
+    int64_t rows = a.M - r0;
+    rows = rows > kBM ? kBM : rows;
+    const uint64_t addr = reinterpret_cast<uint64_t>(a.out) + uint64_t(r0 * a.ld_out * 4);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(addr));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(addr >> 32));
+    const int bytes = __builtin_amdgcn_readfirstlane(int(rows * a.ld_out * 4));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((uint64_t(hi) << 32) | lo), 0, bytes,
+                                             0x00020000);
+  };
+  auto lprev_rs = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, 0, 0x00020000);  // zero records: first tile's stores dropped
+  f32x4 lov[2], lb4;
+  auto lstore_prev = [&]() {
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      f32x4 v = lov[m];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[j] = v[j] + lb4[j];
+        if (a.relu) v[j] = fmaxf(v[j], 0.0f);
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), lprev_rs, lo_off,
+                                             int(m * LROWS * a.ld_out * 4), 0);
+    }
+  };
 
   int64_t t = pid;
   for (int64_t i = 0; i < my_tiles; ++i, t += n_pairs) {
@@ -423,12 +470,19 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
         constexpr int s = decltype(S)::value;
         Frags& cur = (s & 1) ? fb : fa;
         Frags& nxt = (s & 1) ? fa : fb;
+        if constexpr (LS && s == KS - 1) {  // the previous tile's out rows (last k-step: no next-step fragments live; its lgkmcnt(0) covers them)
+          const uint32_t ob = uint32_t(reinterpret_cast<uintptr_t>(&Os[buf ^ 1][lrow0][4 * lc4]));
+          asm volatile("ds_read_b128 %0, %1" : "=v"(lov[0]) : "v"(ob));
+          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(lov[1]) : "v"(ob), "i"(LROWS * OSTRIDE * 4));
+          asm volatile("ds_read_b128 %0, %1" : "=v"(lb4) : "v"(uint32_t(reinterpret_cast<uintptr_t>(&Ob[4 * lc4]))));
+        }
         if constexpr (s + 1 < KS) {
           read_frags(nxt, std::integral_constant<int, s + 1>{}, lds_lane);
           wait_frags(cur, acc, std::integral_constant<int, 6>{});
         } else {
           wait_frags(cur, acc, std::integral_constant<int, 0>{});
         }
+        if constexpr (LS && s == KS - 1) asm volatile("" : "+v"(lov[0]), "+v"(lov[1]), "+v"(lb4));
         // small terms first; two independent accumulator chains (row tiles).
         // Experiment KGX_DENSE_TRANSPOSED: D = W^T x^T, so a lane ends with 4
         // consecutive output columns of one row (one dwordx4 store per block)
@@ -455,6 +509,7 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
 #pragma unroll
         for (int r = 0; r < 2; ++r) acc[r] = KGX_MF(cur.h[r], wh[s], acc[r]);
 #undef KGX_MF
+        if constexpr (LS && s == KS - 1) lstore_prev();
       };
       [&]<int... S>(std::integer_sequence<int, S...>) {
         (step(std::integral_constant<int, S>{}), ...);
@@ -463,7 +518,14 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
     // Raw buffer stores through a per-tile descriptor: rows past M fall
     // outside its record count and columns past N carry an out-of-range
     // offset, so both are dropped by the range check (no branches).
-    if (!TWO && !ACC && a.pstore) {
+    if constexpr (LS) {
+      // this tile into the LDS out tile (stored during the next tile); lane holds rows 4 lq + j of column lr
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) Os[buf][16 * r + 4 * lq + j][wave * 16 + lr] = acc[r][j];
+      lprev_rs = tile_rsrc_ls(t);
+    } else if (!TWO && !ACC && a.pstore) {
       // lane holds rows 4 lq + j of column lr of each 16x16 block: into the LDS
       // out tile for the producers' stores (bias / ReLU applied there)
 #pragma unroll
@@ -532,12 +594,27 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
     }
     lds_barrier();  // buffer `buf` free for the producers; the stores stay in flight
   }
+  if constexpr (LS) {  // the last tile's rows (written before the last barrier)
+    const int lb = int((my_tiles - 1) & 1);
+#pragma unroll
+    for (int m = 0; m < 2; ++m) lov[m] = *reinterpret_cast<const f32x4*>(&Os[lb][lrow0 + m * LROWS][4 * lc4]);
+    lb4 = *reinterpret_cast<const f32x4*>(&Ob[4 * lc4]);
+    lstore_prev();
+  }
 }
 
 template <int KS, int WAVES>
 int launch(const DenseArgs& a, hipStream_t s) {
   auto k = a.accumulate ? (a.K1 > 0 ? dense_kernel<KS, WAVES, true, true> : dense_kernel<KS, WAVES, true, false>)
                         : (a.K1 > 0 ? dense_kernel<KS, WAVES, false, true> : dense_kernel<KS, WAVES, false, false>);
+#ifndef KGX_DENSE_NO_LS
+  // K > 128 only: measured C4 (K 256) 6.91 -> 6.66 ms, C5 (K 200) 0.90 -> 0.86 ms, but the
+  // 10M x 128 -> 128 shape 2.13 -> 2.18 ms (half the MFMA time per tile to hide the extra LDS traffic)
+  if constexpr (KS == 8) {
+    if (!a.accumulate && a.vec_out && !a.pstore && a.debug == 0)
+      k = a.K1 > 0 ? dense_kernel<KS, WAVES, false, true, true> : dense_kernel<KS, WAVES, false, false, true>;
+  }
+#endif
   static int cus = 0;
   if (cus == 0) {
     int dev = 0;
