@@ -71,7 +71,9 @@ def pmc_traffic(config: str, kernels) -> tuple[float | None, str | None]:
     """HBM bytes per step of the launches in `kernels` (summed: one op may be
     several kernels) from the newest committed rocprofv3 PMC summary
     (profiles/r*/pmc_<config>.json, written by tools/pmc_summary.py), used only
-    if it was profiled from the kernel sources being run."""
+    if every kernel it sums was profiled from the source files being run: each
+    kernel entry carries the hash of the .hip file defining it plus its headers
+    (older summaries: one hash over all of csrc/)."""
     import importlib.util
 
     spec = importlib.util.spec_from_file_location("pmc_summary", ROOT / "tools" / "pmc_summary.py")
@@ -80,10 +82,16 @@ def pmc_traffic(config: str, kernels) -> tuple[float | None, str | None]:
     kernels = [kernels] if isinstance(kernels, str) else list(kernels)
     for path in sorted(ROOT.glob(f"profiles/r*/pmc_{config}.json"), reverse=True):
         d = json.loads(path.read_text())
-        if d.get("source_hash") != mod.source_hash() or kernels[0] not in d.get("kernels", {}):
+        have = d.get("kernels", {})
+        if kernels[0] not in have:
             continue
-        have = d["kernels"]
-        return sum(have[k]["traffic_bytes_per_launch"] for k in kernels if k in have), str(path.relative_to(ROOT))
+        used = [k for k in kernels if k in have]
+        if all("source_hash" in have[k] for k in used):
+            if any(have[k]["source_hash"] != mod.kernel_source_hash(k) for k in used):
+                continue
+        elif d.get("source_hash") != mod.source_hash():
+            continue
+        return sum(have[k]["traffic_bytes_per_launch"] for k in used), str(path.relative_to(ROOT))
     return None, None
 
 
@@ -123,7 +131,7 @@ def host_cpus() -> dict:
             "affinity_cpus": affinity, "cgroup_cpu_quota": quota}
 
 
-def cpu_baseline(device: torch.device) -> dict:
+def cpu_baseline(device: torch.device, repeats: int = 3) -> dict:
     """Time the oracle's op-for-op Keras-torch CPU GCNConv forward (the reference's
     CPU path) on a bounded sample: the C2-shaped 1M-node / 10M-edge R-MAT graph,
     with every CPU this process may run on (os.cpu_count(), limited by its
@@ -141,18 +149,25 @@ def cpu_baseline(device: torch.device) -> dict:
     x = torch.randn(n, f, generator=g)
     w = (torch.rand(f, f, generator=g) * 2 - 1) * (6.0 / (2 * f)) ** 0.5
     b = torch.zeros(f)
-    t0 = time.perf_counter()
-    y = R.gcn_forward(x, ei, w, b)
-    dt = time.perf_counter() - t0
-    del y
+    # SURVEY.md §8(d) / BASELINE.md §3: median of 3 timed forwards after 1 warm-up
+    times = []
+    for i in range(1 + repeats):
+        t0 = time.perf_counter()
+        y = R.gcn_forward(x, ei, w, b)
+        dt = time.perf_counter() - t0
+        del y
+        if i:
+            times.append(dt)
+    med = sorted(times)[len(times) // 2]
     return {
-        "value": (e + n) / dt,
+        "value": (e + n) / med,
         "unit": "edges/s",
         "cores": threads,
         "kind": "port",
         "host": info,
         "sample": f"oracle GCNConv fwd (Keras-torch CPU lowering, op for op) on R-MAT N={n} E={e} "
-                  f"(+{n} self loops) F {f}->{f}, 1 timed forward = {dt:.2f} s, torch threads={threads}",
+                  f"(+{n} self loops) F {f}->{f}, median of {repeats} timed forwards after 1 warm-up = "
+                  f"{med:.2f} s (all: {', '.join(f'{t:.2f}' for t in times)} s), torch threads={threads}",
     }
 
 

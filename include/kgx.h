@@ -236,6 +236,22 @@ int kgx_spmm_gemm_ex2(int reduce, const int32_t* rowptr, const int32_t* rows, in
                       const float* W, int64_t F_out, const float* bias, int flags, float gin_scale, float* out,
                       int64_t ld_out, float* partials, float* agg_out, int64_t ld_agg, kgx_stream_t stream);
 
+/* kgx_spmm_gemm_ex3: kgx_spmm_gemm_ex2 gathering from TWO feature tables:
+ * source columns c < n_x1 are rows of x, columns c >= n_x1 are rows
+ * c - n_x1 of x2 (same leading dimension ld_x, 16-byte aligned).  The sharded
+ * layers' halo pass reads a row's own-source edges from the layer input and
+ * its halo edges from the exchange's receive buffer in ONE pass, so the row is
+ * written once instead of written and read-modify-written (distributed.py;
+ * gcn_conv.py:233-272 per shard).  x2 NULL: kgx_spmm_gemm_ex2.  Rows indexed
+ * by pre_gin are rows of x. */
+int kgx_spmm_gemm_ex3(int reduce, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
+                      const int32_t* items, int64_t n_items, int64_t n_long_items, int64_t n_short_end,
+                      const int32_t* tiny_pack, const float* tiny_w, int64_t n_tiny_deg2,
+                      const int32_t* split, int64_t n_split, const int32_t* idx, const float* w,
+                      const float* x, int64_t ld_x, const float* x2, int64_t n_x1, int64_t F_in,
+                      const float* W, int64_t F_out, const float* bias, int flags, float gin_scale, float* out,
+                      int64_t ld_out, float* partials, float* agg_out, int64_t ld_agg, kgx_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * Backward of the segment max / min reduction (autograd of kgx_spmm MAX/MIN).
  * torch's scatter_reduce amax/amin backward, under the reference's isinf

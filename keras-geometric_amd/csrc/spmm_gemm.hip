@@ -76,7 +76,17 @@ struct FusedArgs {
   const float2* tw;     // their weights {w0, w1} (weighted reductions)
   int64_t n_tiny;       // rows in tpack
   int64_t n_tiny2;      // the first n_tiny2 of them have degree 2 (the rest <= 1)
+  // two-table gathers (kgx_spmm_gemm_ex3): sources col >= n_x1 are rows of a
+  // second table x2 (same ld_x); x2b = x2 - n_x1 * ld_x (host address math), so
+  // the gather address is one select of the base.  n_x1 = INT32_MAX: one table.
+  const float* x2b;
+  int32_t n_x1;
 };
+
+// Source row of column c: x[c] or x2[c - n_x1] (one 64-bit select per gathered row).
+__device__ __forceinline__ const float* gsrc(const FusedArgs& a, int32_t c) {
+  return (c >= a.n_x1 ? a.x2b : a.x) + row_off(c, a.ld_x);
+}
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops
 // (lgkmcnt) but NOT for its outstanding global loads (vmcnt), unlike
@@ -234,7 +244,7 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
       if (u < pn)  // exec-masked: rows of degree < PF issue no redundant loads
-        vload<4>(pv[u], a.x + row_off(c[u], a.ld_x) + f);
+        vload<4>(pv[u], gsrc(a, c[u]) + f);
     }
   };
 
@@ -281,7 +291,7 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
 #endif
       float v[B][4];
 #pragma unroll
-      for (int u = 0; u < B; ++u) vload<4>(v[u], a.x + row_off(c[u], a.ld_x) + f);
+      for (int u = 0; u < B; ++u) vload<4>(v[u], gsrc(a, c[u]) + f);
 #pragma unroll
       for (int u = 0; u < B; ++u)
 #pragma unroll
@@ -487,7 +497,7 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
       for (int r = 0; r < kRPG; ++r)
 #pragma unroll
         for (int u = 0; u < kSPF; ++u)
-          if (u < deg[r]) vload<4>(v[r][u], a.x + row_off(c[r][u], a.ld_x) + f);
+          if (u < deg[r]) vload<4>(v[r][u], gsrc(a, c[r][u]) + f);
 #pragma unroll
       for (int r = 0; r < kRPG; ++r)
 #pragma unroll
@@ -515,7 +525,7 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
           if constexpr (WEIGHTED) wt[u] = a.w[ee];
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) vload<4>(v[u], a.x + row_off(c[u], a.ld_x) + f);
+        for (int u = 0; u < 2; ++u) vload<4>(v[u], gsrc(a, c[u]) + f);
 #pragma unroll
         for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -749,8 +759,8 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
   auto gather = [&](const Rec& r, f4 (&v)[kTinyRPG][NG]) {
 #pragma unroll
     for (int j = 0; j < kTinyRPG; ++j) {
-      v[j][0] = *reinterpret_cast<const f4*>(a.x + row_off(r.p[j].z, a.ld_x) + f);
-      if constexpr (NG == 2) v[j][1] = *reinterpret_cast<const f4*>(a.x + row_off(r.p[j].w, a.ld_x) + f);
+      v[j][0] = *reinterpret_cast<const f4*>(gsrc(a, r.p[j].z) + f);
+      if constexpr (NG == 2) v[j][1] = *reinterpret_cast<const f4*>(gsrc(a, r.p[j].w) + f);
     }
   };
   auto produce = [&](int64_t i, const auto& c, const f4 (&v)[kTinyRPG][NG]) {
@@ -994,7 +1004,24 @@ extern "C" int kgx_spmm_gemm_ex2(int reduce, const int32_t* rowptr, const int32_
                                  int64_t F_in, const float* W, int64_t F_out, const float* bias, int flags,
                                  float gin_scale, float* out, int64_t ld_out, float* partials, float* agg_out,
                                  int64_t ld_agg, kgx_stream_t stream_) {
+  return kgx_spmm_gemm_ex3(reduce, rowptr, rows, n_rows, items, n_items, n_long_items, n_short_end, tiny_pack, tiny_w,
+                           n_tiny_deg2, split, n_split, idx, w, x, ld_x, nullptr, 0, F_in, W, F_out, bias, flags,
+                           gin_scale, out, ld_out, partials, agg_out, ld_agg, stream_);
+}
+
+extern "C" int kgx_spmm_gemm_ex3(int reduce, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
+                                 const int32_t* items, int64_t n_items, int64_t n_long_items, int64_t n_short_end,
+                                 const int32_t* tiny_pack, const float* tiny_w, int64_t n_tiny_deg2,
+                                 const int32_t* split, int64_t n_split, const int32_t* idx, const float* w,
+                                 const float* x, int64_t ld_x, const float* x2, int64_t n_x1, int64_t F_in,
+                                 const float* W, int64_t F_out, const float* bias, int flags, float gin_scale,
+                                 float* out, int64_t ld_out, float* partials, float* agg_out, int64_t ld_agg,
+                                 kgx_stream_t stream_) {
   hipStream_t stream = as_stream(stream_);
+  KGX_REQUIRE(!x2 || (n_x1 >= 0 && n_x1 < (int64_t(1) << 31) && reinterpret_cast<uintptr_t>(x2) % 16 == 0),
+              KGX_ERR_ARG, "kgx_spmm_gemm: x2 must be 16-byte aligned and 0 <= n_x1 < 2^31");
+  KGX_REQUIRE(!items || tiny_pack || n_short_end == n_items, KGX_ERR_ARG,
+              "kgx_spmm_gemm: without tiny_pack, n_short_end must equal n_items");
   KGX_REQUIRE(!items || (n_long_items >= 0 && n_long_items <= n_short_end && n_short_end <= n_items), KGX_ERR_ARG,
               "kgx_spmm_gemm: need 0 <= n_long_items <= n_short_end <= n_items");
   KGX_REQUIRE(!tiny_pack || (items && (w == nullptr || tiny_w)), KGX_ERR_ARG,
@@ -1038,6 +1065,11 @@ extern "C" int kgx_spmm_gemm_ex2(int reduce, const int32_t* rowptr, const int32_
   a.w = w;
   a.x = x;
   a.ld_x = ld_x;
+  a.n_x1 = x2 ? int32_t(n_x1) : INT32_MAX;
+  // x2 - n_x1 * ld_x as an address (modular): gsrc adds row_off(c) for c >= n_x1
+  a.x2b = x2 ? reinterpret_cast<const float*>(reinterpret_cast<uintptr_t>(x2) -
+                                               uintptr_t(n_x1) * uintptr_t(ld_x) * sizeof(float))
+             : x;
   a.W = W;
   a.F_out = int(F_out);
   a.bias = bias;

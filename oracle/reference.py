@@ -222,8 +222,14 @@ def sage_forward(x, edge_index, w_neigh, w_self=None, bias=None, aggregator="mea
 
 
 def gatv2_forward(x, edge_index, kernel, att, bias=None, heads=1, concat=True, negative_slope=0.2,
-                  add_self_loops_: bool = True):
-    """GATv2Conv.call/_gatv2_propagate (gatv2_conv.py:129-352)."""
+                  add_self_loops_: bool = True, lrelu_positive=None):
+    """GATv2Conv.call/_gatv2_propagate (gatv2_conv.py:129-352).
+
+    lrelu_positive (test instrument, default None = the reference): a bool
+    [E', heads, C] mask fixing which branch the leaky ReLU of :277-278 takes.
+    Its derivative jumps from 1 to negative_slope at z = 0, so where an fp32
+    and an fp64 evaluation put a z within ~1e-8 of 0 on opposite sides their
+    gradients differ at O(1) for that edge (tests/test_gatv2_conditioning.py)."""
     x = K.convert(x)
     ei = K.cast(K.convert(edge_index), torch.int32)
     kernel = K.convert(kernel)
@@ -241,7 +247,11 @@ def gatv2_forward(x, edge_index, kernel, att, bias=None, heads=1, concat=True, n
     src, dst = ei[0], ei[1]
     h_j = K.take(h, src, axis=0)
     h_i = K.take(h, dst, axis=0)
-    z = K.leaky_relu(K.add(h_i, h_j), negative_slope)  # :277-278
+    if lrelu_positive is None:
+        z = K.leaky_relu(K.add(h_i, h_j), negative_slope)  # :277-278
+    else:
+        zin = K.add(h_i, h_j)
+        z = torch.where(lrelu_positive, zin, zin * negative_slope)
     scores = torch.sum(K.multiply(z, K.convert(att)), dim=-1)  # :284
     mx = K.segment_max(scores, dst, n)  # :298
     ex = torch.exp(torch.subtract(scores, K.take(mx, dst, axis=0)))  # :299-302

@@ -12,9 +12,11 @@ is doubled -- verified for this kernel family's row-gather pattern by the
 calibration in tools/exp_agg.py `calib`.
 WRITE_SIZE is exact for 16-B-per-lane stores.
 
-The output carries a hash of the kernel sources; bench.py only attaches the
-traffic when the hash matches the sources it runs, so a stale profile is never
-reported against a changed kernel.
+Every kernel entry carries a hash of ITS sources: the .hip file that defines
+it plus the headers that file includes (kernel_source_hash); bench.py attaches
+the traffic only when the hash of each kernel it reports matches the sources
+it runs, so a stale profile is never reported against a changed kernel, and an
+edit to an unrelated kernel's file does not invalidate it.
 """
 
 from __future__ import annotations
@@ -22,6 +24,7 @@ from __future__ import annotations
 import csv
 import hashlib
 import json
+import re
 import statistics
 import sys
 from pathlib import Path
@@ -30,12 +33,52 @@ ROOT = Path(__file__).resolve().parents[1]
 CSRC = ROOT / "keras-geometric_amd" / "csrc"
 
 
+INCLUDE = ROOT / "include"
+
+
 def source_hash() -> str:
+    """Hash of every kernel source (kept for the profile's header; per-kernel
+    validity uses kernel_source_hash)."""
     h = hashlib.sha256()
     for p in sorted(CSRC.glob("*")):
         if p.suffix in (".hip", ".cpp", ".h"):
             h.update(p.name.encode())
             h.update(p.read_bytes())
+    return h.hexdigest()[:16]
+
+
+def _closure(path: Path, seen: set) -> None:
+    """path and the local headers it includes, transitively."""
+    if path in seen or not path.exists():
+        return
+    seen.add(path)
+    for inc in re.findall(r'#include\s+"([^"]+)"', path.read_text()):
+        for d in (path.parent, CSRC, INCLUDE):
+            if (d / inc).exists():
+                _closure(d / inc, seen)
+                break
+
+
+def kernel_file(kernel: str) -> Path | None:
+    """The .hip file whose __global__ function is named `kernel` (a short name)."""
+    pat = re.compile(r"__global__[^;{]*?\b" + re.escape(kernel) + r"\s*\(", re.S)
+    for p in sorted(CSRC.glob("*.hip")):
+        if pat.search(p.read_text()):
+            return p
+    return None
+
+
+def kernel_source_hash(kernel: str) -> str | None:
+    """Hash of the source file defining `kernel` and the headers it includes."""
+    f = kernel_file(kernel)
+    if f is None:
+        return None
+    files: set = set()
+    _closure(f, files)
+    h = hashlib.sha256()
+    for p in sorted(files, key=lambda q: q.name):
+        h.update(p.name.encode())
+        h.update(p.read_bytes())
     return h.hexdigest()[:16]
 
 
@@ -71,6 +114,7 @@ def main() -> None:
             continue
         kernels[short(name)] = {
             "kernel": name,
+            "source_hash": kernel_source_hash(short(name)),
             "fetch_size_kib_median": fk,
             "write_size_kib_median": wk,
             "traffic_bytes_per_launch": t,
