@@ -330,18 +330,22 @@ def main() -> None:
             with torch.no_grad():
                 return layer(x)
 
-        pp = sg._pp  # push-pull halo plan of the default path (None: pull-only or EXACT)
-        n_moved = pp.n_rows if pp is not None else sg.n_halo
+        pp = sg._pp  # exchange plan of the default path (None: pull-only table path or EXACT)
+        if pp is not None and pp.kind == "allgather":  # every rank's rows; this rank's own slice is not moved
+            n_moved = pp.n_rows * (world - 1) // world
+        else:
+            n_moved = pp.n_rows if pp is not None else sg.n_halo
         # exchanged row width: X rows (F_in) on the aggregate-first paths, X W rows
         # (F_out) when the GCN layer transforms first (shapes the fused kernel does not take)
         transform_first = kind == "gcn" and (args.exact or not kops.fused_transform_supported(f_in, f_out)
                                              and f_out < f_in)
         f_x = f_out if transform_first else f_in
-        shard_info = {"halo_rows_pull_only": sg.n_halo, "halo_rows": n_moved,
+        shard_info = {"exchange": pp.kind if pp is not None else "pull-table",
+                      "halo_rows_pull_only": sg.n_halo, "halo_rows": n_moved,
                       "halo_rows_pushed_partials": pp.n_push if pp is not None else 0,
                       "halo_MB_per_layer": n_moved * f_x * 4 / 1e6,
                       "halo_chunks": sg.halo_k if sg.halo_k is not None else (len(pp.chunks) if pp else len(sg.chunks)),
-                      "halo_chunk_tuning_s": sg.tuning}
+                      "exchange_tuning_s": sg.tuning}
 
     for _ in range(args.warmup):
         step()
@@ -417,7 +421,8 @@ def main() -> None:
     wl += " (+self loops), normalized, bias" if kind == "gcn" else ""
     wl += f", F {f_in}->{f_out}"
     if world > 1:
-        wl += ", dst-range shards, RCCL halo all-to-all pipelined under the own-source pass"
+        wl += (", dst-range shards, RCCL all-gather of node rows" if shard_info.get("exchange") == "allgather"
+               else ", dst-range shards, RCCL halo all-to-all") + " pipelined under the own-source pass"
     result = {
         "metric": METRIC if kind == "gcn" else f"aggregated edges/sec + achieved HBM GB/s, {LAYER_NAME[kind]} fwd",
         "value": value,

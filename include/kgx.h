@@ -169,6 +169,18 @@ int kgx_spmm_ex(int reduce, int epilogue, const int32_t* rowptr, const int32_t* 
                 float gin_scale, const int32_t* drop_key, float drop_p, uint64_t drop_seed, float* partials,
                 kgx_stream_t stream);
 
+/* kgx_spmm_ex2: kgx_spmm_ex gathering from TWO tables: sources c < n_table1 are
+ * rows of table, c >= n_table1 rows c - n_table1 of table2 (same ld_table).
+ * Needs the schedule (items; not EXACT / std).  The sharded GIN / SAGE layers
+ * reduce a row's own-source and halo edges in one pass (distributed.py).
+ * table2 NULL: kgx_spmm_ex. */
+int kgx_spmm_ex2(int reduce, int epilogue, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
+                 const int32_t* items, int64_t n_items, int64_t n_long_items, const int32_t* split, int64_t n_split,
+                 const int32_t* idx, const float* w, const float* table, int64_t ld_table, const float* table2,
+                 int64_t n_table1, int64_t F, float* out, int64_t ld_out, const float* bias, const float* xroot,
+                 int64_t ld_x, float gin_scale, const int32_t* drop_key, float drop_p, uint64_t drop_seed,
+                 float* partials, kgx_stream_t stream);
+
 /* Message dropout mask (training; GCNConv.message dropout, gcn_conv.py:237-242;
  * GATv2 attention dropout, gatv2_conv.py:252-253): element (key, f) is kept
  * with probability 1 - p and scaled by 1/(1-p).  The mask is a pure function

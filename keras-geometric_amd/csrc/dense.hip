@@ -214,9 +214,11 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
 #ifndef KGX_DENSE_OLD_SPLIT
       // fast path: paired conversions (split3_pair_rn, ~4.5 VALU per element:
       // the producer's split must fit in the issue slots the consumers' MFMAs
-      // leave free on its SIMD).  chk = sum of 2x over the thread's slots is
-      // finite iff no element is inf / NaN or >= 2^127 (where bf16(x) could
-      // round to inf); otherwise the slots are redone with split3_a_lo below.
+      // leave free on its SIMD).  chk = sum of 2|x| over the thread's slots
+      // (|x| is a free source modifier of v_fma_f32): a sum of non-negative
+      // terms, so it is non-finite whenever one element is inf / NaN or
+      // >= 2^127 (where bf16(x) could round to inf) -- no cancellation can hide
+      // one -- and the slots are then redone with split3_a_lo below.
       float chk0 = 0.0f, chk1 = 0.0f;
 #pragma unroll
       for (int j = 0; j < NL; ++j) {
@@ -224,10 +226,10 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
         f32x4 x = p[j];
         if constexpr (TWO)
           x = __builtin_bit_cast(f32x4, __builtin_bit_cast(u32x4, p[j]) | __builtin_bit_cast(u32x4, q[j]));
-        chk0 = fmaf(x[0], 2.0f, chk0);
-        chk1 = fmaf(x[1], 2.0f, chk1);
-        chk0 = fmaf(x[2], 2.0f, chk0);
-        chk1 = fmaf(x[3], 2.0f, chk1);
+        chk0 = fmaf(fabsf(x[0]), 2.0f, chk0);
+        chk1 = fmaf(fabsf(x[1]), 2.0f, chk1);
+        chk0 = fmaf(fabsf(x[2]), 2.0f, chk0);
+        chk1 = fmaf(fabsf(x[3]), 2.0f, chk1);
         uint32_t h0, m0, l0, h1, m1, l1;
         split3_pair_rn(x[0], x[1], h0, m0, l0);
         split3_pair_rn(x[2], x[3], h1, m1, l1);
@@ -255,8 +257,8 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
           pm[e] = m;
           pl[e] = lo;
         }
-        // inf / NaN among the four (their sum is then non-finite): lo plane (rare)
-        if (!__builtin_isfinite(__fadd_rn(__fadd_rn(x[0], x[1]), __fadd_rn(x[2], x[3])))) {
+        // inf / NaN or a magnitude bf16 rounds to inf among the four: split3_a_lo (rare)
+        if (!split_fast_ok(x[0], x[1], x[2], x[3])) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             short h, m, lo;

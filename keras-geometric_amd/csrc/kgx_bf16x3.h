@@ -39,14 +39,34 @@ __device__ __forceinline__ void split3_a(float x, short& hi, short& mid, short& 
   lo = bf16_bits(r);
 }
 
-// activation split: non-finite values moved to the lo plane, (0, 0, x)
+// activation split for the rare path: non-finite values moved to the lo plane,
+// (0, 0, x); a finite x whose RNE bf16 overflows (|x| >= 0x1.ffp127) keeps
+// bf16's largest finite value (rounded toward zero) in hi, so x = hi + mid +
+// lo still holds exactly (Sterbenz: x - hi is exact) and x*w stays finite.
 __device__ __forceinline__ void split3_a_lo(float x, short& hi, short& mid, short& lo) {
-  const bool fin = __builtin_isfinite(x);
-  short h, m, l;
-  split3_a(x, h, m, l);
-  hi = fin ? h : short(0);
-  mid = fin ? m : short(0);
-  lo = fin ? l : h;  // h = bf16(x) = +-inf or NaN
+  if (__builtin_isfinite(x)) {
+    short h = bf16_bits(x);
+    if (!__builtin_isfinite(bf16_value(h))) h = x < 0.0f ? short(0xff7f) : short(0x7f7f);
+    float r = __fsub_rn(x, bf16_value(h));  // exact
+    const short m = bf16_bits(r);
+    r = __fsub_rn(r, bf16_value(m));  // exact
+    hi = h;
+    mid = m;
+    lo = bf16_bits(r);
+  } else {
+    hi = 0;
+    mid = 0;
+    lo = bf16_bits(x);  // +-inf or NaN
+  }
+}
+
+// The fast split (split3_a) is exact for four values iff none is inf / NaN
+// (their sum is then finite) and their largest magnitude is below 0x1.ffp127
+// (RNE to bf16 then stays finite: no cancellation in the sum can hide a huge
+// pair).  Otherwise the caller takes split3_a_lo.
+__device__ __forceinline__ bool split_fast_ok(float a, float b, float c, float d) {
+  const float m = fmaxf(fmaxf(fabsf(a), fabsf(b)), fmaxf(fabsf(c), fabsf(d)));
+  return __builtin_isfinite(__fadd_rn(__fadd_rn(a, b), __fadd_rn(c, d))) && m < 0x1.ffp127f;
 }
 
 // split3_a of a pair, packed (element 0 in the low half): fragments assembled

@@ -61,7 +61,19 @@ struct SpmmArgs {
   int f_base;  // first column of this launch (column slicing of wide F)
   int long_rows;  // EXACT mode: rows of degree >= kLongRow are reduced by spmm_long_kernel
   int64_t n_long;  // items [n_long, n_items): short rows (degree <= KGX_SHORT_ROW_MAX) for spmm_short_kernel
+  // two-table gathers (kgx_spmm_ex2): sources c >= n_t1 are rows c - n_t1 of a second
+  // table (same ld_t); t2b = table2 - n_t1 * ld_t as an address.  n_t1 = INT32_MAX: one table.
+  const float* t2b;
+  int32_t n_t1;
 };
+
+// Source row of column c: table[c], or with TWO table2[c - n_t1] (a separate
+// instantiation, so the one-table kernels keep their registers and issue).
+template <bool TWO>
+__device__ __forceinline__ const float* tsrc(const SpmmArgs& a, int32_t c) {
+  if constexpr (TWO) return (c >= a.n_t1 ? a.t2b : a.table) + row_off(c, a.ld_t);
+  return a.table + row_off(c, a.ld_t);
+}
 
 // EXACT mode has no hub split (each row is one sequential reduction), so a hub
 // row of 10^5 edges is a latency chain; rows this long get their own kernel
@@ -130,7 +142,7 @@ __device__ __forceinline__ void epilogue(const SpmmArgs& a, int32_t row, int f, 
 // to end-1, whose row is already being fetched), then an in-order fold where
 // clamped edges contribute the reduction's identity.  No load sits under a
 // lane-dependent branch, so hipcc keeps all U gathers in flight.
-template <int U, int VEC, int NT, int RED, bool WEIGHTED, bool DROP = false>
+template <int U, int VEC, int NT, int RED, bool WEIGHTED, bool DROP = false, bool TWO = false>
 __device__ __forceinline__ void edge_block(const SpmmArgs& a, int32_t e, int32_t end, const int (&fl)[NT],
                                            float (&acc)[NT][VEC]) {
   using R = Reducer<RED>;
@@ -157,7 +169,7 @@ __device__ __forceinline__ void edge_block(const SpmmArgs& a, int32_t e, int32_t
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int t = 0; t < NT; ++t) vload<VEC>(v[u][t], a.table + row_off(c[u], a.ld_t) + fl[t]);
+    for (int t = 0; t < NT; ++t) vload<VEC>(v[u][t], tsrc<TWO>(a, c[u]) + fl[t]);
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -173,7 +185,7 @@ __device__ __forceinline__ void edge_block(const SpmmArgs& a, int32_t e, int32_t
       }
 }
 
-template <int VEC, int NT, int RED, bool WEIGHTED, bool DROP = false>
+template <int VEC, int NT, int RED, bool WEIGHTED, bool DROP = false, bool TWO = false>
 __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
   using R = Reducer<RED>;
   // gathers in flight per group (NT = 1: 6 measured best at NS, 9.2-9.4 ms vs 9.5 at 8, 9.9 at 12)
@@ -223,10 +235,10 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
       for (int k = 0; k < VEC; ++k) acc[t][k] = R::init();
 
     int32_t e = beg;
-    for (; e + U <= end; e += U) edge_block<U, VEC, NT, RED, WEIGHTED, DROP>(a, e, end, fl, acc);
+    for (; e + U <= end; e += U) edge_block<U, VEC, NT, RED, WEIGHTED, DROP, TWO>(a, e, end, fl, acc);
     // tail in half-width blocks: at most TU-1 clamped (redundant, cache-hit) loads
     constexpr int TU = U > 1 ? U / 2 : 1;
-    for (; e < end; e += TU) edge_block<TU, VEC, NT, RED, WEIGHTED, DROP>(a, e, end, fl, acc);
+    for (; e < end; e += TU) edge_block<TU, VEC, NT, RED, WEIGHTED, DROP, TWO>(a, e, end, fl, acc);
 
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -560,7 +572,7 @@ __global__ __launch_bounds__(kHubThreads, 1) void spmm_hub_kernel(SpmmArgs a) {
 constexpr int kSR = KGX_SPMM_SHORT_R;
 constexpr int kSPF = KGX_SPMM_SHORT_PF;
 
-template <int VEC, int RED, bool WEIGHTED>
+template <int VEC, int RED, bool WEIGHTED, bool TWO = false>
 __global__ __launch_bounds__(kBlock) void spmm_short_kernel(SpmmArgs a) {
   using R = Reducer<RED>;
   const int G = a.G;
@@ -602,7 +614,7 @@ __global__ __launch_bounds__(kBlock) void spmm_short_kernel(SpmmArgs a) {
       for (int r = 0; r < kSR; ++r)
 #pragma unroll
         for (int u = 0; u < kSPF; ++u)
-          if (u < deg[r]) vload<VEC>(v[r][u], a.table + row_off(c[r][u], a.ld_t) + fl);
+          if (u < deg[r]) vload<VEC>(v[r][u], tsrc<TWO>(a, c[r][u]) + fl);
 #pragma unroll
       for (int r = 0; r < kSR; ++r)
 #pragma unroll
@@ -630,7 +642,7 @@ __global__ __launch_bounds__(kBlock) void spmm_short_kernel(SpmmArgs a) {
           if constexpr (WEIGHTED) wt[u] = a.w[ee];
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) vload<VEC>(v[u], a.table + row_off(c[u], a.ld_t) + fl);
+        for (int u = 0; u < 2; ++u) vload<VEC>(v[u], tsrc<TWO>(a, c[u]) + fl);
 #pragma unroll
         for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -742,7 +754,7 @@ __global__ __launch_bounds__(kBlock) void spmm_std_kernel(SpmmArgs a) {
 
 
 
-template <int VEC, int NT, int RED, bool W>
+template <int VEC, int NT, int RED, bool W, bool TWO = false>
 int launch_main(const SpmmArgs& a_in, hipStream_t s) {
   SpmmArgs a = a_in;
   if constexpr (NT == 1) {
@@ -774,7 +786,7 @@ int launch_main(const SpmmArgs& a_in, hipStream_t s) {
   }
   if constexpr (NT == 1) {
     if (a.items && a.n_long < a.n_items && !a.drop_key) {
-      auto ks = spmm_short_kernel<VEC, RED, W>;
+      auto ks = spmm_short_kernel<VEC, RED, W, TWO>;
       hipLaunchKernelGGL(ks, dim3(resident_grid(ks, (a.n_items - a.n_long + kSR - 1) / kSR, a.G)), dim3(kBlock), 0, s,
                          a);
       KGX_CHECK_LAUNCH();
@@ -786,8 +798,8 @@ int launch_main(const SpmmArgs& a_in, hipStream_t s) {
   }
   const int64_t work_long = a.items ? a.n_long : a.n_rows;
   if (work_long > 0) {
-    auto k = spmm_kernel<VEC, NT, RED, W>;
-    if constexpr (RED == KGX_SUM) {
+    auto k = spmm_kernel<VEC, NT, RED, W, false, TWO>;
+    if constexpr (RED == KGX_SUM && !TWO) {
       if (a.drop_key) k = spmm_kernel<VEC, NT, RED, W, true>;
     }
     hipLaunchKernelGGL(k, dim3(resident_grid(k, work_long, a.G)), dim3(kBlock), 0, s, a);
@@ -812,6 +824,10 @@ int dispatch_w(const SpmmArgs& a, hipStream_t s) {
     return KGX_OK;
   }
   constexpr int RR = RED == KGX_STD ? KGX_SUM : RED;
+  if constexpr (RR == KGX_SUM) {
+    if (a.n_t1 != INT32_MAX)  // two tables: plain / weighted sums (the sharded layers' merged pass)
+      return a.w ? launch_main<VEC, NT, RR, true, true>(a, s) : launch_main<VEC, NT, RR, false, true>(a, s);
+  }
   return a.w ? launch_main<VEC, NT, RR, true>(a, s) : launch_main<VEC, NT, RR, false>(a, s);
 }
 
@@ -859,7 +875,23 @@ extern "C" int kgx_spmm_ex(int reduce, int epilogue, const int32_t* rowptr, cons
                            int64_t F, float* out, int64_t ld_out, const float* bias, const float* xroot,
                            int64_t ld_x, float gin_scale, const int32_t* drop_key, float drop_p, uint64_t drop_seed,
                            float* partials, kgx_stream_t stream_) {
+  return kgx_spmm_ex2(reduce, epilogue, rowptr, rows, n_rows, items, n_items, n_long_items, split, n_split, idx, w,
+                      table, ld_table, nullptr, 0, F, out, ld_out, bias, xroot, ld_x, gin_scale, drop_key, drop_p,
+                      drop_seed, partials, stream_);
+}
+
+extern "C" int kgx_spmm_ex2(int reduce, int epilogue, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
+                            const int32_t* items, int64_t n_items, int64_t n_long_items, const int32_t* split,
+                            int64_t n_split, const int32_t* idx, const float* w, const float* table, int64_t ld_table,
+                            const float* table2, int64_t n_table1, int64_t F, float* out, int64_t ld_out,
+                            const float* bias, const float* xroot, int64_t ld_x, float gin_scale,
+                            const int32_t* drop_key, float drop_p, uint64_t drop_seed, float* partials,
+                            kgx_stream_t stream_) {
   hipStream_t stream = as_stream(stream_);
+  KGX_REQUIRE(!table2 || (n_table1 >= 0 && n_table1 < (int64_t(1) << 31) && items), KGX_ERR_ARG,
+              "kgx_spmm: a second table needs 0 <= n_table1 < 2^31 and the schedule (not EXACT mode)");
+  KGX_REQUIRE(!table2 || (reduce == KGX_SUM && !drop_key), KGX_ERR_UNSUPPORTED,
+              "kgx_spmm: two-table gathers are implemented for plain / weighted sums");
   KGX_REQUIRE(!items || (n_long_items >= 0 && n_long_items <= n_items), KGX_ERR_ARG,
               "kgx_spmm: n_long_items must lie in [0, n_items]");
   KGX_REQUIRE(reduce >= KGX_SUM && reduce <= KGX_STD, KGX_ERR_ARG, "kgx_spmm: unknown reduce %d", reduce);
@@ -911,9 +943,11 @@ extern "C" int kgx_spmm_ex(int reduce, int epilogue, const int32_t* rowptr, cons
   }
 
   // widest vector the shapes and pointers allow
+  a.n_t1 = table2 ? int32_t(n_table1) : INT32_MAX;
   auto ok = [&](int v) {
     const int b = 4 * v;
     return F % v == 0 && ld_table % v == 0 && ld_out % v == 0 && aligned(table, b) && aligned(out, b) &&
+           (!table2 || aligned(table2, b)) &&
            (epilogue != KGX_EPI_BIAS || aligned(bias, b)) &&
            (epilogue != KGX_EPI_GIN || (ld_x % v == 0 && aligned(xroot, b))) && aligned(partials, b);
   };
@@ -933,6 +967,10 @@ extern "C" int kgx_spmm_ex(int reduce, int epilogue, const int32_t* rowptr, cons
     s.G = G;
     s.lgG = lg;
     s.table = table + c0;
+    // table2 - n_t1 * ld_t (+ the slice's first column), as an address; tsrc adds row_off(c)
+    s.t2b = table2 ? reinterpret_cast<const float*>(reinterpret_cast<uintptr_t>(table2 + c0) -
+                                                    uintptr_t(n_table1) * uintptr_t(ld_table) * sizeof(float))
+                   : s.table;
     s.out = out + c0;
     s.bias = bias ? bias + c0 : nullptr;
     s.xroot = xroot ? xroot + c0 : nullptr;

@@ -83,9 +83,13 @@ struct FusedArgs {
   int32_t n_x1;
 };
 
-// Source row of column c: x[c] or x2[c - n_x1] (one 64-bit select per gathered row).
+// Source row of column c: x[c], or with TWO x2[c - n_x1] (one 64-bit select per
+// gathered row; a separate instantiation, so the one-table kernels keep their
+// register budget).
+template <bool TWO>
 __device__ __forceinline__ const float* gsrc(const FusedArgs& a, int32_t c) {
-  return (c >= a.n_x1 ? a.x2b : a.x) + row_off(c, a.ld_x);
+  if constexpr (TWO) return (c >= a.n_x1 ? a.x2b : a.x) + row_off(c, a.ld_x);
+  return a.x + row_off(c, a.ld_x);
 }
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops
@@ -147,8 +151,8 @@ struct Red {
   }
 };
 
-template <int RED, bool WEIGHTED>
-__global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
+template <int RED, bool WEIGHTED, bool TWO>
+__global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedArgs a) {  // TWO: hold 4 waves per SIMD
   using R = Red<RED>;
 #ifdef KGX_FUSED_U
   constexpr int U = KGX_FUSED_U;
@@ -244,7 +248,7 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
       if (u < pn)  // exec-masked: rows of degree < PF issue no redundant loads
-        vload<4>(pv[u], gsrc(a, c[u]) + f);
+        vload<4>(pv[u], gsrc<TWO>(a, c[u]) + f);
     }
   };
 
@@ -291,7 +295,7 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
 #endif
       float v[B][4];
 #pragma unroll
-      for (int u = 0; u < B; ++u) vload<4>(v[u], gsrc(a, c[u]) + f);
+      for (int u = 0; u < B; ++u) vload<4>(v[u], gsrc<TWO>(a, c[u]) + f);
 #pragma unroll
       for (int u = 0; u < B; ++u)
 #pragma unroll
@@ -330,7 +334,7 @@ __global__ __launch_bounds__(kThreads) void spmm_gemm_kernel(FusedArgs a) {
       // inf / NaN in this lane's values (their sum is then non-finite): move
       // them to the lo plane (split3_a_lo) -- a rare branch instead of two
       // selects per value on every row
-      if (!__builtin_isfinite(__fadd_rn(__fadd_rn(r[0], r[1]), __fadd_rn(r[2], r[3])))) {
+      if (!split_fast_ok(r[0], r[1], r[2], r[3])) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           short h, m_, l;
@@ -421,7 +425,7 @@ constexpr int kRPG = KGX_SHORT_RPG;        // rows per group per tile
 constexpr int kSPF = KGX_SHORT_PF;         // edges per row gathered up front (all rows together)
 constexpr int kShortRows = kGroups * kRPG;
 
-template <int RED, bool WEIGHTED>
+template <int RED, bool WEIGHTED, bool TWO>
 __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs a) {  // 4 waves per SIMD: two blocks per CU
   using R = Red<RED>;
   // split planes of the 64 aggregated rows; after the MFMAs the same bytes hold the f32 results
@@ -497,7 +501,7 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
       for (int r = 0; r < kRPG; ++r)
 #pragma unroll
         for (int u = 0; u < kSPF; ++u)
-          if (u < deg[r]) vload<4>(v[r][u], gsrc(a, c[r][u]) + f);
+          if (u < deg[r]) vload<4>(v[r][u], gsrc<TWO>(a, c[r][u]) + f);
 #pragma unroll
       for (int r = 0; r < kRPG; ++r)
 #pragma unroll
@@ -525,7 +529,7 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
           if constexpr (WEIGHTED) wt[u] = a.w[ee];
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) vload<4>(v[u], gsrc(a, c[u]) + f);
+        for (int u = 0; u < 2; ++u) vload<4>(v[u], gsrc<TWO>(a, c[u]) + f);
 #pragma unroll
         for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -558,7 +562,7 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
         pm[k] = m_;
         pl[k] = l;
       }
-      if (!__builtin_isfinite(__fadd_rn(__fadd_rn(v[0], v[1]), __fadd_rn(v[2], v[3])))) {
+      if (!split_fast_ok(v[0], v[1], v[2], v[3])) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           short h, m_, l;
@@ -656,7 +660,7 @@ constexpr int tiny_rows() { return kTinyGroups * (NG == 1 ? KGX_TINY_RPG1 : KGX_
 
 // NG: edges gathered per row (2 for the degree-2 head of the tail, 1 for the
 // degree <= 1 rest: the schedule is degree-descending, so each is a range).
-template <int RED, bool WEIGHTED, bool EXTRA, int NG>  // EXTRA: pre_gin or agg_out (loads / stores under a row mask)
+template <int RED, bool WEIGHTED, bool EXTRA, int NG, bool TWO>  // EXTRA: pre_gin or agg_out (loads / stores under a row mask)
 __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedArgs a) {
   using R = Red<RED>;
   constexpr int kTinyRPG = NG == 1 ? KGX_TINY_RPG1 : KGX_TINY_RPG;  // rows per group per tile
@@ -759,8 +763,8 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
   auto gather = [&](const Rec& r, f4 (&v)[kTinyRPG][NG]) {
 #pragma unroll
     for (int j = 0; j < kTinyRPG; ++j) {
-      v[j][0] = *reinterpret_cast<const f4*>(gsrc(a, r.p[j].z) + f);
-      if constexpr (NG == 2) v[j][1] = *reinterpret_cast<const f4*>(gsrc(a, r.p[j].w) + f);
+      v[j][0] = *reinterpret_cast<const f4*>(gsrc<TWO>(a, r.p[j].z) + f);
+      if constexpr (NG == 2) v[j][1] = *reinterpret_cast<const f4*>(gsrc<TWO>(a, r.p[j].w) + f);
     }
   };
   auto produce = [&](int64_t i, const auto& c, const f4 (&v)[kTinyRPG][NG]) {
@@ -798,7 +802,7 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
         pm[k] = m_;
         pl[k] = l;
       }
-      if (!__builtin_isfinite(__fadd_rn(__fadd_rn(o[0], o[1]), __fadd_rn(o[2], o[3])))) {
+      if (!split_fast_ok(o[0], o[1], o[2], o[3])) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           short h, m_, l;
@@ -905,7 +909,7 @@ __global__ __launch_bounds__(256) void spmm_gemm_fixup_kernel(FusedArgs a) {
   }
 }
 
-template <int RED, bool W>
+template <int RED, bool W, bool TWO = false>
 int launch(const FusedArgs& a, hipStream_t s) {
   const int64_t work = a.items ? a.n_long : a.n_rows;
   if (work > 0) {
@@ -917,7 +921,7 @@ int launch(const FusedArgs& a, hipStream_t s) {
         cus = 256;
     }
     int per_cu = 0;
-    auto k = spmm_gemm_kernel<RED, W>;
+    auto k = spmm_gemm_kernel<RED, W, TWO>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, 0) != hipSuccess || per_cu <= 0)
       per_cu = 2;
     const int64_t need = (work + kGroups - 1) / kGroups;
@@ -929,7 +933,7 @@ int launch(const FusedArgs& a, hipStream_t s) {
   }
   if (a.items && a.n_long < a.n_short_end) {
     int per_cu = 0;
-    auto k = spmm_gemm_short_kernel<RED, W>;
+    auto k = spmm_gemm_short_kernel<RED, W, TWO>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, 0) != hipSuccess || per_cu <= 0)
       per_cu = 2;
     static int cus2 = 0;
@@ -952,8 +956,8 @@ int launch(const FusedArgs& a, hipStream_t s) {
       b.tw = a.tw ? a.tw + (part ? a.n_tiny2 : 0) : nullptr;
       b.n_tiny = part ? a.n_tiny - a.n_tiny2 : a.n_tiny2;
       if (b.n_tiny <= 0) continue;
-      auto k = part ? (extra ? spmm_gemm_tiny_kernel<RED, W, true, 1> : spmm_gemm_tiny_kernel<RED, W, false, 1>)
-                    : (extra ? spmm_gemm_tiny_kernel<RED, W, true, 2> : spmm_gemm_tiny_kernel<RED, W, false, 2>);
+      auto k = part ? (extra ? spmm_gemm_tiny_kernel<RED, W, true, 1, TWO> : spmm_gemm_tiny_kernel<RED, W, false, 1, TWO>)
+                    : (extra ? spmm_gemm_tiny_kernel<RED, W, true, 2, TWO> : spmm_gemm_tiny_kernel<RED, W, false, 2, TWO>);
       const int rows = part ? tiny_rows<1>() : tiny_rows<2>();
       const int64_t need = (b.n_tiny + rows - 1) / rows;
       const int64_t cap = a.share_gpu ? int64_t(cu_count()) * 7 / 8 : int64_t(cu_count());
@@ -1020,6 +1024,8 @@ extern "C" int kgx_spmm_gemm_ex3(int reduce, const int32_t* rowptr, const int32_
   hipStream_t stream = as_stream(stream_);
   KGX_REQUIRE(!x2 || (n_x1 >= 0 && n_x1 < (int64_t(1) << 31) && reinterpret_cast<uintptr_t>(x2) % 16 == 0),
               KGX_ERR_ARG, "kgx_spmm_gemm: x2 must be 16-byte aligned and 0 <= n_x1 < 2^31");
+  KGX_REQUIRE(!x2 || (reduce == KGX_SUM && !(flags & KGX_FUSED_PRE_GIN)), KGX_ERR_UNSUPPORTED,
+              "kgx_spmm_gemm: two-table gathers are implemented for plain sums (the sharded GCN pass)");
   KGX_REQUIRE(!items || tiny_pack || n_short_end == n_items, KGX_ERR_ARG,
               "kgx_spmm_gemm: without tiny_pack, n_short_end must equal n_items");
   KGX_REQUIRE(!items || (n_long_items >= 0 && n_long_items <= n_short_end && n_short_end <= n_items), KGX_ERR_ARG,
@@ -1093,6 +1099,7 @@ extern "C" int kgx_spmm_gemm_ex3(int reduce, const int32_t* rowptr, const int32_
   a.debug = 0;
 #endif
   const bool wt = w != nullptr;
+  if (x2) return wt ? launch<KGX_SUM, true, true>(a, stream) : launch<KGX_SUM, false, true>(a, stream);
   switch (reduce) {
     case KGX_SUM: return wt ? launch<KGX_SUM, true>(a, stream) : launch<KGX_SUM, false>(a, stream);
     case KGX_MEAN: return wt ? launch<KGX_MEAN, true>(a, stream) : launch<KGX_MEAN, false>(a, stream);

@@ -80,18 +80,28 @@ class KgxBackend:
     def supports_fused(self, f_in: int, f_out: int) -> bool:
         return kops.fused_transform_supported(f_in, f_out)
 
-    def aggregate_transform(self, g, x, W, bias=None, out=None):
-        """GCN sum with the edge weights, then @ W (+ bias); out += ... if given."""
-        return kops.aggregate_transform(g, x, W, "sum", weighted=True, bias=bias, out=out)
+    def aggregate_transform(self, g, x, W, bias=None, out=None, x2=None, accumulate=True):
+        """GCN sum with the edge weights, then @ W (+ bias); out += ... if given
+        (accumulate=False: g's scheduled rows of out overwritten).  x2: second
+        table for sources >= x.shape[0] (two-table gathers)."""
+        return kops.aggregate_transform(g, x, W, "sum", weighted=True, bias=bias, out=out, x2=x2,
+                                        accumulate=accumulate)
+
+    def restrict_rows(self, g, row_mask):
+        return G.restrict_rows(g, row_mask)
 
     def aggregate(self, g, table, reduce="sum", weighted=False, epilogue=nat.EPI_NONE, bias=None, xroot=None,
                   gin_scale=1.0, exact=False):
         return kops.aggregate(g, table, reduce, weighted=weighted, epilogue=epilogue, bias=bias, xroot=xroot,
                               gin_scale=gin_scale, exact=exact)
 
-    def aggregate_accumulate(self, g, table, out, weighted=False):
-        """out += the (weighted) row sums of table over g, in place (KGX_EPI_ACCUM)."""
-        return kops.aggregate_accumulate(g, table, out, weighted=weighted)
+    def aggregate_accumulate(self, g, table, out, weighted=False, epilogue=nat.EPI_ACCUM, bias=None, xroot=None,
+                             gin_scale=1.0, table2=None):
+        """out += the (weighted) row sums of table over g, in place (KGX_EPI_ACCUM);
+        another epilogue overwrites g's scheduled rows; table2: second table for
+        sources >= table.shape[0]."""
+        return kops.aggregate_accumulate(g, table, out, weighted=weighted, epilogue=epilogue, bias=bias,
+                                         xroot=xroot, gin_scale=gin_scale, table2=table2)
 
 
 class TorchComm:
@@ -119,6 +129,15 @@ class TorchComm:
     def broadcast(self, t, src: int = 0) -> None:
         dist.broadcast(t, src=src, group=self.group)
 
+    def all_gather(self, out, inp) -> None:
+        """out = [rank 0's inp | rank 1's inp | ...] (equal sizes)."""
+        dist.all_gather_into_tensor(out, inp, group=self.group)
+
+    def all_gather_start(self, out, inp):
+        """all_gather behind the CURRENT stream's work; the handle's wait()
+        orders the then-current stream after it (as all_to_all_start)."""
+        return dist.all_gather_into_tensor(out, inp, group=self.group, async_op=True)
+
 
 class HostStagedComm(TorchComm):
     """Exchange staged through host memory over a gloo group: for rehearsing the
@@ -138,6 +157,16 @@ class HostStagedComm(TorchComm):
         h = t.detach().cpu()
         dist.broadcast(h, src=src, group=self.group)
         t.copy_(h)
+
+    def all_gather(self, out, inp) -> None:
+        h = inp.detach().cpu()
+        parts = [torch.empty_like(h) for _ in range(dist.get_world_size(self.group))]
+        dist.all_gather(parts, h, group=self.group)
+        out.copy_(torch.cat(parts))
+
+    def all_gather_start(self, out, inp):
+        self.all_gather(out, inp)
+        return None
 
 
 def _inference_only(layer: Layer, weights) -> None:
@@ -195,6 +224,12 @@ class HaloChunk:
     # a push-pull chunk: its exchange steps (pulled rows, then partials), each
     # landing in its own contiguous slice of [lo, hi)
     steps: list | None = None
+    # "a2a": all-to-all-v of send rows; "allgather": every rank contributes its
+    # local rows [src_lo, src_hi), padded to `pad` rows, and receives all ranks'
+    kind: str = "a2a"
+    src_lo: int = 0
+    src_hi: int = 0
+    pad: int = 0
 
 
 @dataclass
@@ -205,6 +240,11 @@ class PushPullPlan:
     n_rows: int  # halo rows received per layer
     n_pull: int  # of which source rows
     n_push: int  # of which partial sums pushed by the owners
+    recv_graph: object = None  # receiver CSR over all halo rows (sources = halo buffer rows)
+    step_parts: list | None = None  # receiver CSR per exchange step, in issue order (accumulate-only)
+    weighted: bool = True  # receiver edges carry the GCN norms (else weight 1, plain partial sums)
+    kind: str = "halo"  # "halo" (push-pull all-to-all) or "allgather" (every rank's rows, chunked)
+    merged: tuple | None = None  # (own pass, first-step pass, steps accumulated after): ShardedGraph.merged_passes
 
 
 class _Works:
@@ -280,8 +320,9 @@ class ShardedGraph:
     _pp: PushPullPlan | None = None  # the push-pull plan last used
     _pp_by_k: dict | None = None
     chunks_fixed: bool = False  # K given (halo_chunks= or KGX_HALO_CHUNKS): no tuning
-    halo_k: int | None = None  # push-pull chunk count chosen by tune_halo_chunks
-    tuning: dict | None = None  # K -> slowest rank's forward seconds
+    halo_k: int | None = None  # exchange chunk count chosen by tune_exchange (or fixed)
+    tuning: dict | None = None  # K (or "exchange:K") -> slowest rank's forward seconds
+    exchange: str | None = None  # "halo" / "allgather"; None: not chosen yet (push-pull halo until tuned)
 
     @property
     def lo(self) -> int:
@@ -374,6 +415,13 @@ class ShardedGraph:
         return torch.empty((self.n_local + self.n_halo, features), dtype=torch.float32, device=like.device)
 
     def _pack(self, x_local: torch.Tensor, c: HaloChunk) -> torch.Tensor:
+        if c.kind == "allgather":  # a contiguous slice of the layer input; padded only when short
+            rows = x_local[c.src_lo: c.src_hi]
+            if rows.shape[0] == c.pad:
+                return rows
+            buf = x_local.new_zeros((c.pad, x_local.shape[1]))
+            buf[: rows.shape[0]] = rows
+            return buf
         if c.send_graph is not None:
             return self.backend.aggregate(c.send_graph, x_local, "sum", weighted=True)
         if c.send_rows.numel():
@@ -410,8 +458,8 @@ class ShardedGraph:
             raise ValueError("push_pull_plan(weighted=True): the shard graph has no edge weights")
         if self._pp_by_k is None:
             self._pp_by_k = {}
-        if (K, weighted) in self._pp_by_k:
-            self._pp = self._pp_by_k[(K, weighted)]
+        if ("halo", K, weighted) in self._pp_by_k:
+            self._pp = self._pp_by_k[("halo", K, weighted)]
             return self._pp
         g, comm, world, lo, n_local = self.graph, self.comm, self.world, self.lo, self.n_local
         dev = g.col.device
@@ -521,33 +569,107 @@ class ShardedGraph:
         rcol = torch.cat([pull_pos[pidx], push_pos])
         rrow = torch.cat([hd[via_pull], push_keys % stride])
         rw = torch.cat([hw[via_pull], torch.ones(push_keys.numel(), dtype=torch.float32, device=dev)])
-        parts = []
+        parts, step_parts, rg = [], [], None
         if off:
             rg = self.backend.build_graph(rcol.to(torch.int32), rrow.to(torch.int32), off, n_local, 128)
             rg.w = rw[rg.eid.long()].contiguous()
             # a leading empty range makes every chunk part accumulate-only
             parts = list(self.backend.split_by_source(rg, [0, 0] + [c.hi for c in chunks])[1:])
-        self._pp = PushPullPlan(chunks=chunks, parts=parts, n_rows=off, n_pull=rp[-1], n_push=ru[-1])
-        self._pp_by_k[(K, weighted)] = self._pp
+            step_parts = list(self.backend.split_by_source(rg, [0, 0] + [st.hi for c in chunks for st in c.steps])[1:])
+        self._pp = PushPullPlan(chunks=chunks, parts=parts, n_rows=off, n_pull=rp[-1], n_push=ru[-1], recv_graph=rg,
+                                step_parts=step_parts, weighted=weighted)
+        self._pp_by_k[("halo", K, weighted)] = self._pp
         return self._pp
 
-    def tune_halo_chunks(self, run, candidates=(1, 2, 4, 8)) -> int:
-        """Choose the push-pull chunk count K by timing one forward per
-        candidate (`run(K)`; plans are built before their timed call).  The
-        best K depends on the all-to-all rate of the machine (K = 1
-        has the least device work, more chunks hide more of a slow exchange),
-        so it is measured, like a library autotuner, not assumed.  Collective:
-        every rank times the same candidates and the slowest rank's time counts."""
+    def allgather_plan(self, n_chunks: int = 1, weighted: bool | None = None) -> PushPullPlan:
+        """Exchange plan that moves EVERY rank's rows: K all-gathers (RCCL over
+        xGMI), chunk k = rows [k cs, (k+1) cs) of every rank (cs = ceil(max
+        rank rows / K)), landing chunk-major in a [K * world * cs] table.  No
+        request lists, no packing kernel (each step sends a contiguous slice of
+        the layer input), no partial sums: worth it when the graph's remote
+        sources cover most of the other ranks' rows anyway -- SURVEY.md §8(e)
+        proposes it for C5, whose X is 0.98 GB.  The receiver CSR maps each
+        remote edge to its source's table row."""
+        K = max(1, int(n_chunks))
+        if weighted is None:
+            weighted = self.graph.w is not None
+        key = ("allgather", K, weighted)
+        if self._pp_by_k is None:
+            self._pp_by_k = {}
+        if key in self._pp_by_k:
+            self._pp = self._pp_by_k[key]
+            return self._pp
+        g, world, n_local = self.graph, self.world, self.n_local
+        dev = g.col.device
+        sizes = [b - a for a, b in zip(self.bounds, self.bounds[1:])]
+        cs = max(1, -(-max(sizes) // K))
+        span = world * cs
+        rows = torch.repeat_interleave(torch.arange(g.n_dst, device=dev), g.deg.long(), output_size=g.kept)
+        col = g.col.long()
+        remote = col >= n_local
+        gid = self.halo_ids.long()[col[remote] - n_local]
+        bt = torch.tensor(self.bounds[1:-1], dtype=torch.long, device=dev)
+        owner = torch.bucketize(gid, bt, right=True)
+        i = gid - torch.tensor(self.bounds[:-1], dtype=torch.long, device=dev)[owner]
+        k = i // cs
+        pos = k * span + owner * cs + (i - k * cs)
+        n_rows = K * span
+        none_i32 = torch.empty(0, dtype=torch.int32, device=dev)
+        chunks = []
+        for kk in range(K):
+            a, b = min(kk * cs, n_local), min((kk + 1) * cs, n_local)
+            st = HaloChunk(lo=kk * span, hi=(kk + 1) * span, recv_splits=[], send_splits=[], send_rows=none_i32,
+                           kind="allgather", src_lo=a, src_hi=b, pad=cs)
+            chunks.append(HaloChunk(lo=st.lo, hi=st.hi, recv_splits=[], send_splits=[], send_rows=none_i32,
+                                    steps=[st], kind="allgather"))
+        parts, rg = [], None
+        if int(remote.sum()):
+            rg = self.backend.build_graph(pos.to(torch.int32), rows[remote].to(torch.int32), n_rows, n_local, 128)
+            wr = g.w[remote] if weighted else torch.ones(int(remote.sum()), dtype=torch.float32, device=dev)
+            rg.w = wr[rg.eid.long()].contiguous()
+            parts = list(self.backend.split_by_source(rg, [0, 0] + [c.hi for c in chunks])[1:])
+        self._pp = PushPullPlan(chunks=chunks, parts=parts, n_rows=n_rows, n_pull=n_rows - K * cs, n_push=0,
+                                recv_graph=rg, step_parts=list(parts), weighted=weighted, kind="allgather")
+        self._pp_by_k[key] = self._pp
+        return self._pp
+
+    def exchange_plan(self, n_chunks: int | None = None, weighted: bool | None = None) -> PushPullPlan:
+        """The plan of the chosen exchange ("halo": push-pull all-to-all; "allgather")."""
+        if self.exchange == "allgather":
+            return self.allgather_plan(n_chunks or self.halo_k or 1, weighted)
+        return self.push_pull_plan(n_chunks, weighted)
+
+    def exchange_candidates(self, feature_bytes: int, halo_ks=(1, 2, 4, 8), gather_ks=(1, 2, 4)) -> list:
+        """(kind, K) pairs worth timing: the push-pull halo at each K, and the
+        all-gather when its table is at most 4x the pull-only halo's bytes
+        (weak-scaled shards, whose halo is a small part of the global graph,
+        skip it without a run)."""
+        fixed = os.environ.get("KGX_EXCHANGE")
+        cands = [("halo", k) for k in halo_ks]
+        gather_rows = self.n_global
+        if fixed == "allgather" or (fixed is None and gather_rows <= 4 * max(self.n_halo, 1)):
+            cands += [("allgather", k) for k in gather_ks]
+        if fixed == "allgather":
+            cands = [c for c in cands if c[0] == "allgather"]
+        return cands
+
+    def tune_exchange(self, run, candidates) -> tuple:
+        """Choose (exchange, K) by timing one forward per candidate (`run(kind,
+        K)`; the plan is built before its timed call), best of two; every rank
+        times the same candidates and the slowest rank's time counts (one
+        all-to-all of the times).  Like a library autotuner: the best choice
+        depends on the links' rate, which only the machine knows."""
         dev = self.graph.col.device
         times = []
-        for K in candidates:
-            self.push_pull_plan(K)
+        for kind, K in candidates:
+            self.exchange, self.halo_k = kind, K
+            self.exchange_plan(K)
             best = float("inf")
-            for _ in range(2):  # best of two: the first also warms the plan's launches
+            for _ in range(2):
                 if dev.type == "cuda":
                     torch.cuda.synchronize(dev)
                 t0 = time.perf_counter()
-                run(K)
+                run(kind, K)
                 if dev.type == "cuda":
                     torch.cuda.synchronize(dev)
                 best = min(best, time.perf_counter() - t0)
@@ -556,10 +678,54 @@ class ShardedGraph:
         every = torch.empty(self.world * t.numel(), dtype=torch.float64, device=dev)
         self.comm.all_to_all_single(every, t.repeat(self.world).contiguous())
         worst = every.view(self.world, -1).max(0).values.cpu()
-        self.halo_k = int(candidates[int(torch.argmin(worst))])
-        self.tuning = {int(k): float(v) for k, v in zip(candidates, worst)}
-        self.push_pull_plan(self.halo_k)
-        return self.halo_k
+        i = int(torch.argmin(worst))
+        self.exchange, self.halo_k = candidates[i]
+        self.tuning = {f"{kind}:{K}": float(v) for (kind, K), v in zip(candidates, worst)}
+        self.exchange_plan(self.halo_k)
+        return candidates[i]
+
+    def merged_passes(self, pp: PushPullPlan):
+        """(g_a, g_b, later): the default path's passes with the first exchange
+        step folded into the rows it touches (cached on the plan).
+
+        H = the local rows with an edge in the first step (chunk 0's pulled
+        rows).  g_a: the own-source CSR restricted to the rows NOT in H -- it
+        writes them, and runs while the exchange is in flight.  g_b: for the
+        rows in H, their own-source edges followed by their first-step edges
+        (sources >= n_local index the halo buffer), written once by ONE
+        two-table pass (kgx_spmm_gemm_ex3), instead of an own pass that writes
+        them and a halo pass that reads and rewrites them.  later: [(step, CSR)]
+        for the remaining exchange steps (the pushed partials, later chunks),
+        accumulate-only over the rows each touches.  Each row's sum is own
+        edges, then first-step edges, then later steps: a re-association of
+        the one-pass order, tolerance-equal like the rest of this path."""
+        if pp.merged is not None:
+            return pp.merged
+        g_own, _ = self.own_halo_parts()
+        n_local = self.n_local
+        dev = g_own.col.device
+        steps = [st for c in pp.chunks for st in c.steps]
+        first = pp.step_parts[0] if pp.step_parts else None
+        if first is None or first.kept == 0:
+            pp.merged = (g_own, None, [(i, g) for i, g in enumerate(pp.step_parts or []) if g.kept])
+            return pp.merged
+        lo0 = steps[0].lo
+        in_h = first.deg > 0
+        ar = torch.arange(n_local, device=dev)
+        r_own = torch.repeat_interleave(ar, g_own.deg.long(), output_size=g_own.kept)
+        keep = in_h[r_own]
+        r_first = torch.repeat_interleave(ar, first.deg.long(), output_size=first.kept)
+        rows = torch.cat([r_own[keep], r_first])
+        cols = torch.cat([g_own.col[keep].long(), first.col.long() + (n_local + lo0)])
+        # own edges first, then the step's: the stable CSR keeps that order inside every row
+        g_b = self.backend.build_graph(cols.to(torch.int32), rows.to(torch.int32), n_local + pp.n_rows, n_local, 128)
+        if pp.weighted:
+            g_b.w = torch.cat([g_own.w[keep], first.w])[g_b.eid.long()].contiguous()
+        g_b = self.backend.restrict_rows(g_b, in_h)
+        g_a = self.backend.restrict_rows(g_own, ~in_h)
+        later = [(i, g) for i, g in enumerate(pp.step_parts[1:], start=1) if g.kept]
+        pp.merged = (g_a, g_b, later)
+        return pp.merged
 
     def halo_exchange(self, table: torch.Tensor) -> None:
         """table[n_local:] <- rows other ranks own (one all-to-all-v over RCCL
@@ -605,7 +771,14 @@ class ShardedGraph:
                 handles = []
                 for st in c.steps or [c]:
                     send = self._pack(x_local, st)
-                    if start is None:
+                    if st.kind == "allgather":
+                        gstart = getattr(self.comm, "all_gather_start", None) if start is not None else None
+                        if gstart is None:
+                            self.comm.all_gather(halo[st.lo: st.hi], send)
+                            handles.append(None)
+                        else:
+                            handles.append(gstart(halo[st.lo: st.hi], send))
+                    elif start is None:
                         self.comm.all_to_all_single(halo[st.lo: st.hi], send, st.recv_splits, st.send_splits)
                     else:
                         handles.append(start(halo[st.lo: st.hi], send, st.recv_splits, st.send_splits))
@@ -644,9 +817,18 @@ class ShardedGraph:
             raise ValueError("propagate_overlapped: weights / bias go with a plain sum (the GCN layer)")
         x_local = x_local.contiguous()
         g_own, _ = self.own_halo_parts()
-        pp = self.push_pull_plan(weighted=weighted)
+        pp = self.exchange_plan(weighted=weighted)
         halo = self.halo_buffer(x_local.shape[1], x_local, pp.n_rows)
         fold_gin = gin_scale is not None and reduce == "sum"
+        epi = nat.EPI_GIN if fold_gin else (nat.EPI_BIAS if bias is not None else nat.EPI_NONE)
+        if use_merged_halo() or pp.kind == "allgather":
+            out = self._propagate_merged(x_local, pp, halo, weighted, epi, bias, fold_gin, gin_scale)
+            if reduce == "mean":  # aggregators.py:56-85: sum / max(count, 1e-8), count in fp32
+                count = torch.clamp(self.graph.deg[: self.n_local].to(torch.float32), min=1e-8)
+                out = out / count.unsqueeze(1)
+                if gin_scale is not None:
+                    out = torch.tensor(float(gin_scale), dtype=torch.float32, device=out.device) * x_local + out
+            return out
         with torch.no_grad():
             works = self.start_halo_exchange(x_local, halo, pp.chunks)
             epi = nat.EPI_GIN if fold_gin else (nat.EPI_BIAS if bias is not None else nat.EPI_NONE)
@@ -665,6 +847,43 @@ class ShardedGraph:
                 out = out / count.unsqueeze(1)
                 if gin_scale is not None:
                     out = torch.tensor(float(gin_scale), dtype=torch.float32, device=out.device) * x_local + out
+        return out
+
+    def _propagate_merged(self, x_local, pp, halo, weighted, epi, bias, fold_gin, gin_scale):
+        """propagate_overlapped's passes with the first exchange step merged into
+        its rows (merged_passes): the rows without first-step edges (own
+        sources, epilogue applied) while the exchange is in flight; the rows
+        with them in ONE two-table pass (own then first-step edges, epilogue
+        applied) once chunk 0's pulled rows have landed; then out += the later
+        steps' row sums as each lands."""
+        g_a, g_b, later = self.merged_passes(pp)
+        steps = [st for c in pp.chunks for st in c.steps]
+        kw = dict(weighted=weighted, bias=bias, xroot=x_local if fold_gin else None,
+                  gin_scale=float(gin_scale) if fold_gin else 1.0)
+        with torch.no_grad():
+            works = self.start_halo_exchange(x_local, halo, pp.chunks)
+            handles = []
+            for w, c in zip(works, pp.chunks):
+                handles.extend(w.handles if w is not None else [None] * len(c.steps))
+            waited = set()
+
+            def wait_step(i):
+                for j in range(i + 1):
+                    if j not in waited:
+                        waited.add(j)
+                        if handles[j] is not None:
+                            handles[j].wait()
+
+            with kops.sharing_gpu():
+                out = self.backend.aggregate(g_a, x_local, "sum", epilogue=epi, **kw)
+            if g_b is not None:
+                wait_step(0)
+                self.backend.aggregate_accumulate(g_b, x_local, out, epilogue=epi, table2=halo, **kw)
+            for i, g in later:
+                wait_step(i)
+                st = steps[i]
+                self.backend.aggregate_accumulate(g, halo[st.lo: st.hi], out, weighted=weighted)
+            wait_step(len(steps) - 1)
         return out
 
     def propagate(self, x_local: torch.Tensor, reduce: str = "sum", **kw) -> torch.Tensor:
@@ -728,8 +947,10 @@ class ShardedGCNConv(Layer):
                                     bias=self.bias if use_b else None, exact=sg.exact)
 
     def tune(self, x_local: torch.Tensor) -> int | None:
-        """Time the push-pull chunk counts once (ShardedGraph.tune_halo_chunks);
-        a no-op when K is fixed, on one rank, or off the default path."""
+        """Time the exchanges once (ShardedGraph.tune_exchange: the push-pull
+        halo at K = 1 / 2 / 4 / 8 chunks, and the all-gather where its table is
+        not far larger); a no-op when K is fixed, on one rank, or off the
+        default path."""
         sg = self.sg
         if not self.built:
             self._build_device = x_local.device
@@ -739,7 +960,9 @@ class ShardedGCNConv(Layer):
                 or not sg.backend.supports_fused(x_local.shape[1], self.output_dim)):
             return sg.halo_k
         with torch.no_grad():
-            return sg.tune_halo_chunks(lambda K: self._forward_overlapped(x_local, self.bias if use_b else None, K))
+            sg.tune_exchange(lambda kind, K: self._forward_overlapped(x_local, self.bias if use_b else None, K),
+                             sg.exchange_candidates(4 * x_local.shape[1]))
+        return sg.halo_k
 
     def _forward_overlapped(self, x_local: torch.Tensor, bias, n_chunks: int | None = None) -> torch.Tensor:
         """Aggregate-then-transform with the halo exchange pipelined in chunks:
@@ -755,13 +978,16 @@ class ShardedGCNConv(Layer):
         sg = self.sg
         g_own, g_chunks = sg.own_halo_parts()
         chunks, n_rows = sg.chunks, sg.n_halo
+        pp = None
         if use_push_pull():
             if n_chunks is None and sg.halo_k is None and not sg.chunks_fixed and sg.world > 1:
-                self.tune(x_local)  # first call: measure K = 1 / 2 / 4 / 8 once
-            pp = sg.push_pull_plan(n_chunks)
+                self.tune(x_local)  # first call: time the exchanges (and K) once
+            pp = sg.exchange_plan(n_chunks)
             chunks, g_chunks, n_rows = pp.chunks, pp.parts, pp.n_rows
         x_local = x_local.contiguous()
         halo = sg.halo_buffer(x_local.shape[1], x_local, n_rows)
+        if pp is not None and (use_merged_halo() or pp.kind == "allgather"):
+            return self._forward_merged(x_local, bias, pp, halo)
         with torch.no_grad():
             works = sg.start_halo_exchange(x_local, halo, chunks)
             with kops.sharing_gpu():  # the exchange's RCCL kernels run beside this pass
@@ -779,6 +1005,53 @@ class ShardedGCNConv(Layer):
                 with kops.sharing_gpu() if k < last else contextlib.nullcontext():
                     sg.backend.aggregate_transform(g, halo[c.lo: c.hi], self.kernel, out=out)
         return out
+
+
+    def _forward_merged(self, x_local: torch.Tensor, bias, pp: PushPullPlan, halo: torch.Tensor) -> torch.Tensor:
+        """The default path with the first exchange step merged into its rows
+        (ShardedGraph.merged_passes): side stream as _forward_overlapped; main
+        stream: out[rows not in H] = bias + (A_own X) W while the exchange is in
+        flight; once chunk 0's pulled rows have landed, out[H] = bias + (A_own X
+        + A_0 halo_0) W in one two-table pass; then out += (A_s halo_s) W per
+        later step (pushed partials, later chunks) as each lands."""
+        sg = self.sg
+        g_a, g_b, later = sg.merged_passes(pp)
+        steps = [st for c in pp.chunks for st in c.steps]
+        with torch.no_grad():
+            works = sg.start_halo_exchange(x_local, halo, pp.chunks)
+            handles = []
+            for w, c in zip(works, pp.chunks):
+                handles.extend(w.handles if w is not None else [None] * len(c.steps))
+            waited = set()
+
+            def wait_step(i):
+                for j in range(i + 1):  # steps land in issue order on the comm stream
+                    if j not in waited:
+                        waited.add(j)
+                        if handles[j] is not None:
+                            handles[j].wait()
+
+            with kops.sharing_gpu():  # the exchange's packing and RCCL kernels run beside this pass
+                out = sg.backend.aggregate_transform(g_a, x_local, self.kernel, bias=bias)
+            if g_b is not None:
+                wait_step(0)
+                with kops.sharing_gpu() if later else contextlib.nullcontext():
+                    sg.backend.aggregate_transform(g_b, x_local, self.kernel, bias=bias, out=out, x2=halo,
+                                                   accumulate=False)
+            for n, (i, g) in enumerate(later):
+                wait_step(i)
+                st = steps[i]
+                with kops.sharing_gpu() if n + 1 < len(later) else contextlib.nullcontext():
+                    sg.backend.aggregate_transform(g, halo[st.lo: st.hi], self.kernel, out=out)
+            # every step, used or not: also orders the side stream's reads of x_local
+            wait_step(len(steps) - 1)
+        return out
+
+
+def use_merged_halo() -> bool:
+    """The default GCN path merges the first halo step into its rows' pass
+    (KGX_HALO_MERGED=0: the round-2 own pass + accumulating chunk passes)."""
+    return os.environ.get("KGX_HALO_MERGED", "1") not in ("0", "", "false", "False")
 
 
 class _ShardedWrap(Layer):
@@ -802,6 +1075,23 @@ class _ShardedWrap(Layer):
                 self.sg.comm.broadcast(p.data, src=0)
         self.built = True
 
+    def _pipelined(self) -> bool:
+        """Whether the forward takes the pipelined (exchange-overlapped) sum / mean path."""
+        return False
+
+    def _maybe_tune(self, x_local: torch.Tensor) -> None:
+        """First forward on the pipelined path: time the exchanges (the push-pull
+        halo at K = 1 / 2 / 4, the all-gather where its table is not far
+        larger) with this layer's own forward and keep the fastest
+        (ShardedGraph.tune_exchange); K fixed (halo_chunks= / KGX_HALO_CHUNKS),
+        one rank or EXACT mode: no tuning."""
+        sg = self.sg
+        if sg.halo_k is not None or sg.chunks_fixed or sg.world < 2 or sg.exact or not self._pipelined():
+            return
+        with torch.no_grad():
+            sg.tune_exchange(lambda kind, K: self._forward_impl(x_local, None),
+                             sg.exchange_candidates(4 * x_local.shape[1], halo_ks=(1, 2, 4)))
+
 
 class ShardedGINConv(_ShardedWrap):
     """GINConv over a ShardedGraph: h_i = MLP((1+eps) x_i + AGG_j x_j)
@@ -815,13 +1105,20 @@ class ShardedGINConv(_ShardedWrap):
 
         super().__init__(GINConv(output_dim, exact=sg.exact, **gin_kwargs), sg)
 
+    def _pipelined(self) -> bool:
+        return not self.sg.exact and self.conv.aggregator in ("sum", "mean")
+
     def forward(self, x_local: torch.Tensor, training=None) -> torch.Tensor:
         self._ensure_built(x_local)
         _inference_only(self, self.conv.weights)
+        self._maybe_tune(x_local.contiguous())
+        return self._forward_impl(x_local, training)
+
+    def _forward_impl(self, x_local: torch.Tensor, training=None) -> torch.Tensor:
         sg, conv = self.sg, self.conv
         x_local = x_local.contiguous()
         with torch.no_grad():
-            if not sg.exact and conv.aggregator in ("sum", "mean"):  # halo pipelined under the own-source pass
+            if self._pipelined():  # halo pipelined under the own-source pass
                 h = sg.propagate_overlapped(x_local, conv.aggregator, gin_scale=float(conv._scale()))
             else:
                 h = sg.propagate(x_local, conv.aggregator, epilogue=nat.EPI_GIN, xroot=x_local,
@@ -840,15 +1137,22 @@ class ShardedSAGEConv(_ShardedWrap):
 
         super().__init__(SAGEConv(output_dim, exact=sg.exact, **sage_kwargs), sg)
 
+    def _pipelined(self) -> bool:
+        return not self.sg.exact and self.conv.actual_aggregator in ("sum", "mean")
+
     def forward(self, x_local: torch.Tensor, training=None) -> torch.Tensor:
         self._ensure_built(x_local)
         _inference_only(self, self.conv.weights)
+        self._maybe_tune(x_local.contiguous())
+        return self._forward_impl(x_local, training)
+
+    def _forward_impl(self, x_local: torch.Tensor, training=None) -> torch.Tensor:
         sg, conv = self.sg, self.conv
         x_local = x_local.contiguous()
         with torch.no_grad():
             if conv.actual_aggregator == "pooling":
                 aggr = sg.propagate(conv.pool_mlp(x_local).contiguous(), "max")
-            elif not sg.exact and conv.actual_aggregator in ("sum", "mean"):
+            elif self._pipelined():
                 aggr = sg.propagate_overlapped(x_local, conv.actual_aggregator)
             else:
                 aggr = sg.propagate(x_local, conv.actual_aggregator)

@@ -293,6 +293,25 @@ def split_by_part(g: CSRGraph, part_of: torch.Tensor, sources: list, accumulate_
     return parts
 
 
+def restrict_rows(g: CSRGraph, row_mask: torch.Tensor) -> CSRGraph:
+    """A view of g whose schedule covers only the rows with row_mask[row] set
+    (zero-degree ones included): a launch over it writes exactly those rows and
+    leaves every other output row untouched.  CSR arrays are shared; the item
+    and split lists are filtered in order (the schedule stays degree-descending,
+    so the short-row suffix is recomputed and the tiny-row records rebuilt)."""
+    from dataclasses import replace
+
+    if g.n_items == 0:
+        return replace(g, extras={})
+    keep = row_mask[g.items[:, 0].long()]
+    items = g.items[keep].contiguous()
+    split = g.split[row_mask[g.split[:, 0].long()]].contiguous() if g.n_split else g.split
+    sub = replace(g, items=items, split=split, n_items=int(items.shape[0]), n_split=int(split.shape[0]) if g.n_split
+                  else 0, extras={"restricted_of": g})
+    sub.n_long = short_suffix_start(items)
+    return sub
+
+
 # ---------------------------------------------------------------------------
 # cache keyed on the caller's edge_index tensor (kept alive by the entry)
 # ---------------------------------------------------------------------------

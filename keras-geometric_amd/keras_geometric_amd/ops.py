@@ -94,10 +94,21 @@ def spmm_acc_(
     w: Optional[torch.Tensor],
     n_slots: int,
     n_long: int = -1,
+    epilogue: int = 4,
+    bias: Optional[torch.Tensor] = None,
+    xroot: Optional[torch.Tensor] = None,
+    gin_scale: float = 1.0,
+    table2: Optional[torch.Tensor] = None,
 ) -> None:
-    """out[i] += SUM_{e in row i} table[idx[e]] (* w[e]) in place (KGX_EPI_ACCUM)."""
-    table, w = _f32c(table), _f32c(w)
-    dev = nat.require_device(out, table, rowptr, rows, idx, w, items, split)
+    """out[i] += SUM_{e in row i} table[idx[e]] (* w[e]) in place (KGX_EPI_ACCUM,
+    the default epilogue); any other epilogue overwrites the scheduled rows of
+    out (and leaves the rest untouched).  table2: sources >= table.shape[0]
+    are rows of table2 (kgx_spmm_ex2)."""
+    table, w, bias, xroot, table2 = _f32c(table), _f32c(w), _f32c(bias), _f32c(xroot), _f32c(table2)
+    dev = nat.require_device(out, table, rowptr, rows, idx, w, items, split, bias, xroot, table2)
+    if table2 is not None and (table2.dim() != 2 or table2.shape[1] != table.shape[1]
+                               or (table2.shape[0] and table2.stride(0) != table.stride(0))):
+        raise ValueError("spmm_acc_: table2 must have table's row width and leading dimension")
     n_dst = rowptr.numel() - 1
     F = table.shape[1]
     if out.dtype != torch.float32 or out.shape != (n_dst, F) or out.stride(1) != 1:
@@ -111,33 +122,42 @@ def spmm_acc_(
         partials = torch.empty((n_slots, F), dtype=torch.float32, device=dev)
     n_long = n_items if n_long < 0 or n_long > n_items else n_long
     nat.check(
-        nat.lib().kgx_spmm_ex(
-            nat.SUM, nat.EPI_ACCUM, nat.ptr(rowptr), nat.ptr(rows), n_dst,
+        nat.lib().kgx_spmm_ex2(
+            nat.SUM, int(epilogue), nat.ptr(rowptr), nat.ptr(rows), n_dst,
             nat.ptr(items), n_items, n_long, nat.ptr(split), n_split,
-            nat.ptr(idx), nat.ptr(w), nat.ptr(table), table.stride(0), F,
-            nat.ptr(out), out.stride(0), None, None, 0, 1.0, None, 0.0, 0, nat.ptr(partials), nat.stream(dev),
+            nat.ptr(idx), nat.ptr(w), nat.ptr(table), table.stride(0), nat.ptr(table2),
+            table.shape[0] if table2 is not None else 0, F,
+            nat.ptr(out), out.stride(0), nat.ptr(bias), nat.ptr(xroot), xroot.stride(0) if xroot is not None else 0,
+            float(gin_scale), None, 0.0, 0, nat.ptr(partials), nat.stream(dev),
         ),
         "kgx_spmm",
     )
 
 
 @spmm_acc_.register_fake
-def _spmm_acc_fake(out, table, rowptr, rows, items, split, idx, w, n_slots, n_long=-1):
+def _spmm_acc_fake(out, table, rowptr, rows, items, split, idx, w, n_slots, n_long=-1, epilogue=4, bias=None,
+                   xroot=None, gin_scale=1.0, table2=None):
     return None
 
 
-def aggregate_accumulate(g: CSRGraph, table: torch.Tensor, out: torch.Tensor, *, weighted: bool = False) -> torch.Tensor:
+def aggregate_accumulate(g: CSRGraph, table: torch.Tensor, out: torch.Tensor, *, weighted: bool = False,
+                         epilogue: int = nat.EPI_ACCUM, bias: torch.Tensor | None = None,
+                         xroot: torch.Tensor | None = None, gin_scale: float = 1.0,
+                         table2: torch.Tensor | None = None) -> torch.Tensor:
     """out += (weighted) row sums of table rows over g, in place; forward only.
     Meant for accumulate-only graphs (graph.split_by_part), whose schedules skip
-    the rows they add nothing to."""
-    if _needs_grad(table, out):
+    the rows they add nothing to.  Another epilogue (NONE / BIAS / GIN)
+    overwrites g's scheduled rows of out instead; table2 = second table for
+    sources >= table.shape[0] (the sharded layers' merged halo pass)."""
+    if _needs_grad(table, out, table2):
         raise NotImplementedError("aggregate_accumulate is a forward-only (no_grad) path")
     items, _, split, _, n_slots = g.work(False)
     w = g.w if weighted else None
     if weighted and w is None:
         raise ValueError("graph was built without edge weights")
     _timed(lambda: torch.ops.kgx.spmm_acc_(out, table, g.rowptr, g.rows, items, split, g.col, w, n_slots,
-                                           g.n_long if items is not None else -1))
+                                           g.n_long if items is not None else -1, int(epilogue), bias, xroot,
+                                           float(gin_scale), table2))
     return out
 
 
@@ -164,10 +184,19 @@ def _tiny_abi(items, n_items, n_long, tpack, tw, n_short_end, n_tiny2):
     return n_short_end, tpack, tw, n_tiny2
 
 
+def _x2_args(x, x2):
+    """(x2 pointer, n_x1) of kgx_spmm_gemm_ex3: sources >= x.shape[0] are rows of x2."""
+    if x2 is None:
+        return None, 0
+    if x2.dim() != 2 or x2.shape[1] != x.shape[1] or (x2.shape[0] and x2.stride(0) != x.stride(0)):
+        raise ValueError(f"spmm_gemm: x2 {tuple(x2.shape)} must have x's row width and leading dimension")
+    return nat.ptr(x2), x.shape[0]
+
+
 def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale, save_agg,
-                    relu=False, n_long=-1, tpack=None, tw=None, n_short_end=-1, n_tiny2=0):
-    x, w, W, bias = _f32c(x), _f32c(w), _f32c(W), _f32c(bias)
-    dev = nat.require_device(x, rowptr, rows, idx, w, W, bias, items, split)
+                    relu=False, n_long=-1, tpack=None, tw=None, n_short_end=-1, n_tiny2=0, x2=None):
+    x, w, W, bias, x2 = _f32c(x), _f32c(w), _f32c(W), _f32c(bias), _f32c(x2)
+    dev = nat.require_device(x, rowptr, rows, idx, w, W, bias, items, split, x2)
     n_dst = rowptr.numel() - 1
     F_out = W.shape[1]
     out = torch.empty((n_dst, F_out), dtype=torch.float32, device=dev)
@@ -182,11 +211,12 @@ def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, b
     n_long = n_items if n_long < 0 or n_long > n_items else n_long
     n_se, tpack, tw, n_tiny2 = _tiny_abi(items, n_items, n_long, tpack, tw if w is not None else None, n_short_end,
                                          n_tiny2)
+    x2p, n_x1 = _x2_args(x, x2)
     nat.check(
-        nat.lib().kgx_spmm_gemm_ex2(
+        nat.lib().kgx_spmm_gemm_ex3(
             reduce, nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, n_long, n_se, nat.ptr(tpack),
             nat.ptr(tw), n_tiny2, nat.ptr(split), n_split,
-            nat.ptr(idx), nat.ptr(w), nat.ptr(x), x.stride(0), x.shape[1], nat.ptr(W), F_out, nat.ptr(bias),
+            nat.ptr(idx), nat.ptr(w), nat.ptr(x), x.stride(0), x2p, n_x1, x.shape[1], nat.ptr(W), F_out, nat.ptr(bias),
             int(pre_gin) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0) | (nat.FUSED_RELU if relu else 0),
             float(gin_scale), nat.ptr(out), out.stride(0),
             nat.ptr(partials),
@@ -218,14 +248,16 @@ def spmm_gemm(
     tw: Optional[torch.Tensor] = None,
     n_short_end: int = -1,
     n_tiny2: int = 0,
+    x2: Optional[torch.Tensor] = None,
 ) -> torch.Tensor:
+    """x2 (two-table gathers, kgx_spmm_gemm_ex3): sources >= x.shape[0] are rows of x2."""
     return _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale,
-                           False, relu, n_long, tpack, tw, n_short_end, n_tiny2)[0]
+                           False, relu, n_long, tpack, tw, n_short_end, n_tiny2, x2)[0]
 
 
 @spmm_gemm.register_fake
 def _spmm_gemm_fake(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale, relu=False,
-                    n_long=-1, tpack=None, tw=None, n_short_end=-1, n_tiny2=0):
+                    n_long=-1, tpack=None, tw=None, n_short_end=-1, n_tiny2=0, x2=None):
     return x.new_empty((rowptr.shape[0] - 1, W.shape[1]))
 
 
@@ -281,10 +313,14 @@ def spmm_gemm_acc_(
     tw: Optional[torch.Tensor] = None,
     n_short_end: int = -1,
     n_tiny2: int = 0,
+    x2: Optional[torch.Tensor] = None,
+    accumulate: bool = True,
 ) -> None:
-    """out += bias + REDUCE(...) @ W (KGX_FUSED_ACCUMULATE), in place."""
-    x, w, W, bias = _f32c(x), _f32c(w), _f32c(W), _f32c(bias)
-    dev = nat.require_device(out, x, rowptr, rows, idx, w, W, bias, items, split)
+    """out += bias + REDUCE(...) @ W (KGX_FUSED_ACCUMULATE), in place; with
+    accumulate=False the scheduled rows of out are overwritten instead (and the
+    rest left untouched): two launches over disjoint row sets fill one output."""
+    x, w, W, bias, x2 = _f32c(x), _f32c(w), _f32c(W), _f32c(bias), _f32c(x2)
+    dev = nat.require_device(out, x, rowptr, rows, idx, w, W, bias, items, split, x2)
     n_dst = rowptr.numel() - 1
     if out.dtype != torch.float32 or out.shape != (n_dst, W.shape[1]) or out.stride(1) != 1:
         raise ValueError(f"spmm_gemm_acc_: out must be float32 [{n_dst}, {W.shape[1]}] with unit column stride")
@@ -298,12 +334,13 @@ def spmm_gemm_acc_(
     n_long = n_items if n_long < 0 or n_long > n_items else n_long
     n_se, tpack, tw, n_tiny2 = _tiny_abi(items, n_items, n_long, tpack, tw if w is not None else None, n_short_end,
                                          n_tiny2)
+    x2p, n_x1 = _x2_args(x, x2)
     nat.check(
-        nat.lib().kgx_spmm_gemm_ex2(
+        nat.lib().kgx_spmm_gemm_ex3(
             reduce, nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, n_long, n_se, nat.ptr(tpack),
             nat.ptr(tw), n_tiny2, nat.ptr(split), n_split,
-            nat.ptr(idx), nat.ptr(w), nat.ptr(x), x.stride(0), x.shape[1], nat.ptr(W), W.shape[1], nat.ptr(bias),
-            nat.FUSED_ACCUMULATE, 1.0, nat.ptr(out), out.stride(0), nat.ptr(partials), None, 0, nat.stream(dev),
+            nat.ptr(idx), nat.ptr(w), nat.ptr(x), x.stride(0), x2p, n_x1, x.shape[1], nat.ptr(W), W.shape[1],
+            nat.ptr(bias), (nat.FUSED_ACCUMULATE if accumulate else 0) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0), 1.0, nat.ptr(out), out.stride(0), nat.ptr(partials), None, 0, nat.stream(dev),
         ),
         "kgx_spmm_gemm",
     )
@@ -311,7 +348,7 @@ def spmm_gemm_acc_(
 
 @spmm_gemm_acc_.register_fake
 def _spmm_gemm_acc_fake(out, x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, n_long=-1, tpack=None,
-                        tw=None, n_short_end=-1, n_tiny2=0):
+                        tw=None, n_short_end=-1, n_tiny2=0, x2=None, accumulate=True):
     return None
 
 
@@ -638,14 +675,14 @@ def _tiny_of(g, items):
     return tiny.tiny_pack(g)
 
 
-def _aggregate_transform_raw(g, x, W, red, weighted, bias, pre_gin, gin_scale, exact, relu=False):
+def _aggregate_transform_raw(g, x, W, red, weighted, bias, pre_gin, gin_scale, exact, relu=False, x2=None):
     items, _, split, _, n_slots = g.work(exact)
     w = g.w if weighted else None
     if weighted and w is None:
         raise ValueError("graph was built without GCN normalisation weights")
     return _timed(lambda: torch.ops.kgx.spmm_gemm(
         x, g.rowptr, g.rows, items, split, g.col, w, n_slots, red, W, bias, bool(pre_gin), float(gin_scale),
-        bool(relu), g.n_long if items is not None else -1, *_tiny_of(g, items)
+        bool(relu), g.n_long if items is not None else -1, *_tiny_of(g, items), x2
     ))
 
 
@@ -729,11 +766,18 @@ def aggregate_transform(
     exact: bool = False,
     out: torch.Tensor | None = None,
     relu: bool = False,
+    x2: torch.Tensor | None = None,
+    accumulate: bool = True,
 ) -> torch.Tensor:
     """out = bias + PRE(REDUCE_{e in row} x[col_e] * w_e) @ W in one fused launch
-    (out += ... in place when `out` is given; relu=True applies max(., 0) in the
-    kernel's store).  Differentiable in x, W, bias."""
+    (out += ... in place when `out` is given, or, with accumulate=False, the
+    graph's scheduled rows of `out` overwritten; relu=True applies max(., 0) in
+    the kernel's store).  Differentiable in x, W, bias.  x2 (forward only): a
+    second table, sources col >= x.shape[0] gather x2[col - x.shape[0]]
+    (the sharded layers' own rows + received halo rows in one pass)."""
     red = _reduce_id(reduce)
+    if x2 is not None and _needs_grad(x, x2, W, bias):
+        raise NotImplementedError("aggregate_transform(x2=...) is a forward-only (no_grad) path")
     if out is not None:  # accumulate into `out` (sum only: the caller splits a row's edges)
         if pre_gin or relu or red != nat.SUM:
             raise ValueError("aggregate_transform(out=...) accumulates plain sums only")
@@ -743,8 +787,10 @@ def aggregate_transform(
         w = g.w if weighted else None
         _timed(lambda: torch.ops.kgx.spmm_gemm_acc_(out, x, g.rowptr, g.rows, items, split, g.col, w, n_slots, red,
                                                    W, bias, g.n_long if items is not None else -1,
-                                                   *_tiny_of(g, items)))
+                                                   *_tiny_of(g, items), x2, bool(accumulate)))
         return out
+    if x2 is not None:
+        return _aggregate_transform_raw(g, x, W, red, weighted, bias, pre_gin, gin_scale, exact, relu, x2)
     if _needs_grad(x, W, bias):
         y = _AggregateTransformFn.apply(x, W, bias, g, red, weighted, pre_gin, float(gin_scale), exact)
         return torch.relu(y) if relu else y

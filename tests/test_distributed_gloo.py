@@ -56,8 +56,18 @@ class OracleBackend:
                                          device=torch.device("cpu")))
         return parts
 
-    def aggregate_accumulate(self, g, table, out, weighted=False):
-        out += self.aggregate(g, table, "sum", weighted=weighted)
+    def aggregate_accumulate(self, g, table, out, weighted=False, epilogue=nat.EPI_ACCUM, bias=None, xroot=None,
+                             gin_scale=1.0, table2=None):
+        table = table if table2 is None else torch.cat([table, table2])
+        mask = getattr(g, "row_mask", None)
+        if mask is None:
+            mask = torch.ones(g.n_dst, dtype=torch.bool)
+        if epilogue == nat.EPI_ACCUM:
+            out[mask] += self.aggregate(g, table, "sum", weighted=weighted)[mask]
+        else:
+            y = self.aggregate(g, table, "sum", weighted=weighted, epilogue=epilogue, bias=bias, xroot=xroot,
+                               gin_scale=gin_scale)
+            out[mask] = y[mask]
         return out
 
     def transform(self, x, W, bias=None):
@@ -67,14 +77,27 @@ class OracleBackend:
     def supports_fused(self, f_in, f_out):
         return True
 
-    def aggregate_transform(self, g, x, W, bias=None, out=None):
-        """sum_e w_e x[col_e] in CSR order, then @ W (+ bias); out += ... if given."""
-        y = torch.matmul(self.aggregate(g, x, "sum", weighted=True), W)
+    def restrict_rows(self, g, row_mask):
+        return SimpleNamespace(**vars(g), row_mask=row_mask)
+
+    def aggregate_transform(self, g, x, W, bias=None, out=None, x2=None, accumulate=True):
+        """sum_e w_e x[col_e] in CSR order, then @ W (+ bias); out += ... if given
+        (accumulate=False: overwrite); x2: sources >= len(x) are rows of x2.  A
+        row-restricted graph (restrict_rows) writes only its rows; the others
+        come out NaN (unwritten) so a pass that misses a row fails the test."""
+        table = x if x2 is None else torch.cat([x, x2])
+        y = torch.matmul(self.aggregate(g, table, "sum", weighted=True), W)
         if bias is not None:
             y = K.add(y, bias)
+        mask = getattr(g, "row_mask", None)
+        if mask is None:
+            mask = torch.ones(g.n_dst, dtype=torch.bool)
         if out is None:
-            return y
-        out += y
+            return torch.where(mask.unsqueeze(1), y, torch.full_like(y, float("nan")))
+        if accumulate:
+            out[mask] += y[mask]
+        else:
+            out[mask] = y[mask]
         return out
 
     def aggregate(self, g, table, reduce="sum", weighted=False, epilogue=nat.EPI_NONE, bias=None, **kw):
@@ -87,6 +110,9 @@ class OracleBackend:
             out = K.add(out, bias)
         elif epilogue == nat.EPI_GIN:  # (1+eps) x_i + aggr (gin_conv.py:216-222)
             out = torch.tensor(kw["gin_scale"], dtype=torch.float32) * kw["xroot"] + out
+        mask = getattr(g, "row_mask", None)
+        if mask is not None:  # a row-restricted launch leaves the other rows unwritten
+            out = torch.where(mask.unsqueeze(1), out, torch.full_like(out, float("nan")))
         return out
 
 
@@ -169,6 +195,13 @@ def _worker(rank, world, chunks, port, q):
             y = layer(torch.from_numpy(x[lo:hi]))  # push-pull halo (the default)
         pp = sg._pp
         assert pp is not None and pp.n_rows == pp.n_pull + pp.n_push == pp.chunks[-1].hi
+        assert pp.merged is not None and pp.merged[1] is not None  # the first step folded into its rows' pass
+        os.environ["KGX_HALO_MERGED"] = "0"
+        try:
+            with torch.no_grad():
+                y_unmerged = layer(torch.from_numpy(x[lo:hi]))  # own pass + accumulating chunk passes
+        finally:
+            del os.environ["KGX_HALO_MERGED"]
         os.environ["KGX_HALO_PUSH"] = "0"
         try:
             with torch.no_grad():
@@ -186,8 +219,18 @@ def _worker(rank, world, chunks, port, q):
             layer2.bias.copy_(torch.from_numpy(b))
         with torch.no_grad():
             y_tuned = layer2(torch.from_numpy(x[lo:hi]))
-        assert sorted(sg2.tuning) == [1, 2, 4, 8] and sg2.halo_k in (1, 2, 4, 8)
-        assert len(sg2._pp.chunks) == sg2.halo_k
+        # every candidate timed: the push-pull halo at K = 1 / 2 / 4 / 8 and (this small
+        # graph's remote sources cover most rows) the all-gather at K = 1 / 2 / 4
+        assert sorted(sg2.tuning) == sorted([f"halo:{k}" for k in (1, 2, 4, 8)] + [f"allgather:{k}" for k in (1, 2, 4)])
+        assert sg2.exchange in ("halo", "allgather") and sg2.halo_k in (1, 2, 4, 8)
+        assert len(sg2._pp.chunks) == sg2.halo_k and sg2._pp.kind == sg2.exchange
+        # the all-gather exchange on its own (K = 1 and 3), within the tolerance of the reference
+        ys_gather = []
+        for kk in (1, 3):
+            sg2.exchange, sg2.halo_k = "allgather", kk
+            with torch.no_grad():
+                ys_gather.append(layer2(torch.from_numpy(x[lo:hi])).numpy())
+            assert sg2._pp.kind == "allgather" and len(sg2._pp.chunks) == kk
         # shapes the fused kernel does not take: X W first, then the pipelined weighted sum
         sg3 = kd.ShardedGraph.build(torch.from_numpy(s[keep]), torch.from_numpy(d[keep]), bounds,
                                     backend=UnfusedOracleBackend(), n_features=F_OUT, halo_chunks=chunks)
@@ -222,7 +265,7 @@ def _worker(rank, world, chunks, port, q):
             y_again = layer(xl)  # the weighted plan is still the one the GCN layer uses
         assert torch.equal(y_again, y)
         q.put((rank, gcn.numpy(), mx.numpy(), sg.n_halo, sum(sg.send_counts), y.numpy(), y_pull.numpy(), pp.n_push,
-               y_tuned.numpy(), y_unfused.numpy(), y_wide.numpy()))
+               y_tuned.numpy(), y_unfused.numpy(), y_wide.numpy(), y_unmerged.numpy(), ys_gather[0], ys_gather[1]))
     finally:
         dist.destroy_process_group()
 
@@ -264,7 +307,7 @@ def test_sharded_equals_unsharded_bitwise(world, chunks):
     # overlapped layer path, push-pull and pull-only halos: own-source part, then
     # one part per halo chunk per row (re-associated sums)
     assert sum(results[r][6] for r in range(world)) > 0  # partial sums were pushed
-    for i in (4, 5, 7, 8):
+    for i in (4, 5, 7, 8, 10, 11, 12):
         y_split = np.concatenate([results[r][i] for r in range(world)])
         err = np.abs(y_split - y) / np.maximum(1, np.abs(y))
         assert err.max() <= 1e-5

@@ -105,6 +105,24 @@ def test_dense_nonfinite_propagates(dev):
     assert scaled_err(y[m], ref[m].double()) <= TOL
 
 
+@pytest.mark.parametrize("K", [128, 256])
+def test_dense_huge_finite_pairs(dev, K):
+    """Finite activations whose RNE bf16 rounds to inf (|x| >= 0x1.ffp127),
+    paired with a cancelling partner in the same float4 (a signed
+    running sum hid them from the fast split's guard, which then produced NaN):
+    every output stays finite and f32-accurate."""
+    g = torch.Generator().manual_seed(K)
+    x = torch.randn(96, K, generator=g)
+    W = glorot(K, 64, g) * 0.5
+    x[5, 0], x[5, 2] = -1.70e38, 3.397e38   # the advisor's pair: 2x overflows, the fma chain did not
+    x[9, 4], x[9, 5] = 3.40e38, -3.40e38    # exact cancellation
+    x[40, K - 1] = -3.4028e38               # a lone near-FLT_MAX value
+    y = torch.ops.kgx.dense(x.to(dev), W.to(dev), None, None, None, False).cpu()
+    ref = ref64(x, W)
+    assert bool(torch.isfinite(y).all())
+    assert scaled_err(y, ref) <= TOL
+
+
 def test_dense_empty_and_limits(dev):
     W = torch.randn(128, 64, device=dev)
     assert torch.ops.kgx.dense(torch.empty(0, 128, device=dev), W, None, None, None, False).shape == (0, 64)

@@ -57,6 +57,14 @@ class ThreadComm(kd.TorchComm):
         self.all_to_all_single(out, inp, out_splits, in_splits)  # synchronous: rows ordered on return
         return None
 
+    def all_gather(self, out, inp):
+        w = self.hub.world
+        self.all_to_all_single(out, inp.repeat(w, *([1] * (inp.dim() - 1))).contiguous())
+
+    def all_gather_start(self, out, inp):
+        self.all_gather(out, inp)
+        return None
+
     def broadcast(self, t, src=0):
         if self.r == src:
             self.hub.slots[src] = t.detach().clone()
@@ -117,6 +125,11 @@ class AsyncThreadComm(ThreadComm):
                 torch.cuda.current_stream().wait_event(done)
 
         return Work()
+
+    def all_gather_start(self, out, inp):
+        w = self.hub.world
+        n = inp.shape[0]
+        return self.all_to_all_start(out, inp.repeat(w, *([1] * (inp.dim() - 1))), [n] * w, [n] * w)
 
 
 COMMS = {"sync": lambda hub, r: ThreadComm(hub, r),

@@ -1,6 +1,11 @@
-"""One rank's device work of the weak-scaled sharded GCN layer, on one GPU.
+"""One rank's device work of a sharded layer, on one GPU.
 
-  python tools/shard_sim.py [--world 8] [--chunks 1,2,4,8] [--steps 10]
+  python tools/shard_sim.py [--config ns|c4|c5] [--world 8] [--chunks 1,2,4,8]
+                            [--exchange halo,allgather] [--link-gbps 400] [--steps 10]
+
+ns: GCN weak scaling (every rank 10M nodes / 100M edges of one N x 10M graph);
+c4: GIN-sum 10M / 100M F256 and c5: SAGE-mean 2.45M / 123.7M F100, strong
+scaling (rank 0's shard of the one graph), as bench.py --config c4 / c5.
 
 Builds rank 0's shard of the P x 10M-node / P x 100M-edge R-MAT graph as
 bench.py --gpus P does, but with a loopback comm: the peers' requests are
@@ -91,20 +96,63 @@ class LoopbackComm(kd.TorchComm):
     def broadcast(self, t, src=0):
         pass
 
+    def all_gather(self, out, inp):
+        """Peers mirror this rank: every rank's slice is a copy of ours."""
+        out.view(self.w, *inp.shape).copy_(inp.unsqueeze(0).expand(self.w, *inp.shape))
+
+    def all_gather_start(self, out, inp):
+        """As all_to_all_start: the modelled link time covers the (world-1)/world received share."""
+        if self.link_gbps <= 0:
+            self.all_gather(out, inp)
+            ev = torch.cuda.Event()
+            ev.record()
+            return _EventWork(ev)
+        if self.link is None:
+            self.link = torch.cuda.Stream(priority=-1)
+        ready = torch.cuda.Event()
+        ready.record()
+        self.link.wait_event(ready)
+        with torch.cuda.stream(self.link):
+            ms = out.numel() * out.element_size() * (self.w - 1) / self.w / (self.link_gbps * 1e6)
+            if ms > 0:
+                torch.cuda._sleep(int(ms * self.cycles_per_ms))
+            self.all_gather(out, inp)
+            inp.record_stream(self.link)
+            out.record_stream(self.link)
+            ev = torch.cuda.Event()
+            ev.record()
+        return _EventWork(ev)
+
+
+CONFIGS = {  # name: (layer, nodes, edges, features, scaling) -- bench.py's configs
+    "ns": ("gcn", 10_000_000, 100_000_000, 128, "weak"),
+    "c4": ("gin", 10_000_000, 100_000_000, 256, "strong"),
+    "c5": ("sage", 2_449_029, 123_718_280, 100, "strong"),
+}
+
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="ns", choices=sorted(CONFIGS),
+                    help="ns: GCN weak (N x 10M / N x 100M); c4: GIN-sum 10M/100M F256 strong; "
+                         "c5: SAGE-mean 2.45M/123.7M F100 strong")
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--chunks", default="1,2,4,8")
-    ap.add_argument("--push", default="0,1", help="KGX_HALO_PUSH values to run (0: pull-only halo)")
+    ap.add_argument("--exchange", default="halo", help="halo,allgather: exchanges to run")
+    ap.add_argument("--push", default="1", help="KGX_HALO_PUSH values to run (0: pull-only halo)")
+    ap.add_argument("--merged", default="1", help="KGX_HALO_MERGED values to run (0: round-2 own pass + chunk passes)")
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--nodes", type=int, default=10_000_000)
-    ap.add_argument("--edges", type=int, default=100_000_000)
+    ap.add_argument("--nodes", type=int, default=None)
+    ap.add_argument("--edges", type=int, default=None)
     ap.add_argument("--link-gbps", type=float, default=0.0,
                     help="model the exchange: per-GPU receive rate in GB/s (0: the exchange is free)")
     args = ap.parse_args()
+    layer_kind, n_cfg, e_cfg, F, scaling = CONFIGS[args.config]
+    n_cfg = args.nodes or n_cfg
+    e_cfg = args.edges or e_cfg
     dev = torch.device("cuda", 0)
     P = args.world
+    n_glob, e_glob = (n_cfg * P, e_cfg * P) if scaling == "weak" else (n_cfg, e_cfg)
     cycles_per_ms = 0.0
     if args.link_gbps > 0:  # calibrate torch.cuda._sleep's cycles against events
         t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -114,14 +162,26 @@ def main():
         t1.record()
         torch.cuda.synchronize()
         cycles_per_ms = 100_000_000 / t0.elapsed_time(t1)
-    for push, K in [(p, int(v)) for p in args.push.split(",") for v in args.chunks.split(",")]:
+    runs = [(x, m, p, int(v)) for x in args.exchange.split(",") for m in args.merged.split(",")
+            for p in args.push.split(",") for v in args.chunks.split(",")]
+    for exchange, merged, push, K in runs:
+        if exchange == "allgather" and (push == "0" or merged == "0"):
+            continue  # the all-gather has neither pulls nor pushes, and always runs merged
         os.environ["KGX_HALO_PUSH"] = push
-        n_local = kd.equal_bounds(args.nodes * P, P)[1]
+        os.environ["KGX_HALO_MERGED"] = merged
+        n_local = kd.equal_bounds(n_glob, P)[1]
         comm = LoopbackComm(P, n_local, args.link_gbps, cycles_per_ms)
-        sg = kd.ShardedGraph.rmat(args.nodes * P, args.edges * P, seed=0, device=dev, comm=comm,
-                                  self_loops=True, gcn_norm=True, halo_chunks=K)
-        x = torch.randn(sg.n_local, 128, device=dev)
-        layer = kd.ShardedGCNConv(128, sg)
+        gcn = layer_kind == "gcn"
+        sg = kd.ShardedGraph.rmat(n_glob, e_glob, seed=0, device=dev, comm=comm, self_loops=gcn, gcn_norm=gcn,
+                                  halo_chunks=K, n_features=F)
+        sg.exchange = exchange
+        x = torch.randn(sg.n_local, F, device=dev)
+        if layer_kind == "gcn":
+            layer = kd.ShardedGCNConv(F, sg)
+        elif layer_kind == "gin":
+            layer = kd.ShardedGINConv(F, sg, aggregator="sum")
+        else:
+            layer = kd.ShardedSAGEConv(F, sg, aggregator="mean")
         with torch.no_grad():
             layer(x)
             g_own, g_chunks = sg.own_halo_parts()
@@ -143,11 +203,16 @@ def main():
         pp = sg._pp
         if pp is not None:
             g_chunks = pp.parts
+        recv_rows = (pp.n_rows * (P - 1) // P if pp.kind == "allgather" else pp.n_rows) if pp else sg.n_halo
         print(json.dumps({
-            "world": P, "chunks": K, "push_pull": pp is not None, "link_gbps": args.link_gbps, "step_ms": round(t0.elapsed_time(t1) / args.steps, 3),
+            "config": args.config, "layer": layer_kind, "scaling": scaling, "nodes": n_glob, "edges": e_glob,
+            "features": F, "world": P, "exchange": pp.kind if pp else "pull", "chunks": K,
+            "push_pull": pp is not None and pp.kind == "halo", "merged": merged == "1",
+            "link_gbps": args.link_gbps, "step_ms": round(t0.elapsed_time(t1) / args.steps, 3),
             "launch_ms": [round(v, 3) for v in launch_ms],
             "own_edges": g_own.kept, "chunk_edges": [g.kept for g in g_chunks],
             "halo_rows_pull_only": sg.n_halo, "halo_rows": pp.n_rows if pp else sg.n_halo,
+            "received_MB": recv_rows * F * 4 / 1e6,
             "pulled": pp.n_pull if pp else sg.n_halo, "pushed": pp.n_push if pp else 0,
             "chunk_items": [g.n_items for g in g_chunks], "n_local": sg.n_local,
         }), flush=True)
