@@ -173,13 +173,19 @@ int kgx_spmm_ex(int reduce, int epilogue, const int32_t* rowptr, const int32_t* 
  * rows of table, c >= n_table1 rows c - n_table1 of table2 (same ld_table).
  * Needs the schedule (items; not EXACT / std).  The sharded GIN / SAGE layers
  * reduce a row's own-source and halo edges in one pass (distributed.py).
- * table2 NULL: kgx_spmm_ex. */
+ * table2 NULL: kgx_spmm_ex.
+ * counters (EXACT mode, items NULL): two caller-owned int32, zeroed before the
+ * call, from which the launch hands out rows dynamically; the hub-row kernel
+ * then runs on a library-owned forked stream beside the main kernel and is
+ * joined back into `stream` before the call's last launch (bit-identical
+ * results: every row is still reduced by one lane chain in CSR order,
+ * aggregators.py:126-137).  NULL: the static schedule, one stream. */
 int kgx_spmm_ex2(int reduce, int epilogue, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
                  const int32_t* items, int64_t n_items, int64_t n_long_items, const int32_t* split, int64_t n_split,
                  const int32_t* idx, const float* w, const float* table, int64_t ld_table, const float* table2,
                  int64_t n_table1, int64_t F, float* out, int64_t ld_out, const float* bias, const float* xroot,
                  int64_t ld_x, float gin_scale, const int32_t* drop_key, float drop_p, uint64_t drop_seed,
-                 float* partials, kgx_stream_t stream);
+                 float* partials, int32_t* counters, kgx_stream_t stream);
 
 /* Message dropout mask (training; GCNConv.message dropout, gcn_conv.py:237-242;
  * GATv2 attention dropout, gatv2_conv.py:252-253): element (key, f) is kept

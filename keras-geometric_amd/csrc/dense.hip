@@ -107,7 +107,9 @@ constexpr int kProducerWaves = 4;
 // tile (Os, double-buffered by tile parity) and, during the next tile's last
 // k-step, every wave reads two whole-row float4 runs back and stores them with
 // dwordx4: one wave instruction = two 512-B rows.
-template <int KS, int WAVES, bool ACC, bool TWO, bool LS = false>
+// PS: the opt-in producer-store experiment (KGX_DENSE_PSTORE); only LS and PS
+// instantiations carry the LDS out tile.
+template <int KS, int WAVES, bool ACC, bool TWO, bool LS = false, bool PS = false>
 __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(DenseArgs a) {
   using G = Geom<KS>;
   constexpr int TP = 64 * kProducerWaves;
@@ -118,7 +120,7 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
   // output tile staged for the producers' stores (a.pstore), double-buffered by step parity
   constexpr int OCOLS = 16 * WAVES;
   constexpr int OSTRIDE = OCOLS + 4;  // floats; 4 mod 32 dwords between rows
-  __shared__ float Os[2][kBM][OSTRIDE];
+  __shared__ float Os[2][(LS || PS) ? kBM : 1][(LS || PS) ? OSTRIDE : 1];
   __shared__ float Ob[LS ? OCOLS : 1];  // LS: this block's bias columns (read beside the out rows)
 
   const int tid = threadIdx.x;
@@ -289,7 +291,7 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
     const int ocol = cg * OCOLS + 4 * pc4;
     float ob4[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) ob4[j] = (!TWO && !ACC && a.pstore && a.bias && ocol + j < a.N) ? a.bias[ocol + j] : 0.0f;
+    for (int j = 0; j < 4; ++j) ob4[j] = (PS && a.bias && ocol + j < a.N) ? a.bias[ocol + j] : 0.0f;
     auto store_out = [&](int64_t step) {  // step < 0: dummy stores (dropped)
       const int64_t tile = pid + (step < 0 ? 0 : step) * n_pairs;
       const int64_t r0 = tile * kBM;
@@ -324,7 +326,7 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
       return;
     }
     // two operands hold two register sets per slot: no registers left for the store path
-    const bool pstore = !TWO && !ACC && a.pstore;
+    constexpr bool pstore = PS && !TWO && !ACC;
     int64_t t = pid;
     load_tile(P[0], Q[0], t);
     wait_set(P[0], Q[0], Zero{});
@@ -527,7 +529,7 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
 #pragma unroll
         for (int j = 0; j < 4; ++j) Os[buf][16 * r + 4 * lq + j][wave * 16 + lr] = acc[r][j];
       lprev_rs = tile_rsrc_ls(t);
-    } else if (!TWO && !ACC && a.pstore) {
+    } else if constexpr (PS && !TWO && !ACC) {
       // lane holds rows 4 lq + j of column lr of each 16x16 block: into the LDS
       // out tile for the producers' stores (bias / ReLU applied there)
 #pragma unroll
@@ -617,6 +619,7 @@ int launch(const DenseArgs& a, hipStream_t s) {
       k = a.K1 > 0 ? dense_kernel<KS, WAVES, false, true, true> : dense_kernel<KS, WAVES, false, false, true>;
   }
 #endif
+  if (a.pstore && a.K1 == 0) k = dense_kernel<KS, WAVES, false, false, false, true>;
   static int cus = 0;
   if (cus == 0) {
     int dev = 0;

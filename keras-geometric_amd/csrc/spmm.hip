@@ -65,6 +65,10 @@ struct SpmmArgs {
   // table (same ld_t); t2b = table2 - n_t1 * ld_t as an address.  n_t1 = INT32_MAX: one table.
   const float* t2b;
   int32_t n_t1;
+  // EXACT mode, dynamic row pickup (kgx_spmm_ex2 counters): dyn[0] hands out the
+  // hub kernel's (row, column group) items, dyn[1] spmm_kernel's row batches.
+  // NULL: the static grid-stride schedule.
+  int32_t* dyn;
 };
 
 // Source row of column c: table[c], or with TWO table2[c - n_t1] (a separate
@@ -212,16 +216,39 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
     fl[t] = fv[t] ? fo[t] : a.F - VEC;  // load offset, always in range
   }
 
-  for (int64_t it = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> a.lgG; it < n_work; it += ngroups) {
+  // EXACT mode with a.dyn: each group takes batches of kDynRows consecutive rows
+  // from a counter (lane 0's atomic, broadcast to the group), so groups whose
+  // blocks started late -- behind the hub kernel running beside this one --
+  // take less, and the launch ends together.  Otherwise: static grid-stride.
+  const bool dyn = a.dyn != nullptr && !a.items;
+  constexpr int kDynRows = 8;
+  const int64_t gid = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> a.lgG;
+  int64_t it = gid, batch_end = 0;
+  if (dyn) it = batch_end = 0;
+  for (;;) {
+    if (dyn) {
+      if (it >= batch_end) {
+        int64_t b = 0;
+        if (lane == 0) b = int64_t(atomicAdd(a.dyn + 1, kDynRows));
+        b = __shfl(b, 0, G);  // the group's lane 0 (groups are aligned G-lane slices of the wave)
+        it = b;
+        batch_end = b + kDynRows < n_work ? b + kDynRows : n_work;
+      }
+      if (it >= n_work) break;
+    } else if (it >= n_work) {
+      break;
+    }
+    const int64_t cur = it;
+    it = dyn ? it + 1 : it + ngroups;
     int32_t row, beg, end, slot;
     if (a.items) {
-      const int4 v = a.items[it];
+      const int4 v = a.items[cur];
       row = v.x;
       beg = v.y;
       end = v.z;
       slot = v.w;
     } else {
-      row = a.rows[it];
+      row = a.rows[cur];
       beg = a.rowptr[row];
       end = a.rowptr[row + 1];
       slot = -1;
@@ -360,9 +387,27 @@ __global__ __launch_bounds__(kHubThreads, 1) void spmm_hub_kernel(SpmmArgs a) {
   constexpr int D = kHubD / RPL;              // stages of loads in flight (D x RPL rows per lane)
   static_assert(kHubSMax % 8 == 0 && D >= 2 && D % 2 == 0, "hub pipeline shape");
   __shared__ __attribute__((aligned(16))) float ring[3][S * RL];
+  __shared__ int32_t hub_next[2];  // dynamic pickup: the block's next item, by row parity
 
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   const int lane = threadIdx.x & 63;
+  // Items (row, column group) in descending row degree.  Static: p += gridDim.x.
+  // Dynamic (a.dyn): thread 0 (a consumer) takes the block's next item from a
+  // counter while the row runs and parks it in LDS; one extra barrier per row
+  // (rows here have >= 2048 edges) hands it to every wave, so blocks that drew
+  // short hubs take more of them instead of idling behind the largest row.
+  const int64_t n_hub_items = a.n_rows * ((a.F + 4 * G - 1) / (4 * G));
+  int par = 0;
+  auto next_item = [&](int64_t p) -> int64_t {
+    if (!a.dyn) return p + gridDim.x;
+    hub_barrier();  // thread 0's LDS write (waited for with lgkmcnt(0) here) is visible
+    const int64_t q = hub_next[par];
+    par ^= 1;
+    return q;
+  };
+  auto claim_next = [&]() {  // thread 0, at a row's start: the item after this one
+    if (a.dyn && threadIdx.x == 0) hub_next[par] = int32_t(gridDim.x) + atomicAdd(a.dyn, 1);
+  };
 
   // Row h of the degree-ordered list; false past the long rows.  Iteration s
   // of a row: producers write stage s into ring[s % 3]; consumers read stage
@@ -390,8 +435,9 @@ __global__ __launch_bounds__(kHubThreads, 1) void spmm_hub_kernel(SpmmArgs a) {
 #if KGX_HUB_PRIO
     __builtin_amdgcn_s_setprio(3);  // the fold chain is the row's critical path
 #endif
-    for (int64_t p = blockIdx.x; p < a.n_rows * ncg; p += gridDim.x) {
+    for (int64_t p = blockIdx.x; p < n_hub_items; p = next_item(p)) {
       KGX_HUB_ROW(p)
+      claim_next();
       const int f = wave * 64 + lane;
       const int fc = f < RL ? f : RL - 1;
       float acc = R::init();
@@ -444,7 +490,7 @@ __global__ __launch_bounds__(kHubThreads, 1) void spmm_hub_kernel(SpmmArgs a) {
   }
 
   // ---- producers: lane (slot r, features f..f+3) of every stage
-  for (int64_t p = blockIdx.x; p < a.n_rows * ncg; p += gridDim.x) {
+  for (int64_t p = blockIdx.x; p < n_hub_items; p = next_item(p)) {
     KGX_HUB_ROW(p)
     const int slot = (wave - CW) * RPW + lane / G;
     if (__builtin_amdgcn_readfirstlane(slot) >= SP) {  // idle producer wave: barriers only
@@ -754,9 +800,31 @@ __global__ __launch_bounds__(kBlock) void spmm_std_kernel(SpmmArgs a) {
 
 
 
+// A per-host-thread side stream and fork / join events (EXACT mode's hub kernel
+// beside spmm_kernel).  Thread-local: concurrent launches from several host
+// threads (one rank per thread in the tests) never share events.
+struct ForkJoin {
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  int device = -1;
+};
+ForkJoin& fork_join() {
+  thread_local ForkJoin fj;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (fj.device != dev) {
+    (void)hipStreamCreateWithFlags(&fj.side, hipStreamNonBlocking);
+    (void)hipEventCreateWithFlags(&fj.fork, hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&fj.join, hipEventDisableTiming);
+    fj.device = dev;
+  }
+  return fj;
+}
+
 template <int VEC, int NT, int RED, bool W, bool TWO = false>
 int launch_main(const SpmmArgs& a_in, hipStream_t s) {
   SpmmArgs a = a_in;
+  ForkJoin* joined = nullptr;
   if constexpr (NT == 1) {
     static const bool hub_off = [] {
       const char* h = getenv("KGX_HUB");
@@ -771,8 +839,27 @@ int launch_main(const SpmmArgs& a_in, hipStream_t s) {
       else if (gh == 8) kh = spmm_hub_kernel<8, RED, W>;
       const int64_t work = a.n_rows * ((a.F + 4 * gh - 1) / (4 * gh));
       const int64_t nb = work < cu_count() ? work : cu_count();  // one resident block per CU
-      hipLaunchKernelGGL(kh, dim3(unsigned(nb)), dim3(kHubThreads), 0, s, a);
-      KGX_CHECK_LAUNCH();
+      if (a.dyn) {
+        // dynamic pickup: the hub kernel runs on a forked stream BESIDE spmm_kernel
+        // (which skips the hub rows and takes its rows from a counter), so the CUs
+        // the hub kernel's tail leaves idle -- its largest row alone is ~1 ms at
+        // NS -- run ordinary rows instead of waiting; joined back below.
+        ForkJoin& fj = fork_join();
+        if (hipEventRecord(fj.fork, s) != hipSuccess || hipStreamWaitEvent(fj.side, fj.fork, 0) != hipSuccess) {
+          set_error("kgx_spmm: stream fork failed");
+          return KGX_ERR_HIP;
+        }
+        hipLaunchKernelGGL(kh, dim3(unsigned(nb)), dim3(kHubThreads), 0, fj.side, a);
+        KGX_CHECK_LAUNCH();
+        if (hipEventRecord(fj.join, fj.side) != hipSuccess) {
+          set_error("kgx_spmm: stream join failed");
+          return KGX_ERR_HIP;
+        }
+        joined = &fj;
+      } else {
+        hipLaunchKernelGGL(kh, dim3(unsigned(nb)), dim3(kHubThreads), 0, s, a);
+        KGX_CHECK_LAUNCH();
+      }
     } else if (!a.items && a.n_rows > 0) {  // EXACT: long rows first, on their own kernel
       a.long_rows = 1;
       auto kl = spmm_long_kernel<VEC, RED, W>;
@@ -804,6 +891,10 @@ int launch_main(const SpmmArgs& a_in, hipStream_t s) {
     }
     hipLaunchKernelGGL(k, dim3(resident_grid(k, work_long, a.G)), dim3(kBlock), 0, s, a);
     KGX_CHECK_LAUNCH();
+  }
+  if (joined && hipStreamWaitEvent(s, joined->join, 0) != hipSuccess) {
+    set_error("kgx_spmm: stream join failed");
+    return KGX_ERR_HIP;
   }
   if (a.items && a.n_split > 0) {
     auto k = spmm_fixup_kernel<VEC, NT, RED>;
@@ -877,7 +968,7 @@ extern "C" int kgx_spmm_ex(int reduce, int epilogue, const int32_t* rowptr, cons
                            float* partials, kgx_stream_t stream_) {
   return kgx_spmm_ex2(reduce, epilogue, rowptr, rows, n_rows, items, n_items, n_long_items, split, n_split, idx, w,
                       table, ld_table, nullptr, 0, F, out, ld_out, bias, xroot, ld_x, gin_scale, drop_key, drop_p,
-                      drop_seed, partials, stream_);
+                      drop_seed, partials, nullptr, stream_);
 }
 
 extern "C" int kgx_spmm_ex2(int reduce, int epilogue, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
@@ -886,7 +977,7 @@ extern "C" int kgx_spmm_ex2(int reduce, int epilogue, const int32_t* rowptr, con
                             const float* table2, int64_t n_table1, int64_t F, float* out, int64_t ld_out,
                             const float* bias, const float* xroot, int64_t ld_x, float gin_scale,
                             const int32_t* drop_key, float drop_p, uint64_t drop_seed, float* partials,
-                            kgx_stream_t stream_) {
+                            int32_t* counters, kgx_stream_t stream_) {
   hipStream_t stream = as_stream(stream_);
   KGX_REQUIRE(!table2 || (n_table1 >= 0 && n_table1 < (int64_t(1) << 31) && items), KGX_ERR_ARG,
               "kgx_spmm: a second table needs 0 <= n_table1 < 2^31 and the schedule (not EXACT mode)");
@@ -944,6 +1035,7 @@ extern "C" int kgx_spmm_ex2(int reduce, int epilogue, const int32_t* rowptr, con
 
   // widest vector the shapes and pointers allow
   a.n_t1 = table2 ? int32_t(n_table1) : INT32_MAX;
+  a.dyn = (!use_items && reduce != KGX_STD) ? counters : nullptr;
   auto ok = [&](int v) {
     const int b = 4 * v;
     return F % v == 0 && ld_table % v == 0 && ld_out % v == 0 && aligned(table, b) && aligned(out, b) &&

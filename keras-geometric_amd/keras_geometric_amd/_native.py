@@ -63,7 +63,7 @@ _SIGNATURES = {
     "kgx_spmm_ex2": [
         _int, _int, _i32p, _i32p, _i64, _i32p, _i64, _i64, _i32p, _i64,
         _i32p, _f32p, _f32p, _i64, _f32p, _i64, _i64, _f32p, _i64,
-        _f32p, _f32p, _i64, ctypes.c_float, _i32p, ctypes.c_float, ctypes.c_uint64, _f32p, ctypes.c_void_p,
+        _f32p, _f32p, _i64, ctypes.c_float, _i32p, ctypes.c_float, ctypes.c_uint64, _f32p, _i32p, ctypes.c_void_p,
     ],
     "kgx_dropout_mask": [ctypes.c_uint64, ctypes.c_float, _i32p, _i64, _i64, _f32p, ctypes.c_void_p],
     "kgx_spmm_gemm": [

@@ -244,7 +244,7 @@ class PushPullPlan:
     step_parts: list | None = None  # receiver CSR per exchange step, in issue order (accumulate-only)
     weighted: bool = True  # receiver edges carry the GCN norms (else weight 1, plain partial sums)
     kind: str = "halo"  # "halo" (push-pull all-to-all) or "allgather" (every rank's rows, chunked)
-    merged: tuple | None = None  # (own pass, first-step pass, steps accumulated after): ShardedGraph.merged_passes
+    merged: dict | None = None  # unit -> (own pass, first-group pass, later groups, first wait): merged_passes
 
 
 class _Works:
@@ -636,7 +636,7 @@ class ShardedGraph:
     def exchange_plan(self, n_chunks: int | None = None, weighted: bool | None = None) -> PushPullPlan:
         """The plan of the chosen exchange ("halo": push-pull all-to-all; "allgather")."""
         if self.exchange == "allgather":
-            return self.allgather_plan(n_chunks or self.halo_k or 1, weighted)
+            return self.allgather_plan(n_chunks or self.halo_k or len(self.chunks), weighted)
         return self.push_pull_plan(n_chunks, weighted)
 
     def exchange_candidates(self, feature_bytes: int, halo_ks=(1, 2, 4, 8), gather_ks=(1, 2, 4)) -> list:
@@ -684,32 +684,46 @@ class ShardedGraph:
         self.exchange_plan(self.halo_k)
         return candidates[i]
 
-    def merged_passes(self, pp: PushPullPlan):
+    def merged_passes(self, pp: PushPullPlan, unit: str | None = None):
         """(g_a, g_b, later): the default path's passes with the first exchange
-        step folded into the rows it touches (cached on the plan).
+        group folded into the rows it touches (cached on the plan per unit).
 
-        H = the local rows with an edge in the first step (chunk 0's pulled
-        rows).  g_a: the own-source CSR restricted to the rows NOT in H -- it
-        writes them, and runs while the exchange is in flight.  g_b: for the
-        rows in H, their own-source edges followed by their first-step edges
+        Groups: unit "step" (default; KGX_HALO_MERGE=step) -- every exchange
+        step on its own (chunk k's pulled rows, then its pushed partials);
+        "chunk" -- a chunk's steps together.  H = the local rows with an edge in
+        the first group.  g_a: the own-source CSR restricted to the rows NOT in
+        H -- it writes them, while the exchange is in flight.  g_b: for the rows
+        in H, their own-source edges followed by their first-group edges
         (sources >= n_local index the halo buffer), written once by ONE
-        two-table pass (kgx_spmm_gemm_ex3), instead of an own pass that writes
-        them and a halo pass that reads and rewrites them.  later: [(step, CSR)]
-        for the remaining exchange steps (the pushed partials, later chunks),
+        two-table pass (kgx_spmm_gemm_ex3 / kgx_spmm_ex2) instead of an own pass
+        that writes them and a halo pass that reads and rewrites them.  later:
+        [(step to wait for, CSR, halo lo, halo hi)] for the remaining groups,
         accumulate-only over the rows each touches.  Each row's sum is own
-        edges, then first-step edges, then later steps: a re-association of
+        edges, then first-group edges, then later groups: a re-association of
         the one-pass order, tolerance-equal like the rest of this path."""
-        if pp.merged is not None:
-            return pp.merged
+        unit = unit or os.environ.get("KGX_HALO_MERGE", "step")
+        if pp.merged is None:
+            pp.merged = {}
+        if unit in pp.merged:
+            return pp.merged[unit]
         g_own, _ = self.own_halo_parts()
         n_local = self.n_local
         dev = g_own.col.device
         steps = [st for c in pp.chunks for st in c.steps]
-        first = pp.step_parts[0] if pp.step_parts else None
+        groups, idx = [], 0
+        if unit == "chunk":
+            for k, c in enumerate(pp.chunks):
+                idx += len(c.steps)
+                if k < len(pp.parts):
+                    groups.append((idx - 1, pp.parts[k], c.lo, c.hi))
+        else:
+            for i, g in enumerate(pp.step_parts or []):
+                groups.append((i, g, steps[i].lo, steps[i].hi))
+        first = groups[0][1] if groups else None
         if first is None or first.kept == 0:
-            pp.merged = (g_own, None, [(i, g) for i, g in enumerate(pp.step_parts or []) if g.kept])
-            return pp.merged
-        lo0 = steps[0].lo
+            pp.merged[unit] = (g_own, None, [t for t in groups if t[1].kept], -1)
+            return pp.merged[unit]
+        lo0 = groups[0][2]
         in_h = first.deg > 0
         ar = torch.arange(n_local, device=dev)
         r_own = torch.repeat_interleave(ar, g_own.deg.long(), output_size=g_own.kept)
@@ -717,15 +731,15 @@ class ShardedGraph:
         r_first = torch.repeat_interleave(ar, first.deg.long(), output_size=first.kept)
         rows = torch.cat([r_own[keep], r_first])
         cols = torch.cat([g_own.col[keep].long(), first.col.long() + (n_local + lo0)])
-        # own edges first, then the step's: the stable CSR keeps that order inside every row
+        # own edges first, then the group's: the stable CSR keeps that order inside every row
         g_b = self.backend.build_graph(cols.to(torch.int32), rows.to(torch.int32), n_local + pp.n_rows, n_local, 128)
         if pp.weighted:
             g_b.w = torch.cat([g_own.w[keep], first.w])[g_b.eid.long()].contiguous()
         g_b = self.backend.restrict_rows(g_b, in_h)
         g_a = self.backend.restrict_rows(g_own, ~in_h)
-        later = [(i, g) for i, g in enumerate(pp.step_parts[1:], start=1) if g.kept]
-        pp.merged = (g_a, g_b, later)
-        return pp.merged
+        later = [t for t in groups[1:] if t[1].kept]
+        pp.merged[unit] = (g_a, g_b, later, groups[0][0])
+        return pp.merged[unit]
 
     def halo_exchange(self, table: torch.Tensor) -> None:
         """table[n_local:] <- rows other ranks own (one all-to-all-v over RCCL
@@ -856,7 +870,7 @@ class ShardedGraph:
         with them in ONE two-table pass (own then first-step edges, epilogue
         applied) once chunk 0's pulled rows have landed; then out += the later
         steps' row sums as each lands."""
-        g_a, g_b, later = self.merged_passes(pp)
+        g_a, g_b, later, first_wait = self.merged_passes(pp)
         steps = [st for c in pp.chunks for st in c.steps]
         kw = dict(weighted=weighted, bias=bias, xroot=x_local if fold_gin else None,
                   gin_scale=float(gin_scale) if fold_gin else 1.0)
@@ -877,12 +891,11 @@ class ShardedGraph:
             with kops.sharing_gpu():
                 out = self.backend.aggregate(g_a, x_local, "sum", epilogue=epi, **kw)
             if g_b is not None:
-                wait_step(0)
+                wait_step(first_wait)
                 self.backend.aggregate_accumulate(g_b, x_local, out, epilogue=epi, table2=halo, **kw)
-            for i, g in later:
+            for i, g, lo, hi in later:
                 wait_step(i)
-                st = steps[i]
-                self.backend.aggregate_accumulate(g, halo[st.lo: st.hi], out, weighted=weighted)
+                self.backend.aggregate_accumulate(g, halo[lo: hi], out, weighted=weighted)
             wait_step(len(steps) - 1)
         return out
 
@@ -1015,8 +1028,9 @@ class ShardedGCNConv(Layer):
         + A_0 halo_0) W in one two-table pass; then out += (A_s halo_s) W per
         later step (pushed partials, later chunks) as each lands."""
         sg = self.sg
-        g_a, g_b, later = sg.merged_passes(pp)
+        g_a, g_b, later, first_wait = sg.merged_passes(pp)
         steps = [st for c in pp.chunks for st in c.steps]
+        a_late = os.environ.get("KGX_HALO_A_LATE", "0") == "1"  # measurement A/B: own-only rows after the merged pass
         with torch.no_grad():
             works = sg.start_halo_exchange(x_local, halo, pp.chunks)
             handles = []
@@ -1031,18 +1045,23 @@ class ShardedGCNConv(Layer):
                         if handles[j] is not None:
                             handles[j].wait()
 
-            with kops.sharing_gpu():  # the exchange's packing and RCCL kernels run beside this pass
-                out = sg.backend.aggregate_transform(g_a, x_local, self.kernel, bias=bias)
+            if a_late and g_b is not None:
+                out = torch.empty((x_local.shape[0], self.kernel.shape[1]), dtype=torch.float32,
+                                  device=x_local.device)
+            else:
+                with kops.sharing_gpu():  # the exchange's packing and RCCL kernels run beside this pass
+                    out = sg.backend.aggregate_transform(g_a, x_local, self.kernel, bias=bias)
             if g_b is not None:
-                wait_step(0)
+                wait_step(first_wait)
                 with kops.sharing_gpu() if later else contextlib.nullcontext():
                     sg.backend.aggregate_transform(g_b, x_local, self.kernel, bias=bias, out=out, x2=halo,
                                                    accumulate=False)
-            for n, (i, g) in enumerate(later):
+                if a_late:
+                    sg.backend.aggregate_transform(g_a, x_local, self.kernel, bias=bias, out=out, accumulate=False)
+            for n, (i, g, lo, hi) in enumerate(later):
                 wait_step(i)
-                st = steps[i]
                 with kops.sharing_gpu() if n + 1 < len(later) else contextlib.nullcontext():
-                    sg.backend.aggregate_transform(g, halo[st.lo: st.hi], self.kernel, out=out)
+                    sg.backend.aggregate_transform(g, halo[lo: hi], self.kernel, out=out)
             # every step, used or not: also orders the side stream's reads of x_local
             wait_step(len(steps) - 1)
         return out

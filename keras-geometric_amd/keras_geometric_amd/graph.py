@@ -174,6 +174,15 @@ def _build_schedule(g: CSRGraph, split_len: int) -> None:
     g.items = items[: g.n_items]
     g.split = split[: max(g.n_split, 0)]
     g.n_long = short_suffix_start(g.items)
+    _refresh_tiny(g)
+
+
+def _refresh_tiny(g: CSRGraph) -> None:
+    """(Re)build the tiny-row records of g's schedule now (tiny.py), so no
+    later fused launch has to sync to build them."""
+    from . import tiny
+
+    tiny.tiny_pack(g, refresh=True)
 
 
 SHORT_ROW_MAX = 7  # KGX_SHORT_ROW_MAX (include/kgx.h)
@@ -227,6 +236,7 @@ def transpose(g: CSRGraph) -> CSRGraph:
     t.eid = g.eid[slot].contiguous() if t.kept else g.eid[:0]
     if g.w is not None:
         t.w = g.w[slot].contiguous()
+        _refresh_tiny(t)  # the tiny-row records carry the weights
     t.extras["fwd_slot"] = slot
     g.extras["T"] = t
     return t
@@ -289,6 +299,7 @@ def split_by_part(g: CSRGraph, part_of: torch.Tensor, sources: list, accumulate_
             sub.items = sub.items[: sub.n_items]
             sub.n_long = min(sub.n_long, sub.n_items)
             sub.extras["accumulate_only"] = True
+            _refresh_tiny(sub)
         parts.append(sub)
     return parts
 
@@ -309,6 +320,7 @@ def restrict_rows(g: CSRGraph, row_mask: torch.Tensor) -> CSRGraph:
     sub = replace(g, items=items, split=split, n_items=int(items.shape[0]), n_split=int(split.shape[0]) if g.n_split
                   else 0, extras={"restricted_of": g})
     sub.n_long = short_suffix_start(items)
+    _refresh_tiny(sub)
     return sub
 
 

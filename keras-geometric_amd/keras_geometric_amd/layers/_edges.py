@@ -49,9 +49,14 @@ def graph_for(
                       G.default_split_len(ei.shape[1] + (n_dst if self_loops else 0), n_features))
     src = ei[0].contiguous()
     dst = ei[1].contiguous()
-    return G.cached(
-        key,
-        edge_index_obj,
-        lambda: G.build_csr(src, dst, n_src, n_dst, self_loops=self_loops, gcn_norm=gcn_norm,
-                            segment_only=segment_only, n_features=n_features),
-    )
+
+    def build():
+        g = G.build_csr(src, dst, n_src, n_dst, self_loops=self_loops, gcn_norm=gcn_norm,
+                        segment_only=segment_only, n_features=n_features)
+        if segment_only:
+            # StdAggregator's take(mean, target) raises for ids outside [-n, n)
+            # (aggregators.py:208); decided here, where the build syncs anyway
+            g._take_oob = bool(((dst >= n_dst) | (dst < -n_dst)).any()) if dst.numel() else False
+        return g
+
+    return G.cached(key, edge_index_obj, build)

@@ -61,15 +61,17 @@ def spmm(
     if items is not None and n_split > 0 and reduce != nat.STD:
         partials = torch.empty((n_slots, F), dtype=torch.float32, device=dev)
     n_long = n_items if n_long < 0 or n_long > n_items else n_long
+    # EXACT mode: dynamic row pickup, the hub rows' kernel beside the main one
+    counters = torch.zeros(2, dtype=torch.int32, device=dev) if items is None and reduce != nat.STD else None
     nat.check(
-        nat.lib().kgx_spmm_ex(
+        nat.lib().kgx_spmm_ex2(
             reduce, epilogue, nat.ptr(rowptr), nat.ptr(rows), n_dst,
             nat.ptr(items), n_items, n_long, nat.ptr(split), n_split,
-            nat.ptr(idx), nat.ptr(w), nat.ptr(table), table.stride(0), F,
+            nat.ptr(idx), nat.ptr(w), nat.ptr(table), table.stride(0), None, 0, F,
             nat.ptr(out), out.stride(0),
             nat.ptr(bias), nat.ptr(xroot), xroot.stride(0) if xroot is not None else 0, float(gin_scale),
             nat.ptr(drop_key) if drop_p > 0 else None, float(drop_p), int(drop_seed) & (2**64 - 1),
-            nat.ptr(partials), nat.stream(dev),
+            nat.ptr(partials), nat.ptr(counters), nat.stream(dev),
         ),
         "kgx_spmm",
     )
@@ -128,7 +130,7 @@ def spmm_acc_(
             nat.ptr(idx), nat.ptr(w), nat.ptr(table), table.stride(0), nat.ptr(table2),
             table.shape[0] if table2 is not None else 0, F,
             nat.ptr(out), out.stride(0), nat.ptr(bias), nat.ptr(xroot), xroot.stride(0) if xroot is not None else 0,
-            float(gin_scale), None, 0.0, 0, nat.ptr(partials), nat.stream(dev),
+            float(gin_scale), None, 0.0, 0, nat.ptr(partials), None, nat.stream(dev),
         ),
         "kgx_spmm",
     )

@@ -32,13 +32,19 @@ def tiny_suffix_start(items: torch.Tensor) -> int:
     return int(nz[-1]) + 1 if nz.numel() else 0
 
 
-def tiny_pack(g) -> tuple[Optional[torch.Tensor], Optional[torch.Tensor], int, int]:
+def tiny_pack(g, refresh: bool = False) -> tuple[Optional[torch.Tensor], Optional[torch.Tensor], int, int]:
     """(pack [n, 4] int32, weights [n, 2] float32 or None, n_short_end, n_deg2)
     for graph g's schedule, or (None, None, -1, 0) when the tail is too short
     or disabled (KGX_TINY=0).  The first n_deg2 records have degree 2 (the
-    kernel gathers one edge per row for the rest).  Cached on g."""
+    kernel gathers one edge per row for the rest).  Cached on g; built when
+    the schedule is (graph._build_schedule, refresh=True), where the graph
+    build syncs anyway, so a fused launch never syncs and can be captured
+    into a HIP graph whatever ran on the graph first."""
     cached = getattr(g, "_kgx_tiny", None)
-    if cached is not None:
+    w_now = getattr(g, "w", None)
+    # the records carry the edge weights: a weight tensor assigned after the
+    # schedule was built (sharded / transposed graphs) makes them stale
+    if cached is not None and not refresh and getattr(g, "_kgx_tiny_w", None) is w_now:
         return cached
     res = (None, None, -1, 0)
     items = getattr(g, "items", None)
@@ -55,6 +61,10 @@ def tiny_pack(g) -> tuple[Optional[torch.Tensor], Optional[torch.Tensor], int, i
             last = max(int(g.col.numel()) - 1, 0)
             i0 = beg.clamp(max=last)
             i1 = (beg + (deg > 1).long()).clamp(max=last)
+            if g.col.numel() == 0:  # no edges: no source row to gather; the short-row kernel masks them all
+                res = (None, None, -1, 0)
+                g._kgx_tiny, g._kgx_tiny_w = res, w_now
+                return res
             c0 = torch.where(deg > 0, g.col[i0].long(), torch.zeros_like(deg))
             c1 = torch.where(deg > 0, g.col[i1].long(), torch.zeros_like(deg))
             pack = torch.stack([t[:, 0].long(), deg, c0, c1], 1).to(torch.int32).contiguous()
@@ -71,6 +81,7 @@ def tiny_pack(g) -> tuple[Optional[torch.Tensor], Optional[torch.Tensor], int, i
             res = (pack, tw, start, n2)
     try:
         g._kgx_tiny = res
+        g._kgx_tiny_w = w_now
     except AttributeError:
         pass
     return res

@@ -195,7 +195,14 @@ def _worker(rank, world, chunks, port, q):
             y = layer(torch.from_numpy(x[lo:hi]))  # push-pull halo (the default)
         pp = sg._pp
         assert pp is not None and pp.n_rows == pp.n_pull + pp.n_push == pp.chunks[-1].hi
-        assert pp.merged is not None and pp.merged[1] is not None  # the first step folded into its rows' pass
+        assert pp.merged is not None and pp.merged["step"][1] is not None  # the first step folded into its rows' pass
+        os.environ["KGX_HALO_MERGE"] = "chunk"  # a chunk's steps (pulled rows + partials) merged together
+        try:
+            with torch.no_grad():
+                y_chunk = layer(torch.from_numpy(x[lo:hi]))
+        finally:
+            del os.environ["KGX_HALO_MERGE"]
+        assert pp.merged["chunk"][1] is not None
         os.environ["KGX_HALO_MERGED"] = "0"
         try:
             with torch.no_grad():
@@ -265,7 +272,8 @@ def _worker(rank, world, chunks, port, q):
             y_again = layer(xl)  # the weighted plan is still the one the GCN layer uses
         assert torch.equal(y_again, y)
         q.put((rank, gcn.numpy(), mx.numpy(), sg.n_halo, sum(sg.send_counts), y.numpy(), y_pull.numpy(), pp.n_push,
-               y_tuned.numpy(), y_unfused.numpy(), y_wide.numpy(), y_unmerged.numpy(), ys_gather[0], ys_gather[1]))
+               y_tuned.numpy(), y_unfused.numpy(), y_wide.numpy(), y_unmerged.numpy(), ys_gather[0], ys_gather[1],
+               y_chunk.numpy()))
     finally:
         dist.destroy_process_group()
 
@@ -307,7 +315,7 @@ def test_sharded_equals_unsharded_bitwise(world, chunks):
     # overlapped layer path, push-pull and pull-only halos: own-source part, then
     # one part per halo chunk per row (re-associated sums)
     assert sum(results[r][6] for r in range(world)) > 0  # partial sums were pushed
-    for i in (4, 5, 7, 8, 10, 11, 12):
+    for i in (4, 5, 7, 8, 10, 11, 12, 13):
         y_split = np.concatenate([results[r][i] for r in range(world)])
         err = np.abs(y_split - y) / np.maximum(1, np.abs(y))
         assert err.max() <= 1e-5

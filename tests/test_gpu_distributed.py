@@ -317,11 +317,12 @@ def test_sharded_gin_sage_hip(dev):
         assert err.max() <= 1e-5, (i, err.max())
 
 
-def _run_pipelined_rank(rank, hub, dev, x, out, comm_kind="sync"):
+def _run_pipelined_rank(rank, hub, dev, x, out, comm_kind="sync", exchange="halo"):
     try:
         comm = COMMS[comm_kind](hub, rank)
         sg = kd.ShardedGraph.rmat(N, E, seed=9, device=dev, comm=comm, n_features=F, self_loops=False,
-                                  gcn_norm=False)
+                                  gcn_norm=False, halo_chunks=2)
+        sg.exchange = exchange
         xl = x[sg.lo: sg.lo + sg.n_local]
         res = []
         for layer in (kd.ShardedGINConv(32, sg, mlp_hidden=[48], aggregator="sum", eps_init=0.5),
@@ -334,14 +335,15 @@ def _run_pipelined_rank(rank, hub, dev, x, out, comm_kind="sync"):
                     assert torch.equal(layer(xl), y), "halo buffer reuse across forwards"
             torch.cuda.synchronize()
             res.append((y.cpu().numpy(), layer.conv.get_weights()))
-        out[rank] = (res, sg._pp.n_push, len(sg._pp.chunks))
+        out[rank] = (res, sg._pp.n_push, len(sg._pp.chunks), sg._pp.kind)
     except BaseException as e:
         out[rank] = e
         hub.barrier.abort()
 
 
-@pytest.mark.parametrize("comm", ["sync", "async_delayed"])
-def test_sharded_gin_sage_pipelined_hip(comm, dev):
+@pytest.mark.parametrize("comm,exchange", [("sync", "halo"), ("async_delayed", "halo"), ("sync", "allgather"),
+                                           ("async_delayed", "allgather")])
+def test_sharded_gin_sage_pipelined_hip(comm, exchange, dev):
     """Sharded GIN (sum, mean) and SAGE (mean) on the default path: push-pull
     halo in chunks, own-source kgx_spmm pass, then KGX_EPI_ACCUM passes per
     landed chunk.  Equal to the single-GPU layers within the forward-error
@@ -353,7 +355,8 @@ def test_sharded_gin_sage_pipelined_hip(comm, dev):
     x = torch.randn(N, F, generator=torch.Generator().manual_seed(3)).to(dev)
     hub = ThreadHub(world)
     res = {}
-    threads = [threading.Thread(target=_run_pipelined_rank, args=(r, hub, dev, x, res, comm)) for r in range(world)]
+    threads = [threading.Thread(target=_run_pipelined_rank, args=(r, hub, dev, x, res, comm, exchange))
+               for r in range(world)]
     for t in threads:
         t.start()
     for t in threads:
@@ -361,7 +364,9 @@ def test_sharded_gin_sage_pipelined_hip(comm, dev):
     for r in range(world):
         if isinstance(res.get(r), BaseException):
             raise res[r]
-    assert sum(res[r][1] for r in range(world)) > 0 and all(res[r][2] == 2 for r in range(world))
+    assert all(res[r][2] == 2 and res[r][3] == exchange for r in range(world))
+    if exchange == "halo":
+        assert sum(res[r][1] for r in range(world)) > 0  # partial sums were pushed
     ei = synthetic.rmat_edge_index(N, E, seed=9, device=dev)
     singles = [lambda: kgx.GINConv(32, mlp_hidden=[48], aggregator="sum", eps_init=0.5, exact=True),
                lambda: kgx.GINConv(32, aggregator="mean", eps_init=0.25, exact=True),

@@ -12,7 +12,9 @@ import torch
 
 import keras_geometric_amd as kgx
 from keras_geometric_amd.layers import GATv2Conv, GCNConv, GINConv, MessagePassing, SAGEConv
+from keras_geometric_amd import ops as kops
 from oracle import reference as R
+from oracle.rmat import rmat_edges, scale_for
 
 pytestmark = pytest.mark.gpu
 T = torch.from_numpy
@@ -318,3 +320,30 @@ def test_hip_graph_capture_replay(dev, golden):
         graph.replay()
         torch.cuda.synchronize()
     exact(out, ref.detach().cpu().numpy())
+
+
+def test_hip_graph_capture_graph_warmed_by_unfused_op(dev):
+    """a cached graph first used only by an UNFUSED op (kgx_spmm),
+    then by a fused GCN launch inside a capture: the tiny-row records are built
+    with the schedule, so the fused launch needs no host sync and captures."""
+    from keras_geometric_amd import graph as G
+
+    N, E = 20000, 200000
+    s, d = rmat_edges(41, scale_for(N), N, 0, E)
+    ei = T(np.stack([s, d]).astype(np.int32)).to(dev)
+    x = torch.randn(N, 128, device=dev)
+    g = G.build_csr(ei[0].contiguous(), ei[1].contiguous(), N, N, self_loops=True, gcn_norm=True)
+    W = torch.randn(128, 64, device=dev) / 11.3
+    with torch.no_grad():
+        kops.aggregate(g, x, "sum", weighted=True)  # the unfused op warms the graph
+        assert getattr(g, "_kgx_tiny", None) is not None and g._kgx_tiny[0] is not None
+        ref = kops.aggregate_transform(g, x, W, "sum", weighted=True)
+        s_ = torch.cuda.Stream()
+        s_.wait_stream(torch.cuda.current_stream())
+        torch.cuda.current_stream().wait_stream(s_)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = kops.aggregate_transform(g, x, W, "sum", weighted=True)
+        graph.replay()
+        torch.cuda.synchronize()
+    assert torch.equal(out, ref)

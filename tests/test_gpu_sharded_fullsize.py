@@ -10,7 +10,9 @@ stream behind a spin, so a missing wait reads rows that have not landed).
 Every device operation -- shard generation, shard CSR, push-pull halo plan,
 halo packing, the own-source pass under the exchange, one accumulating pass
 per halo chunk, the node update (GIN's MLP Dense; SAGE's two linear maps +
-bias + ReLU) -- runs through the kgx kernels exactly as with RCCL.
+bias + ReLU) -- runs through the kgx kernels exactly as with RCCL.  C5 runs
+with both exchanges the layer can pick (push-pull halo all-to-all, and the
+all-gather of every rank's rows).
 
 Each rank's rows are compared with the single-GPU layer (rank 0's weights) on
 the whole graph (gin_conv.py:228-300, sage_conv.py:351-439).  The sharded
@@ -36,7 +38,7 @@ from test_gpu_distributed import AsyncThreadComm, ThreadHub
 pytestmark = [pytest.mark.gpu, pytest.mark.slow, pytest.mark.timeout(900)]
 
 
-def _run(world, make_layer, n, e, f, x, seed, chunks):
+def _run(world, make_layer, n, e, f, x, seed, chunks, exchange="halo"):
     hub = ThreadHub(world)
     hub.barrier = threading.Barrier(world, timeout=600)
     res = {}
@@ -46,6 +48,7 @@ def _run(world, make_layer, n, e, f, x, seed, chunks):
             comm = AsyncThreadComm(hub, r, delay_cycles=5_000_000)
             sg = kd.ShardedGraph.rmat(n, e, seed=seed, device=x.device, comm=comm, self_loops=False,
                                       gcn_norm=False, n_features=f, halo_chunks=chunks)
+            sg.exchange = exchange
             xl = x[sg.lo: sg.lo + sg.n_local]
             layer = make_layer(sg)
             with torch.no_grad():
@@ -54,6 +57,7 @@ def _run(world, make_layer, n, e, f, x, seed, chunks):
             torch.cuda.synchronize()
             assert torch.equal(y, y2), "halo buffer reuse across forwards"
             assert sg._pp is not None and sg._pp.n_rows > 0 and len(sg._pp.chunks) == chunks
+            assert sg._pp.kind == exchange
             res[r] = (sg.lo, y, [w.detach().clone() for w in layer.conv.weights], sg._pp.n_push)
         except BaseException as exc:  # surface worker failures in the test thread
             res[r] = exc
@@ -69,7 +73,8 @@ def _run(world, make_layer, n, e, f, x, seed, chunks):
             raise res[r]
         assert r in res, f"rank {r} did not finish"
     assert [res[r][0] for r in range(world)] == kd.equal_bounds(n, world)[:-1]
-    assert sum(res[r][3] for r in range(world)) > 0  # pushed partials were exercised
+    if exchange == "halo":
+        assert sum(res[r][3] for r in range(world)) > 0  # pushed partials were exercised
     return torch.cat([res[r][1] for r in range(world)]), res[0][2]
 
 
@@ -105,10 +110,11 @@ def test_c4_sharded_gin_sum_world8_fullsize(dev):
            x, ei, weights)
 
 
-def test_c5_sharded_sage_mean_world4_fullsize(dev):
+@pytest.mark.parametrize("exchange", ["halo", "allgather"])
+def test_c5_sharded_sage_mean_world4_fullsize(dev, exchange):
     n, e, f, world = 2_449_029, 123_718_280, 100, 4
     x = torch.randn(n, f, device=dev, generator=torch.Generator(device=dev).manual_seed(42))
     got, weights = _run(world, lambda sg: kd.ShardedSAGEConv(f, sg, aggregator="mean"), n, e, f, x, seed=0,
-                        chunks=2)
+                        chunks=2, exchange=exchange)
     ei = synthetic.rmat_edge_index(n, e, seed=0, device=dev)
     _check(got, kgx.SAGEConv(f, aggregator="mean"), kgx.SAGEConv(f, aggregator="mean"), x, ei, weights)

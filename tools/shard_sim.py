@@ -141,6 +141,8 @@ def main():
     ap.add_argument("--exchange", default="halo", help="halo,allgather: exchanges to run")
     ap.add_argument("--push", default="1", help="KGX_HALO_PUSH values to run (0: pull-only halo)")
     ap.add_argument("--merged", default="1", help="KGX_HALO_MERGED values to run (0: round-2 own pass + chunk passes)")
+    ap.add_argument("--merge-unit", default="step", help="KGX_HALO_MERGE values: step, chunk")
+    ap.add_argument("--a-late", default="0", help="KGX_HALO_A_LATE values (1: own-only rows after the merged pass)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--nodes", type=int, default=None)
     ap.add_argument("--edges", type=int, default=None)
@@ -162,13 +164,18 @@ def main():
         t1.record()
         torch.cuda.synchronize()
         cycles_per_ms = 100_000_000 / t0.elapsed_time(t1)
-    runs = [(x, m, p, int(v)) for x in args.exchange.split(",") for m in args.merged.split(",")
-            for p in args.push.split(",") for v in args.chunks.split(",")]
-    for exchange, merged, push, K in runs:
+    runs = [(x, m, p, int(v), mu, al) for x in args.exchange.split(",") for m in args.merged.split(",")
+            for p in args.push.split(",") for v in args.chunks.split(",") for mu in args.merge_unit.split(",")
+            for al in args.a_late.split(",")]
+    for exchange, merged, push, K, unit, a_late in runs:
         if exchange == "allgather" and (push == "0" or merged == "0"):
             continue  # the all-gather has neither pulls nor pushes, and always runs merged
+        if merged == "0" and (unit != "step" or a_late != "0"):
+            continue
         os.environ["KGX_HALO_PUSH"] = push
         os.environ["KGX_HALO_MERGED"] = merged
+        os.environ["KGX_HALO_MERGE"] = unit
+        os.environ["KGX_HALO_A_LATE"] = a_late
         n_local = kd.equal_bounds(n_glob, P)[1]
         comm = LoopbackComm(P, n_local, args.link_gbps, cycles_per_ms)
         gcn = layer_kind == "gcn"
@@ -207,7 +214,8 @@ def main():
         print(json.dumps({
             "config": args.config, "layer": layer_kind, "scaling": scaling, "nodes": n_glob, "edges": e_glob,
             "features": F, "world": P, "exchange": pp.kind if pp else "pull", "chunks": K,
-            "push_pull": pp is not None and pp.kind == "halo", "merged": merged == "1",
+            "push_pull": pp is not None and pp.kind == "halo", "merged": merged == "1", "merge_unit": unit,
+            "a_late": a_late == "1",
             "link_gbps": args.link_gbps, "step_ms": round(t0.elapsed_time(t1) / args.steps, 3),
             "launch_ms": [round(v, 3) for v in launch_ms],
             "own_edges": g_own.kept, "chunk_edges": [g.kept for g in g_chunks],
