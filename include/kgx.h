@@ -175,11 +175,13 @@ int kgx_spmm_ex(int reduce, int epilogue, const int32_t* rowptr, const int32_t* 
  * reduce a row's own-source and halo edges in one pass (distributed.py).
  * table2 NULL: kgx_spmm_ex.
  * counters (EXACT mode, items NULL): two caller-owned int32, zeroed before the
- * call, from which the launch hands out rows dynamically; the hub-row kernel
- * then runs on a library-owned forked stream beside the main kernel and is
- * joined back into `stream` before the call's last launch (bit-identical
- * results: every row is still reduced by one lane chain in CSR order,
- * aggregators.py:126-137).  NULL: the static schedule, one stream. */
+ * call, from which the hub-row kernel (rows of >= 2048 edges) hands out its
+ * (row, column group) items dynamically, so its blocks balance instead of
+ * waiting behind the largest row (bit-identical results: every row is still
+ * reduced by one lane chain in CSR order, aggregators.py:126-137).  NULL: the
+ * static schedule.  (KGX_EXACT_FORK=1, an experiment: the hub kernel also
+ * forks onto a library-owned stream beside the main kernel, whose rows are
+ * then handed out from counters[1]; joined back into `stream`.) */
 int kgx_spmm_ex2(int reduce, int epilogue, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
                  const int32_t* items, int64_t n_items, int64_t n_long_items, const int32_t* split, int64_t n_split,
                  const int32_t* idx, const float* w, const float* table, int64_t ld_table, const float* table2,

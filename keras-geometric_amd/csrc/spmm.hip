@@ -65,10 +65,11 @@ struct SpmmArgs {
   // table (same ld_t); t2b = table2 - n_t1 * ld_t as an address.  n_t1 = INT32_MAX: one table.
   const float* t2b;
   int32_t n_t1;
-  // EXACT mode, dynamic row pickup (kgx_spmm_ex2 counters): dyn[0] hands out the
-  // hub kernel's (row, column group) items, dyn[1] spmm_kernel's row batches.
-  // NULL: the static grid-stride schedule.
+  // EXACT mode, dynamic pickup (kgx_spmm_ex2 counters): dyn[0] hands out the hub
+  // kernel's (row, column group) items; with dyn_rows, dyn[1] hands out
+  // spmm_kernel's row batches.  NULL: the static grid-stride schedule.
   int32_t* dyn;
+  int dyn_rows;
 };
 
 // Source row of column c: table[c], or with TWO table2[c - n_t1] (a separate
@@ -220,8 +221,12 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
   // from a counter (lane 0's atomic, broadcast to the group), so groups whose
   // blocks started late -- behind the hub kernel running beside this one --
   // take less, and the launch ends together.  Otherwise: static grid-stride.
-  const bool dyn = a.dyn != nullptr && !a.items;
-  constexpr int kDynRows = 8;
+  const bool dyn = a.dyn != nullptr && a.dyn_rows && !a.items;
+  // rows per grab (the KGX_EXACT_FORK experiment, see launch_main)
+#ifndef KGX_DYN_ROWS
+#define KGX_DYN_ROWS 8
+#endif
+  constexpr int kDynRows = KGX_DYN_ROWS;
   const int64_t gid = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> a.lgG;
   int64_t it = gid, batch_end = 0;
   if (dyn) it = batch_end = 0;
@@ -839,7 +844,17 @@ int launch_main(const SpmmArgs& a_in, hipStream_t s) {
       else if (gh == 8) kh = spmm_hub_kernel<8, RED, W>;
       const int64_t work = a.n_rows * ((a.F + 4 * gh - 1) / (4 * gh));
       const int64_t nb = work < cu_count() ? work : cu_count();  // one resident block per CU
-      if (a.dyn) {
+      // Experiment (KGX_EXACT_FORK=1, off by default): the hub kernel forked
+      // beside spmm_kernel, whose rows are then handed out dynamically.
+      // Measured slower at NS: contiguous row batches of the
+      // degree-descending list concentrate the heaviest rows on single groups
+      // (8 / 32 / 256-row batches: 12.7 / 15.0 / 65 ms against 10.9 static).
+      static const bool fork_on = [] {
+        const char* h = getenv("KGX_EXACT_FORK");
+        return h && atoi(h) == 1;
+      }();
+      a.dyn_rows = fork_on ? 1 : 0;
+      if (a.dyn && fork_on) {
         // dynamic pickup: the hub kernel runs on a forked stream BESIDE spmm_kernel
         // (which skips the hub rows and takes its rows from a counter), so the CUs
         // the hub kernel's tail leaves idle -- its largest row alone is ~1 ms at
@@ -1068,6 +1083,10 @@ extern "C" int kgx_spmm_ex2(int reduce, int epilogue, const int32_t* rowptr, con
     s.xroot = xroot ? xroot + c0 : nullptr;
     s.partials = partials ? partials + c0 : nullptr;
     s.f_base = int(c0);
+    if (s.dyn && c0 > 0 && hipMemsetAsync(s.dyn, 0, 2 * sizeof(int32_t), stream) != hipSuccess) {
+      set_error("kgx_spmm: counter reset failed");  // each column slice hands its rows out again
+      return KGX_ERR_HIP;
+    }
     int rc;
     if (VEC == 4) rc = dispatch_nt<4>(nt, reduce, s, stream);
     else if (VEC == 2) rc = dispatch_nt<2>(nt, reduce, s, stream);

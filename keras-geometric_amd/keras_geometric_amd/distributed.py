@@ -323,6 +323,7 @@ class ShardedGraph:
     halo_k: int | None = None  # exchange chunk count chosen by tune_exchange (or fixed)
     tuning: dict | None = None  # K (or "exchange:K") -> slowest rank's forward seconds
     exchange: str | None = None  # "halo" / "allgather"; None: not chosen yet (push-pull halo until tuned)
+    merge_unit: str | None = None  # merged_passes' unit ("step" / "chunk" / "none"); None: KGX_HALO_MERGE or "step"
 
     @property
     def lo(self) -> int:
@@ -639,30 +640,36 @@ class ShardedGraph:
             return self.allgather_plan(n_chunks or self.halo_k or len(self.chunks), weighted)
         return self.push_pull_plan(n_chunks, weighted)
 
-    def exchange_candidates(self, feature_bytes: int, halo_ks=(1, 2, 4, 8), gather_ks=(1, 2, 4)) -> list:
-        """(kind, K) pairs worth timing: the push-pull halo at each K, and the
-        all-gather when its table is at most 4x the pull-only halo's bytes
-        (weak-scaled shards, whose halo is a small part of the global graph,
-        skip it without a run)."""
+    def exchange_candidates(self, feature_bytes: int, halo_ks=(1, 2, 4), gather_ks=(1, 2, 4),
+                            units=("step", "chunk", "none")) -> list:
+        """(exchange, K, merge unit) triples worth timing: the push-pull halo at
+        each K and merge unit (merged_passes), and the all-gather when its table
+        is at most 4x the pull-only halo's bytes (weak-scaled shards, whose halo
+        is a small part of the global graph, skip it without a run).
+        KGX_EXCHANGE / KGX_HALO_MERGE restrict the set."""
         fixed = os.environ.get("KGX_EXCHANGE")
-        cands = [("halo", k) for k in halo_ks]
-        gather_rows = self.n_global
-        if fixed == "allgather" or (fixed is None and gather_rows <= 4 * max(self.n_halo, 1)):
-            cands += [("allgather", k) for k in gather_ks]
-        if fixed == "allgather":
-            cands = [c for c in cands if c[0] == "allgather"]
+        fixed_unit = os.environ.get("KGX_HALO_MERGE")
+        units = (fixed_unit,) if fixed_unit else units
+        cands = [("halo", k, u) for k in halo_ks for u in units]
+        if fixed == "allgather" or (fixed is None and self.n_global <= 4 * max(self.n_halo, 1)):
+            # one step per all-gather chunk: "step" and "chunk" coincide
+            cands += [("allgather", k, u) for k in gather_ks for u in units if u != "chunk"]
+        if fixed:
+            cands = [c for c in cands if c[0] == fixed]
         return cands
 
     def tune_exchange(self, run, candidates) -> tuple:
-        """Choose (exchange, K) by timing one forward per candidate (`run(kind,
-        K)`; the plan is built before its timed call), best of two; every rank
-        times the same candidates and the slowest rank's time counts (one
-        all-to-all of the times).  Like a library autotuner: the best choice
-        depends on the links' rate, which only the machine knows."""
+        """Choose (exchange, K, merge unit) by timing one forward per candidate
+        (`run(kind, K)`, with the candidate installed; the plan is built before
+        its timed call), best of two; every rank times the same candidates and
+        the slowest rank's time counts (one all-to-all of the times).  Like a
+        library autotuner: the best choice depends on the links' rate, which
+        only the machine knows (tools/shard_sim.py: exchange-free, merging a
+        chunk's steps wins; with 400 GB/s links, merging only its pulled rows)."""
         dev = self.graph.col.device
         times = []
-        for kind, K in candidates:
-            self.exchange, self.halo_k = kind, K
+        for kind, K, unit in candidates:
+            self.exchange, self.halo_k, self.merge_unit = kind, K, unit
             self.exchange_plan(K)
             best = float("inf")
             for _ in range(2):
@@ -679,8 +686,8 @@ class ShardedGraph:
         self.comm.all_to_all_single(every, t.repeat(self.world).contiguous())
         worst = every.view(self.world, -1).max(0).values.cpu()
         i = int(torch.argmin(worst))
-        self.exchange, self.halo_k = candidates[i]
-        self.tuning = {f"{kind}:{K}": float(v) for (kind, K), v in zip(candidates, worst)}
+        self.exchange, self.halo_k, self.merge_unit = candidates[i]
+        self.tuning = {f"{kind}:{K}:{unit}": float(v) for (kind, K, unit), v in zip(candidates, worst)}
         self.exchange_plan(self.halo_k)
         return candidates[i]
 
@@ -690,7 +697,8 @@ class ShardedGraph:
 
         Groups: unit "step" (default; KGX_HALO_MERGE=step) -- every exchange
         step on its own (chunk k's pulled rows, then its pushed partials);
-        "chunk" -- a chunk's steps together.  H = the local rows with an edge in
+        "chunk" -- a chunk's steps together; "none" -- nothing merged: the own
+        pass writes every row and each step accumulates (step granularity).  H = the local rows with an edge in
         the first group.  g_a: the own-source CSR restricted to the rows NOT in
         H -- it writes them, while the exchange is in flight.  g_b: for the rows
         in H, their own-source edges followed by their first-group edges
@@ -701,7 +709,7 @@ class ShardedGraph:
         accumulate-only over the rows each touches.  Each row's sum is own
         edges, then first-group edges, then later groups: a re-association of
         the one-pass order, tolerance-equal like the rest of this path."""
-        unit = unit or os.environ.get("KGX_HALO_MERGE", "step")
+        unit = unit or self.merge_unit or os.environ.get("KGX_HALO_MERGE", "step")
         if pp.merged is None:
             pp.merged = {}
         if unit in pp.merged:
@@ -711,6 +719,12 @@ class ShardedGraph:
         dev = g_own.col.device
         steps = [st for c in pp.chunks for st in c.steps]
         groups, idx = [], 0
+        if unit == "none":  # nothing merged: the own pass over every row, then every step accumulates
+            for i, g in enumerate(pp.step_parts or []):
+                if g.kept:
+                    groups.append((i, g, steps[i].lo, steps[i].hi))
+            pp.merged[unit] = (g_own, None, groups, -1)
+            return pp.merged[unit]
         if unit == "chunk":
             for k, c in enumerate(pp.chunks):
                 idx += len(c.steps)

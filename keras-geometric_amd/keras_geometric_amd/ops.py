@@ -27,6 +27,9 @@ def _f32c(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     return t.contiguous()
 
 
+_EXACT_DYN = __import__("os").environ.get("KGX_EXACT_DYN", "1") != "0"
+
+
 @torch.library.custom_op("kgx::spmm", mutates_args=())
 def spmm(
     table: torch.Tensor,
@@ -61,8 +64,9 @@ def spmm(
     if items is not None and n_split > 0 and reduce != nat.STD:
         partials = torch.empty((n_slots, F), dtype=torch.float32, device=dev)
     n_long = n_items if n_long < 0 or n_long > n_items else n_long
-    # EXACT mode: dynamic row pickup, the hub rows' kernel beside the main one
-    counters = torch.zeros(2, dtype=torch.int32, device=dev) if items is None and reduce != nat.STD else None
+    # EXACT mode: the hub-row kernel hands its items out dynamically (KGX_EXACT_DYN=0: static, A/B only)
+    counters = (torch.zeros(2, dtype=torch.int32, device=dev)
+                if items is None and reduce != nat.STD and _EXACT_DYN else None)
     nat.check(
         nat.lib().kgx_spmm_ex2(
             reduce, epilogue, nat.ptr(rowptr), nat.ptr(rows), n_dst,

@@ -226,10 +226,12 @@ def _worker(rank, world, chunks, port, q):
             layer2.bias.copy_(torch.from_numpy(b))
         with torch.no_grad():
             y_tuned = layer2(torch.from_numpy(x[lo:hi]))
-        # every candidate timed: the push-pull halo at K = 1 / 2 / 4 / 8 and (this small
-        # graph's remote sources cover most rows) the all-gather at K = 1 / 2 / 4
-        assert sorted(sg2.tuning) == sorted([f"halo:{k}" for k in (1, 2, 4, 8)] + [f"allgather:{k}" for k in (1, 2, 4)])
-        assert sg2.exchange in ("halo", "allgather") and sg2.halo_k in (1, 2, 4, 8)
+        # every candidate timed: the push-pull halo at K = 1 / 2 / 4 with each merge unit and
+        # (this small graph's remote sources cover most rows) the all-gather at K = 1 / 2 / 4
+        units = ("step", "chunk", "none")
+        assert sorted(sg2.tuning) == sorted([f"halo:{k}:{u}" for k in (1, 2, 4) for u in units]
+                                            + [f"allgather:{k}:{u}" for k in (1, 2, 4) for u in ("step", "none")])
+        assert sg2.exchange in ("halo", "allgather") and sg2.halo_k in (1, 2, 4) and sg2.merge_unit in units
         assert len(sg2._pp.chunks) == sg2.halo_k and sg2._pp.kind == sg2.exchange
         # the all-gather exchange on its own (K = 1 and 3), within the tolerance of the reference
         ys_gather = []

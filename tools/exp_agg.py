@@ -95,6 +95,21 @@ def ns_once(n=10_000_000, e=100_000_000, f=128, split=512):
                       "TBps_alg": b_alg(n, g.kept, f) / ms / 1e9}), flush=True)
 
 
+def exact_once(n=10_000_000, e=100_000_000, f=128):
+    """NS EXACT-mode weighted aggregation (hub rows + dynamic row pickup; env
+    knobs KGX_EXACT_FORK, KGX_HUB apply)."""
+    import os
+
+    dev = torch.device("cuda", 0)
+    ei = synthetic.rmat_edge_index(n, e, seed=0, device=dev)
+    h = torch.randn(n, f, device=dev)
+    g = G.build_csr(ei[0].contiguous(), ei[1].contiguous(), n, n, self_loops=True, gcn_norm=True)
+    ms = timeit(lambda: kops.aggregate(g, h, "sum", weighted=True, exact=True), reps=10)
+    print(json.dumps({"lib": os.path.basename(os.environ.get("KGX_LIB", "libkgx.so")),
+                      "fork": os.environ.get("KGX_EXACT_FORK", "1"), "exact_ms": round(ms, 4),
+                      "TBps_alg": round(b_alg(n, g.kept, f) / ms / 1e9, 3)}), flush=True)
+
+
 def ns_both(n=10_000_000, e=100_000_000, f=128):
     """NS timing of the unfused weighted aggregation and the fused GCN kernel
     with the library named by KGX_LIB (used by `ab`)."""
@@ -163,4 +178,5 @@ if __name__ == "__main__":
     if sys.argv[1] == "ab":
         ab(sys.argv[2:])
     else:
-        {"sweep": sweep, "calib": calib, "ns": ns_once, "both": ns_both, "gat": gat_once}[sys.argv[1]]()
+        {"sweep": sweep, "calib": calib, "ns": ns_once, "both": ns_both, "gat": gat_once,
+         "exact": exact_once}[sys.argv[1]]()
