@@ -1,5 +1,5 @@
 # kgx_dense A/B: GPU dense tests on the main library, then bench_dense.py per library, interleaved.
-# usage: bash tools/gpu_dense_ab.sh variant1 [variant2 ...]   (main library always included)
+# usage: bash tools/gpu_jobs/gpu_dense_ab.sh variant1 [variant2 ...]   (main library always included)
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_gpu_dense.py -x -q --timeout 200 --timeout-method thread > gpurun_out/dense_tests.log 2>&1 || exit $?

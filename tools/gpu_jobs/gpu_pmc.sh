@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes (one counter group per rocprofv3 run) over `exp_agg.py both`
-# (NS unfused spmm + fused GCN kernel).  Usage: bash tools/gpu_pmc.sh
+# (NS unfused spmm + fused GCN kernel).  Usage: bash tools/gpu_jobs/gpu_pmc.sh
 set -o pipefail
 cd "$(dirname "$0")/.." || exit 1
 mkdir -p gpurun_out/pmc

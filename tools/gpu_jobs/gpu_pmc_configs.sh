@@ -1,6 +1,6 @@
 # rocprofv3 kernel stats + PMC traffic (FETCH_SIZE, WRITE_SIZE; separate passes) for
 # the dominant kernels of C3 (gatv2_kernel), C4 (spmm_kernel F256, dense_kernel 256->256)
-# and C5 (spmm_kernel F100, dense_kernel (100+100)->100).  Usage: bash tools/gpu_pmc_configs.sh c3 c4 c5
+# and C5 (spmm_kernel F100, dense_kernel (100+100)->100).  Usage: bash tools/gpu_jobs/gpu_pmc_configs.sh c3 c4 c5
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/prof

@@ -1,5 +1,5 @@
 # Short-row fused kernel: variants / debug decomposition (tools/exp_short.py).
-# usage: bash tools/gpu_short_ab.sh lib[:DEBUG] ...
+# usage: bash tools/gpu_jobs/gpu_short_ab.sh lib[:DEBUG] ...
 set -o pipefail
 mkdir -p gpurun_out
 for spec in "$@"; do

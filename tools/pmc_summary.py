@@ -13,7 +13,7 @@ calibration in tools/exp_agg.py `calib`.
 WRITE_SIZE is exact for 16-B-per-lane stores.
 
 Every kernel entry carries a hash of ITS sources: the .hip file that defines
-it plus the headers that file includes (kernel_source_hash); bench.py attaches
+it plus the csrc/ headers that file includes (kernel_source_hash); bench.py attaches
 the traffic only when the hash of each kernel it reports matches the sources
 it runs, so a stale profile is never reported against a changed kernel, and an
 edit to an unrelated kernel's file does not invalidate it.
@@ -33,7 +33,6 @@ ROOT = Path(__file__).resolve().parents[1]
 CSRC = ROOT / "keras-geometric_amd" / "csrc"
 
 
-INCLUDE = ROOT / "include"
 
 
 def source_hash() -> str:
@@ -48,15 +47,15 @@ def source_hash() -> str:
 
 
 def _closure(path: Path, seen: set) -> None:
-    """path and the local headers it includes, transitively."""
+    """path and the kernel-side headers it includes (csrc/), transitively.  The
+    public ABI header include/kgx.h is left out: its declarations and comments
+    change with the boundary, not with the kernels' code."""
     if path in seen or not path.exists():
         return
     seen.add(path)
     for inc in re.findall(r'#include\s+"([^"]+)"', path.read_text()):
-        for d in (path.parent, CSRC, INCLUDE):
-            if (d / inc).exists():
-                _closure(d / inc, seen)
-                break
+        if (CSRC / inc).exists():
+            _closure(CSRC / inc, seen)
 
 
 def kernel_file(kernel: str) -> Path | None:
