@@ -635,8 +635,9 @@ class ShardedGraph:
         return self._pp
 
     def exchange_plan(self, n_chunks: int | None = None, weighted: bool | None = None) -> PushPullPlan:
-        """The plan of the chosen exchange ("halo": push-pull all-to-all; "allgather")."""
-        if self.exchange == "allgather":
+        """The plan of the chosen exchange ("halo": push-pull all-to-all; "allgather";
+        not chosen yet: KGX_EXCHANGE, else the halo)."""
+        if (self.exchange or os.environ.get("KGX_EXCHANGE", "halo")) == "allgather":
             return self.allgather_plan(n_chunks or self.halo_k or len(self.chunks), weighted)
         return self.push_pull_plan(n_chunks, weighted)
 
