@@ -184,9 +184,13 @@ class sharing_gpu:
 
 def _tiny_abi(items, n_items, n_long, tpack, tw, n_short_end, n_tiny2):
     """(n_short_end, tpack, tw, n_tiny2) arguments of kgx_spmm_gemm_ex2."""
-    if items is None or tpack is None or not (n_long <= n_short_end <= n_items) \
-            or tpack.shape[0] != n_items - n_short_end:
+    if items is None or tpack is None or not (n_long <= n_short_end <= n_items):
         return n_items, None, None, 0
+    from . import tiny
+
+    if tpack.numel() != tiny.pack_numel(n_items - n_short_end, n_tiny2):
+        raise ValueError(f"tiny records: {tpack.numel()} ints for a tail of {n_items - n_short_end} rows "
+                         f"({n_tiny2} of degree 2) -- stale or foreign pack (tiny.py)")
     return n_short_end, tpack, tw, n_tiny2
 
 

@@ -116,3 +116,25 @@ def test_gatv2_softmax_convexity_c3(dev):
     a = kops.gatv2_aggregate(g, hr, hr, att, H, C, 0.2)
     b = kops.gatv2_aggregate(g, hr, hr, att, H, C, 0.2, exact=True)
     assert ((a - b).abs() / b.abs().clamp_min(1.0)).max().item() <= 1e-5
+
+
+def test_tiny_tail_bit_identical_fullsize(big):
+    """The degree <= 2 tail on packed records (spmm_gemm_tiny_kernel) against
+    the same launch with the tail on the short-row kernel, at the north-star
+    size (thousands of tiles per block, where a pipeline or hand-off race
+    would show): bit-identical for the weighted sum and the unweighted max."""
+    _, g, x = big
+    gen = torch.Generator(device=x.device).manual_seed(7)
+    W = torch.randn(F, F, device=x.device, generator=gen) * (1.0 / F) ** 0.5
+    b = torch.randn(F, device=x.device, generator=gen)
+    saved = g._kgx_tiny
+    assert saved[0] is not None
+    for red, weighted in (("sum", True), ("max", False)):
+        y_tiny = kops.aggregate_transform(g, x, W, red, weighted=weighted, bias=b)
+        g._kgx_tiny = (None, None, -1, 0)
+        try:
+            y_short = kops.aggregate_transform(g, x, W, red, weighted=weighted, bias=b)
+        finally:
+            g._kgx_tiny = saved
+        assert torch.equal(y_tiny, y_short), red
+        del y_tiny, y_short

@@ -29,8 +29,9 @@ def _with_tiny(g):
     if hasattr(g, "_kgx_tiny"):
         del g._kgx_tiny
     pack, tw, start, n2 = tiny.tiny_pack(g)
-    assert pack is not None and pack.shape[0] > 4096 and 0 < n2 < pack.shape[0]
-    deg = pack[:, 1].cpu().numpy()
+    n = g.n_items - start
+    assert pack is not None and n > 4096 and 0 < n2 < n
+    deg = tiny.records(pack, tw, n, n2)[0][:, 1].cpu().numpy()
     assert (deg[:n2] == 2).all() and (deg[n2:] <= 1).all()
 
 
@@ -73,6 +74,34 @@ def test_tiny_tail_variants_bit_identical(dev):
         res[on] = r
     for k in res[False]:
         torch.testing.assert_close(res[True][k], res[False][k], rtol=0, atol=0, msg=k)
+
+
+def test_tiny_records_are_read(dev):
+    """The fused launch really takes the tail from the records: scaling the
+    packed one-edge weights (not the graph's) changes exactly those rows."""
+    g, _ = _graph(dev, self_loops=True, gcn_norm=True)
+    _with_tiny(g)
+    gen = torch.Generator(device=dev).manual_seed(6)
+    x = torch.randn(g.rowptr.numel() - 1, 128, device=dev, generator=gen)
+    W = torch.randn(128, 128, device=dev, generator=gen) * 0.1
+    y0 = kops.aggregate_transform(g, x, W, "sum", weighted=True)
+    pack, tw, start, n2 = g._kgx_tiny
+    n = g.n_items - start
+    rec, _ = tiny.records(pack, tw, n, n2)
+    off = 2 * n2 + (-(2 * n2) % 4)
+    tw2 = tw.clone()
+    tw2[off:off + n - n2] *= 2.0
+    tw2[:2 * n2] *= 2.0
+    g._kgx_tiny = (pack, tw2, start, n2)
+    y1 = kops.aggregate_transform(g, x, W, "sum", weighted=True)
+    tail_rows = rec[:, 0][rec[:, 1] > 0].long()
+    changed = (y1 != y0).any(1)
+    assert bool(changed[tail_rows].float().mean() > 0.99)
+    mask = torch.ones_like(changed)
+    mask[rec[:, 0].long()] = False
+    assert not bool(changed[mask].any())
+    torch.testing.assert_close(y1[tail_rows], 2 * y0[tail_rows], rtol=1e-5, atol=1e-5)
+    g._kgx_tiny = (pack, tw, start, n2)
 
 
 def test_tiny_tail_gcn_vs_oracle(dev):

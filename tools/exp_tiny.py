@@ -63,8 +63,64 @@ def main(n=10_000_000, e=100_000_000, f=128, weighted=True, red=0):
     err = ((out_a - out_b).abs() / out_a.abs().clamp_min(1.0)).max().item()
     t_a = timeit(lambda: call(out_a, False))
     t_b = timeit(lambda: call(out_b, True))
-    deg = (pack[:, 1]).long()
-    print(json.dumps({"weighted": weighted, "red": red, "tiny_rows": int(pack.shape[0]), "tiny_start": start,
+    rec = tiny.records(pack, tw, g.n_items - start, n2)[0]
+    deg = rec[:, 1]
+    if err > 1e-5:  # where the two paths differ: position in the tail, degree
+        row_err = ((out_a - out_b).abs() / out_a.abs().clamp_min(1.0)).amax(1)
+        bad = row_err[rec[:, 0].long()] > 1e-5
+        pos = torch.nonzero(bad).flatten()
+        outside = int((row_err > 1e-5).sum()) - int(bad.sum())
+        print(json.dumps({"bad_tail_rows": int(bad.sum()), "bad_rows_outside_tail": outside,
+                          "bad_by_degree": {d: int((bad & (deg == d)).sum()) for d in (0, 1, 2)},
+                          "first_bad_pos": pos[:12].tolist(), "last_bad_pos": pos[-4:].tolist(),
+                          "n2": n2, "tail": int(deg.numel())}), flush=True)
+        # run to run: rows never written (NaN-prefilled) and rows that differ between runs
+        runs = []
+        for _ in range(3):
+            o = torch.full_like(out_b, float("nan"))
+            call(o, True)
+            torch.cuda.synchronize()
+            runs.append(o)
+        nan_rows = [int(torch.isnan(o).any(1).sum()) for o in runs]
+        diff01 = int((runs[0] != runs[1]).any(1).sum())
+        rows = rec[:, 0].long()
+        info = []
+        for p in pos[:6].tolist():
+            r = int(rows[p])
+            got = runs[0][r]
+            cand = {}
+            for d in (-2 * 64 * 256, -64 * 256, -64, -4, -1, 1, 4, 64, 64 * 256, 2 * 64 * 256):
+                q = p + d
+                if 0 <= q < rows.numel():
+                    cand[d] = bool(torch.equal(got, out_a[int(rows[q])]))
+            info.append({"pos": p, "row": r, "nan": bool(torch.isnan(got).any()), "equals_row_at_offset": cand,
+                         "col": int(rec[p, 2]), "w_pack": float(tiny.records(pack, tw, g.n_items - start, n2)[1][p, 0])})
+        print(json.dumps({"nan_rows_per_run": nan_rows, "rows_differing_run0_run1": diff01, "bad": info}), flush=True)
+        # which aggregate did the MFMA side see?  out = agg @ W + b, so agg = (out - b) W^-1;
+        # compare per feature with the row's own aggregate and with rows of nearby tile slots
+        Winv = torch.linalg.inv(W.double())
+        run_bad = ((runs[0] - out_a).abs() / out_a.abs().clamp_min(1.0)).amax(1)[rows] > 1e-5
+        grid = 256
+        for p in torch.nonzero(run_bad).flatten()[:4].tolist():
+            r = int(rows[p])
+            agg = (runs[0][r].double() - b.double()) @ Winv
+            ref = torch.zeros(f, dtype=torch.float64, device=dev)
+            ref[:] = out_a[r].double() - b.double()
+            ref = ref @ Winv
+            wrong = ((agg - ref).abs() > 1e-3 * ref.abs().clamp_min(1.0)).nonzero().flatten()
+            t0 = (p - n2) // 64
+            best = []
+            for tt in range(t0 - 3 * grid, t0 + 2 * grid, grid):
+                for s_ in range(64):
+                    q = n2 + tt * 64 + s_
+                    if q < n2 or q >= rows.numel() or q == p or wrong.numel() == 0:
+                        continue
+                    cand = ((out_a[int(rows[q])].double() - b.double()) @ Winv)[wrong]
+                    if bool(((cand - agg[wrong]).abs() < 1e-3 * cand.abs().clamp_min(1.0)).all()):
+                        best.append({"tile_delta": (tt - t0) // grid, "slot": s_})
+            print(json.dumps({"pos": p, "slot": (p - n2) % 64, "tile": t0, "n_wrong_features": int(wrong.numel()),
+                              "wrong_features": wrong[:32].tolist(), "wrong_equal_to": best[:6]}), flush=True)
+    print(json.dumps({"weighted": weighted, "red": red, "tiny_rows": int(deg.numel()), "tiny_start": start,
                       "n_long": g.n_long, "n_items": g.n_items, "deg0": int((deg == 0).sum()),
                       "deg1": int((deg == 1).sum()), "deg2": int((deg == 2).sum()), "max_rel_err": err,
                       "ms_short_path": round(t_a, 3), "ms_tiny_path": round(t_b, 3)}), flush=True)
