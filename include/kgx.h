@@ -241,15 +241,10 @@ int kgx_spmm_gemm_ex(int reduce, const int32_t* rowptr, const int32_t* rows, int
 
 /* kgx_spmm_gemm_ex2: kgx_spmm_gemm_ex with the schedule's tail of rows of degree
  * <= 2 ([n_short_end, n_items)) taken from packed records instead of the item
- * list (degree-descending: n_tiny_deg2 rows of degree 2, then n1 = n_items -
- * n_short_end - n_tiny_deg2 rows of degree <= 1), both 16-byte aligned:
- *   tiny_pack: n_tiny_deg2 x {row, degree, col0, col1} (col1 = col0 below
- *              degree 2, any valid source for degree 0), then ceil(n1 / 256) * 256 x
- *              {code, col0}: code = row for degree 1, -2 - row for degree 0
- *              (col0 any valid source), padding {-1, 0};
- *   tiny_w (when w is given): n_tiny_deg2 x {w0, w1}, then from float
- *              ceil(2 n_tiny_deg2 / 4) * 4 one weight per degree <= 1 row (padding 0).
- * Built once per graph (tiny.py; tiny.records() unpacks it).  Items
+ * list: tiny_pack[n_items - n_short_end][4] = {row, degree, col0, col1} (col1 =
+ * col0 for degree 1, both any valid source for degree 0) and, when w is given,
+ * tiny_w[..][2] = {w0, w1}; the first n_tiny_deg2 records have degree 2 (the
+ * rest <= 1: degree-descending order).  Built once per graph (tiny.py).  Items
  * [n_long_items, n_short_end) go to the short-row kernel as before.  tiny_pack
  * NULL: n_short_end must equal n_items.  Same boundary as kgx_spmm_gemm
  * (gcn_conv.py:233-272, aggregators.py:56-167). */

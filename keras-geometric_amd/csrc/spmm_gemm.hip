@@ -642,8 +642,7 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
 //    rows into the bf16 planes of one of two LDS tiles.  Their loads run two
 //    tiles ahead: while tile t is folded, tile t+1's rows and tile t+2's
 //    records are in flight (all loads unconditional, so hipcc's vmcnt counts
-//    stay exact and it never drains the queue).  The degree <= 1 rest reads
-//    compact records and runs a tile deeper (tiny1_producer);
+//    stay exact and it never drains the queue);
 //  - MFMA waves 0..7 hold W's split fragments (16 output columns each), take
 //    the other tile and store their results straight from the accumulators.
 // One barrier per tile hands a tile from producers to MFMA waves.
@@ -658,96 +657,6 @@ constexpr int kTinyGroups = 16;  // producer row groups
 #endif
 template <int NG>
 constexpr int tiny_rows() { return kTinyGroups * (NG == 1 ? KGX_TINY_RPG1 : KGX_TINY_RPG); }
-
-// Producer side of the degree <= 1 rest (NG = 1).  Its records are compact
-// (tiny.py): {code, col0} with code = row (degree 1), -2 - row (degree 0, col0
-// any valid source) or -1 (padding), and one weight per row, the arrays padded
-// to whole tiles.  8 registers per tile of records instead of 24 (and the
-// weights loaded with the rows) buy a second tile of row gathers in flight: at
-// iteration i the producers issue tile i+3's records, tile i+2's rows and
-// weights, then fold tile i, so a row load has two tile periods to land (the
-// one-edge rows are pure latency: one 512-byte row per record, and one tile in
-// flight per CU covered ~32 KiB of the ~64 KiB the HBM latency needs).  Group
-// g takes tile rows g + 16 j, as the two-edge path.  Tile and loop indices are
-// 32-bit so every bound test is a scalar compare: a 64-bit compare is a VALU
-// op whose temporary VGPR pair, reused from a pending load's destination, made
-// hipcc drain the whole load queue (vmcnt(0)) once per loop trip.  Same folds
-// as the two-edge path: init, combine(msg(w0 * x[col0])) if degree 1, finish.
-template <class R, bool WEIGHTED, int RPG, int ROWS, bool TWO, class Store>
-__device__ __forceinline__ void tiny1_producer(const FusedArgs& a, int g, int f, int32_t n_tiles, int32_t my_tiles,
-                                               Store& store) {
-  static_assert(256 % ROWS == 0 && ROWS == kTinyGroups * RPG, "tiles must divide the 256-row padding");
-  typedef float f4 __attribute__((ext_vector_type(4)));
-  const int2* recs = reinterpret_cast<const int2*>(a.tpack);
-  const float* ws = reinterpret_cast<const float*>(a.tw);
-  struct Rec {
-    int2 p[RPG];  // {code, col0}
-  };
-  struct Rows {
-    f4 v[RPG];
-    float w[RPG];
-  };
-  // tile k's first record (tiles past the block's range re-read its last one: never stored)
-  auto first = [&](int32_t k) {
-    const int32_t t = int32_t(blockIdx.x) + k * int32_t(gridDim.x);
-    return int64_t(t < n_tiles ? t : n_tiles - 1) * ROWS + g;
-  };
-  auto rec = [&](int32_t k, Rec& r) {
-    const int64_t e = first(k);
-#pragma unroll
-    for (int j = 0; j < RPG; ++j) r.p[j] = recs[e + kTinyGroups * j];
-  };
-  auto gather = [&](int32_t k, const Rec& r, Rows& v) {  // tile k's rows and weights
-#pragma unroll
-    for (int j = 0; j < RPG; ++j) v.v[j] = *reinterpret_cast<const f4*>(gsrc<TWO>(a, r.p[j].y) + f);
-    if constexpr (WEIGHTED) {
-      const int64_t e = first(k);
-#pragma unroll
-      for (int j = 0; j < RPG; ++j) v.w[j] = ws[e + kTinyGroups * j];
-    }
-  };
-  auto produce = [&](int32_t i, const Rec& c, const Rows& v) {
-    const bool live = i < my_tiles;  // the drain iteration's tile is stored as padding (never consumed)
-#pragma unroll
-    for (int j = 0; j < RPG; ++j) {
-      const int32_t code = live ? c.p[j].x : -1;
-      const bool has = code >= 0;
-      const int32_t row = has ? code : (code == -1 ? -1 : -2 - code);
-      float o[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float m0 = WEIGHTED ? __fmul_rn(v.v[j][k], v.w[j]) : v.v[j][k];
-        const float t = R::combine(R::init(), has ? R::msg(m0) : R::init());
-        o[k] = row >= 0 ? R::finish(t, has ? 1 : 0) : 0.0f;
-      }
-      store(i, g + kTinyGroups * j, row, o);
-    }
-  };
-  // register sets rotate by name (the loop unrolled by three); every load is
-  // unconditional, so hipcc's in-order vmcnt waits leave the later ones in flight
-  Rec s0, s1, s2, cur;
-  Rows v0, v1, v2;
-  rec(0, s0);
-  rec(1, s1);
-  gather(0, s0, v0);
-  rec(2, s2);
-  gather(1, s1, v1);
-  cur = s0;
-  auto step = [&](int32_t i, Rec& r_next, Rec& r_gather, Rec& r_free, Rows& vc, Rows& vn) {
-    rec(i + 3, r_free);           // tile i+3's records
-    gather(i + 2, r_gather, vn);  // tile i+2's rows
-    produce(i, cur, vc);          // tile i (rows in flight since i-2)
-    cur = r_next;
-    lds_barrier();
-  };
-  for (int32_t i = 0; i <= my_tiles; i += 3) {
-    step(i, s1, s2, s0, v0, v2);
-    if (i + 1 > my_tiles) break;
-    step(i + 1, s2, s0, s1, v1, v0);
-    if (i + 2 > my_tiles) break;
-    step(i + 2, s0, s1, s2, v2, v1);
-  }
-}
 
 // NG: edges gathered per row (2 for the degree-2 head of the tail, 1 for the
 // degree <= 1 rest: the schedule is degree-descending, so each is a range).
@@ -835,47 +744,6 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
   // ---- producers: tile i at iteration i
   const int pt = tid - 512;
   const int g = pt >> 5, lane = pt & 31, f = lane * 4;
-  typedef float f4 __attribute__((ext_vector_type(4)));
-  // aggregated row segment o of tile i's row tr (graph row `row`, -1 = padding):
-  // the GIN pre-scale / saved aggregate, then its bf16 planes into LDS tile i & 1
-  auto store_tile = [&](int64_t i, int tr, int32_t row, float (&o)[4]) {
-    const int b = int(i & 1);
-    if constexpr (EXTRA) {
-      if (row >= 0 && a.pre_gin) {
-        float xv[4];
-        vload<4>(xv, a.x + int64_t(row) * a.ld_x + f);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) o[k] = __fadd_rn(__fmul_rn(a.gin_scale, xv[k]), o[k]);
-      }
-      if (row >= 0 && a.agg_out) vstore<4>(a.agg_out + int64_t(row) * a.ld_agg + f, o);
-    }
-    bf16x4_t ph, pm, pl;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      short h, m_, l;
-      split3_a(o[k], h, m_, l);
-      ph[k] = h;
-      pm[k] = m_;
-      pl[k] = l;
-    }
-    if (!split_fast_ok(o[0], o[1], o[2], o[3])) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        short h, m_, l;
-        split3_a_lo(o[k], h, m_, l);
-        ph[k] = h;
-        pm[k] = m_;
-        pl[k] = l;
-      }
-    }
-    *reinterpret_cast<bf16x4_t*>(&planes[b][0][tr][f]) = ph;
-    *reinterpret_cast<bf16x4_t*>(&planes[b][1][tr][f]) = pm;
-    *reinterpret_cast<bf16x4_t*>(&planes[b][2][tr][f]) = pl;
-    if (lane == 0) trow[b][tr] = row;
-  };
-  if constexpr (NG == 1) {
-    tiny1_producer<R, WEIGHTED, kTinyRPG, kTinyRows, TWO>(a, g, f, int32_t(n_tiles), int32_t(my_tiles), store_tile);
-  } else {
   struct Rec {
     int4 p[kTinyRPG];
     float2 w[kTinyRPG];
@@ -891,6 +759,7 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
       if constexpr (WEIGHTED) r.w[j] = a.tw[ec];
     }
   };
+  typedef float f4 __attribute__((ext_vector_type(4)));
   auto gather = [&](const Rec& r, f4 (&v)[kTinyRPG][NG]) {
 #pragma unroll
     for (int j = 0; j < kTinyRPG; ++j) {
@@ -899,6 +768,7 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
     }
   };
   auto produce = [&](int64_t i, const auto& c, const f4 (&v)[kTinyRPG][NG]) {
+    const int b = int(i & 1);
 #pragma unroll
     for (int j = 0; j < kTinyRPG; ++j) {
       const int32_t row = c.row[j], deg = c.deg[j];
@@ -908,11 +778,45 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
         float t = R::init();
         const float m0 = WEIGHTED ? __fmul_rn(v[j][0][k], c.w[j].x) : v[j][0][k];
         t = R::combine(t, deg > 0 ? R::msg(m0) : R::init());
-        const float m1 = WEIGHTED ? __fmul_rn(v[j][1][k], c.w[j].y) : v[j][1][k];
-        t = R::combine(t, deg > 1 ? R::msg(m1) : R::init());
+        if constexpr (NG == 2) {
+          const float m1 = WEIGHTED ? __fmul_rn(v[j][1][k], c.w[j].y) : v[j][1][k];
+          t = R::combine(t, deg > 1 ? R::msg(m1) : R::init());
+        }
         o[k] = row >= 0 ? R::finish(t, deg) : 0.0f;
       }
-      store_tile(i, g + kTinyGroups * j, row, o);
+      if constexpr (EXTRA) {
+        if (row >= 0 && a.pre_gin) {
+          float xv[4];
+          vload<4>(xv, a.x + int64_t(row) * a.ld_x + f);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) o[k] = __fadd_rn(__fmul_rn(a.gin_scale, xv[k]), o[k]);
+        }
+        if (row >= 0 && a.agg_out) vstore<4>(a.agg_out + int64_t(row) * a.ld_agg + f, o);
+      }
+      bf16x4_t ph, pm, pl;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        short h, m_, l;
+        split3_a(o[k], h, m_, l);
+        ph[k] = h;
+        pm[k] = m_;
+        pl[k] = l;
+      }
+      if (!split_fast_ok(o[0], o[1], o[2], o[3])) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          short h, m_, l;
+          split3_a_lo(o[k], h, m_, l);
+          ph[k] = h;
+          pm[k] = m_;
+          pl[k] = l;
+        }
+      }
+      const int tr = g + kTinyGroups * j;
+      *reinterpret_cast<bf16x4_t*>(&planes[b][0][tr][f]) = ph;
+      *reinterpret_cast<bf16x4_t*>(&planes[b][1][tr][f]) = pm;
+      *reinterpret_cast<bf16x4_t*>(&planes[b][2][tr][f]) = pl;
+      if (lane == 0) trow[b][tr] = row;
     }
   };
   // Pipeline, at iteration i: issue tile i+2's records, issue tile i+1's row
@@ -951,7 +855,6 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
     if (i + 1 > my_tiles) break;
     step(i + 1, rb, ra, v1, v0);
   }
-  }  // NG == 2
 }
 
 // Split rows: combine chunk partials in order, finish, then out = v @ W + b (VALU).
@@ -1049,12 +952,8 @@ int launch(const FusedArgs& a, hipStream_t s) {
     const bool extra = a.pre_gin || a.agg_out;
     for (int part = 0; part < 2; ++part) {
       FusedArgs b = a;
-      // the compact one-edge records follow the n_tiny2 two-edge ones; their
-      // weights start at float 2 n_tiny2 rounded up to 16 bytes (tiny.py)
       b.tpack = a.tpack + (part ? a.n_tiny2 : 0);
-      b.tw = a.tw ? reinterpret_cast<const float2*>(reinterpret_cast<const float*>(a.tw) +
-                                                    (part ? (2 * a.n_tiny2 + 3) / 4 * 4 : 0))
-                  : nullptr;
+      b.tw = a.tw ? a.tw + (part ? a.n_tiny2 : 0) : nullptr;
       b.n_tiny = part ? a.n_tiny - a.n_tiny2 : a.n_tiny2;
       if (b.n_tiny <= 0) continue;
       auto k = part ? (extra ? spmm_gemm_tiny_kernel<RED, W, true, 1, TWO> : spmm_gemm_tiny_kernel<RED, W, false, 1, TWO>)
@@ -1135,8 +1034,6 @@ extern "C" int kgx_spmm_gemm_ex3(int reduce, const int32_t* rowptr, const int32_
               "kgx_spmm_gemm: the tiny-row records need the schedule (and weights when weighted)");
   KGX_REQUIRE(!tiny_pack || (n_tiny_deg2 >= 0 && n_tiny_deg2 <= n_items - n_short_end), KGX_ERR_ARG,
               "kgx_spmm_gemm: n_tiny_deg2 must lie in [0, n_items - n_short_end]");
-  KGX_REQUIRE(reinterpret_cast<uintptr_t>(tiny_pack) % 16 == 0 && reinterpret_cast<uintptr_t>(tiny_w) % 16 == 0,
-              KGX_ERR_ARG, "kgx_spmm_gemm: tiny_pack and tiny_w must be 16-byte aligned");
   KGX_REQUIRE(reduce >= KGX_SUM && reduce <= KGX_MIN, KGX_ERR_ARG, "kgx_spmm_gemm: reduce %d unsupported", reduce);
   KGX_REQUIRE(F_in == kFin, KGX_ERR_UNSUPPORTED, "kgx_spmm_gemm: F_in must be %d (got %lld)", kFin,
               (long long)F_in);

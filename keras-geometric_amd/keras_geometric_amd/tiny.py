@@ -4,10 +4,8 @@ The fused aggregate->transform launch (kgx_spmm_gemm_ex2) reads the rows of
 degree <= 2 at the end of the degree-descending schedule (on R-MAT about
 two thirds of all rows; the self loop alone is half) from one record each
 instead of an item plus index and weight loads: {row, degree, col0, col1}
-(col1 = col0 for degree 1, 0 and 0 for degree 0) and {w0, w1} for the
-degree-2 head, compact {row (-2 - row for degree 0), col0} and w0 for the
-degree <= 1 rest (padded to whole tiles; layout in include/kgx.h,
-kgx_spmm_gemm_ex2).  Built once per graph with torch ops on the graph's device and cached on the graph.
+(col1 = col0 for degree 1, 0 and 0 for degree 0) and {w0, w1}.  Built once
+per graph with torch ops on the graph's device and cached on the graph.
 Reference semantics are unchanged: the kernel folds exactly the row's CSR
 edges in order (gcn_conv.py:233-272, aggregators.py:56-167).
 """
@@ -21,7 +19,6 @@ import torch
 
 TINY_MAX = 2       # the kernel gathers two edges per row
 _MIN_ROWS = 4096   # below this the tail stays on the short-row kernel
-PAD_ROWS = 256     # the compact one-edge records are padded to a multiple of this (whole kernel tiles)
 
 
 def tiny_suffix_start(items: torch.Tensor) -> int:
@@ -36,30 +33,21 @@ def tiny_suffix_start(items: torch.Tensor) -> int:
 
 
 def pack_numel(n: int, n2: int) -> int:
-    """int32 entries of the packed tail of n rows whose first n2 have degree 2."""
-    return 4 * n2 + 2 * (-(-(n - n2) // PAD_ROWS) * PAD_ROWS)
+    """int32 entries of the packed tail of n rows (n2 of them of degree 2)."""
+    return 4 * n
 
 
 def records(pack: torch.Tensor, tw: Optional[torch.Tensor], n: int, n2: int):
-    """The packed tail back as one {row, degree, col0, col1} record [n, 4] and
-    {w0, w1} [n, 2] (or None) per row: what tests and tools compare."""
-    head = pack[:4 * n2].view(n2, 4).long()
-    rest = pack[4 * n2:4 * n2 + 2 * (n - n2)].view(n - n2, 2).long()
-    has = rest[:, 0] >= 0
-    row = torch.where(has, rest[:, 0], -2 - rest[:, 0])
-    rec = torch.cat([head, torch.stack([row, has.long(), rest[:, 1], rest[:, 1]], 1)])
-    if tw is None:
-        return rec, None
-    w_rest = tw[2 * n2 + (-(2 * n2) % 4):][:n - n2]
-    return rec, torch.cat([tw[:2 * n2].view(n2, 2), torch.stack([w_rest, torch.zeros_like(w_rest)], 1)])
+    """The packed tail as {row, degree, col0, col1} [n, 4] and {w0, w1} [n, 2]
+    (or None) per row: what tests and tools compare."""
+    return pack[:n].long(), (tw[:n] if tw is not None else None)
 
 
 def tiny_pack(g, refresh: bool = False) -> tuple[Optional[torch.Tensor], Optional[torch.Tensor], int, int]:
-    """(pack int32, weights float32 or None, n_short_end, n_deg2) for graph g's
-    schedule, or (None, None, -1, 0) when the tail is too short or disabled
-    (KGX_TINY=0).  The first n_deg2 rows have degree 2 (the kernel gathers one
-    edge per row for the rest); the flat layout is kgx_spmm_gemm_ex2's
-    (include/kgx.h), records() unpacks it.  Cached on g; built when
+    """(pack [n, 4] int32, weights [n, 2] float32 or None, n_short_end, n_deg2)
+    for graph g's schedule, or (None, None, -1, 0) when the tail is too short
+    or disabled (KGX_TINY=0).  The first n_deg2 records have degree 2 (the
+    kernel gathers one edge per row for the rest).  Cached on g; built when
     the schedule is (graph._build_schedule, refresh=True), where the graph
     build syncs anyway, so a fused launch never syncs and can be captured
     into a HIP graph whatever ran on the graph first."""
@@ -90,27 +78,17 @@ def tiny_pack(g, refresh: bool = False) -> tuple[Optional[torch.Tensor], Optiona
                 return res
             c0 = torch.where(deg > 0, g.col[i0].long(), torch.zeros_like(deg))
             c1 = torch.where(deg > 0, g.col[i1].long(), torch.zeros_like(deg))
-            row = t[:, 0].long()
+            pack = torch.stack([t[:, 0].long(), deg, c0, c1], 1).to(torch.int32).contiguous()
+            tw = None
+            if getattr(g, "w", None) is not None:
+                w0 = torch.where(deg > 0, g.w[i0], torch.zeros_like(g.w[i0]))
+                w1 = torch.where(deg > 1, g.w[i1], torch.zeros_like(g.w[i1]))
+                tw = torch.stack([w0, w1], 1).to(torch.float32).contiguous()
             # degree-descending schedule: the degree-2 rows come first; if not
             # (another item order), every record takes the two-edge kernel
             n2 = int((deg == 2).sum())
             if n2 and not bool((deg[:n2] == 2).all()):
-                n2 = row.numel()
-            n1 = row.numel() - n2
-            pad = -n1 % PAD_ROWS
-            head = torch.stack([row[:n2], deg[:n2], c0[:n2], c1[:n2]], 1).reshape(-1)
-            # one-edge rows: {code, col0}, code = row, or -2 - row for degree 0 (col0 = 0)
-            code = torch.where(deg[n2:] > 0, row[n2:], -2 - row[n2:])
-            rest = torch.stack([code, c0[n2:]], 1).reshape(-1)
-            rest = torch.cat([rest, torch.tensor([-1, 0], dtype=rest.dtype, device=rest.device).repeat(pad)])
-            pack = torch.cat([head, rest]).to(torch.int32).contiguous()
-            tw = None
-            if getattr(g, "w", None) is not None:
-                w0 = torch.where(deg > 0, g.w[i0], torch.zeros_like(g.w[i0])).float()
-                w1 = torch.where(deg > 1, g.w[i1], torch.zeros_like(g.w[i1])).float()
-                gap = -(2 * n2) % 4  # the one-edge weights start 16-byte aligned
-                tw = torch.cat([torch.stack([w0[:n2], w1[:n2]], 1).reshape(-1), w0.new_zeros(gap), w0[n2:],
-                                w0.new_zeros(pad)]).contiguous()
+                n2 = pack.shape[0]
             res = (pack, tw, start, n2)
     try:
         g._kgx_tiny = res

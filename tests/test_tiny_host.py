@@ -33,12 +33,7 @@ def test_tiny_pack_layout_roundtrip():
     pack, tw, start, n2 = tiny.tiny_pack(g)
     assert pack is not None and start == 40 and n2 == 3000
     n = g.n_items - start
-    n1 = n - n2
-    # flat layout: 4 n2 + 2 * ceil(n1 / 256) * 256 ints; weights 2 n2 (+ gap to 16 B) + padded one-edge weights
-    assert pack.numel() == 4 * n2 + 2 * (-(-n1 // tiny.PAD_ROWS) * tiny.PAD_ROWS)
-    assert tw.numel() == 2 * n2 + (-(2 * n2) % 4) + (-(-n1 // tiny.PAD_ROWS) * tiny.PAD_ROWS)
-    pad = pack[4 * n2 + 2 * n1:].view(-1, 2)
-    assert (pad[:, 0] == -1).all() and (pad[:, 1] == 0).all()
+    assert pack.numel() == tiny.pack_numel(n, n2) and tuple(tw.shape) == (n, 2)
     rec, w = tiny.records(pack, tw, n, n2)
     t = items[start:]
     d = t[:, 2] - t[:, 1]
@@ -48,10 +43,12 @@ def test_tiny_pack_layout_roundtrip():
     np.testing.assert_array_equal(rec[has, 2].numpy(), col[t[has, 1]])
     two = d == 2
     np.testing.assert_array_equal(rec[two, 3].numpy(), col[t[two, 1] + 1])
+    one = d == 1
+    np.testing.assert_array_equal(rec[one, 3].numpy(), rec[one, 2].numpy())  # col1 = col0 below degree 2
     ww = g.w.numpy()
     np.testing.assert_array_equal(w[has, 0].numpy(), ww[t[has, 1]])
     np.testing.assert_array_equal(w[two, 1].numpy(), ww[t[two, 1] + 1])
-    assert (w[~has].numpy() == 0).all()
+    assert (w[~has].numpy() == 0).all() and (w[one, 1].numpy() == 0).all()
     # every source index the kernels gather is a valid row
     assert int(rec[:, 2].min()) >= 0 and int(rec[:, 3].min()) >= 0
 
@@ -66,7 +63,7 @@ def test_tiny_pack_unweighted_and_unsorted():
     g2.items = g2.items[perm]
     pack2, tw2, start2, n2b = tiny.tiny_pack(g2)
     n = g2.n_items - start2
-    assert n2b == n and pack2.numel() == 4 * n
+    assert n2b == n
     rec, _ = tiny.records(pack2, tw2, n, n2b)
     t = items2[perm][start2:]
     np.testing.assert_array_equal(rec[:, 1].numpy(), t[:, 2] - t[:, 1])
