@@ -70,7 +70,7 @@ struct FusedArgs {
   int share_gpu;    // launch 7/8 of the resident grid
   int relu;         // out = max(result, 0) (not with accumulate)
   float gin_scale;
-  int debug;        // experiment builds only (-DKGX_EXPERIMENTS, env KGX_FUSED_DEBUG): 1 skip MFMA, 2 skip stores
+  int debug;        // experiment builds only (-DKGX_EXPERIMENTS, env KGX_FUSED_DEBUG): 1 skip MFMA, 2 skip stores (main / short kernels); 4 / 8 / 16 tiny kernel: skip MFMA, skip stores, gathers all from row 0
   int64_t n_short_end;  // items [n_long, n_short_end): spmm_gemm_short_kernel
   const int4* tpack;    // rows of degree <= 2 as {row, degree, col0, col1} (spmm_gemm_tiny_kernel)
   const float2* tw;     // their weights {w0, w1} (weighted reductions)
@@ -703,6 +703,9 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
         f32x4 d[kTinyRPG];
 #pragma unroll
         for (int rb = 0; rb < kTinyRPG; ++rb) d[rb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#ifdef KGX_EXPERIMENTS  // cost decomposition (KGX_FUSED_DEBUG 4: no MFMAs, 8: no stores, 16: gathers all hit row 0)
+        if (!(a.debug & 4))
+#endif
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) {
 #pragma unroll
@@ -722,6 +725,9 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
         // lane (m, q) holds column n_col of rows 16 rb + 4 q + j: four 64-byte
         // row segments per store instruction (the wave next door writes the
         // other half of each 128-byte line)
+#ifdef KGX_EXPERIMENTS
+        if (!(a.debug & 8))
+#endif
 #pragma unroll
         for (int rb = 0; rb < kTinyRPG; ++rb)
 #pragma unroll
@@ -763,8 +769,14 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
   auto gather = [&](const Rec& r, f4 (&v)[kTinyRPG][NG]) {
 #pragma unroll
     for (int j = 0; j < kTinyRPG; ++j) {
+#ifdef KGX_EXPERIMENTS
+      const bool hit = a.debug & 16;
+      v[j][0] = *reinterpret_cast<const f4*>(gsrc<TWO>(a, hit ? 0 : r.p[j].z) + f);
+      if constexpr (NG == 2) v[j][1] = *reinterpret_cast<const f4*>(gsrc<TWO>(a, hit ? 0 : r.p[j].w) + f);
+#else
       v[j][0] = *reinterpret_cast<const f4*>(gsrc<TWO>(a, r.p[j].z) + f);
       if constexpr (NG == 2) v[j][1] = *reinterpret_cast<const f4*>(gsrc<TWO>(a, r.p[j].w) + f);
+#endif
     }
   };
   auto produce = [&](int64_t i, const auto& c, const f4 (&v)[kTinyRPG][NG]) {
