@@ -655,6 +655,10 @@ constexpr int kTinyGroups = 16;  // producer row groups
 #ifndef KGX_TINY_RPG1
 #define KGX_TINY_RPG1 4
 #endif
+// MFMA waves compute D^T so each lane stores four adjacent output columns (dwordx4)
+#ifndef KGX_TINY_TSTORE
+#define KGX_TINY_TSTORE 1
+#endif
 template <int NG>
 constexpr int tiny_rows() { return kTinyGroups * (NG == 1 ? KGX_TINY_RPG1 : KGX_TINY_RPG); }
 
@@ -696,7 +700,13 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
       wfm[s] = __builtin_bit_cast(bf16x8_t, pm);
       wfl[s] = __builtin_bit_cast(bf16x8_t, pl);
     }
+#if KGX_TINY_TSTORE
+    const int c4 = wave * 16 + 4 * q;
+    const float4 b4 = (mfma_wave && a.bias) ? make_float4(a.bias[c4], a.bias[c4 + 1], a.bias[c4 + 2], a.bias[c4 + 3])
+                                            : make_float4(0.f, 0.f, 0.f, 0.f);
+#else
     const float bcol = (mfma_wave && a.bias) ? a.bias[n_col] : 0.0f;
+#endif
     for (int64_t i = 0; i <= my_tiles; ++i) {
       if (i >= 1 && mfma_wave) {
         const int b = int((i - 1) & 1);
@@ -714,12 +724,21 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
             const bf16x8_t ah = *reinterpret_cast<const bf16x8_t*>(&planes[b][0][tr][32 * q + 8 * s4]);
             const bf16x8_t am = *reinterpret_cast<const bf16x8_t*>(&planes[b][1][tr][32 * q + 8 * s4]);
             const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(&planes[b][2][tr][32 * q + 8 * s4]);
+#if KGX_TINY_TSTORE  // D^T = W^T x^T: same products, same k order, lane (m, q) gets 4 adjacent columns of row m
+            d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[s4], al, d[rb], 0, 0, 0);
+            d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfl[s4], ah, d[rb], 0, 0, 0);
+            d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfm[s4], am, d[rb], 0, 0, 0);
+            d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[s4], am, d[rb], 0, 0, 0);
+            d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfm[s4], ah, d[rb], 0, 0, 0);
+            d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[s4], ah, d[rb], 0, 0, 0);
+#else
             d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, wfh[s4], d[rb], 0, 0, 0);
             d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfl[s4], d[rb], 0, 0, 0);
             d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, wfm[s4], d[rb], 0, 0, 0);
             d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, wfh[s4], d[rb], 0, 0, 0);
             d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfm[s4], d[rb], 0, 0, 0);
             d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfh[s4], d[rb], 0, 0, 0);
+#endif
           }
         }
         // lane (m, q) holds column n_col of rows 16 rb + 4 q + j: four 64-byte
@@ -728,6 +747,24 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
 #ifdef KGX_EXPERIMENTS
         if (!(a.debug & 8))
 #endif
+#if KGX_TINY_TSTORE
+        // lane (m, q) holds columns 16 wave + 4 q .. + 3 of tile row 16 rb + m: one
+        // dwordx4 per lane, four store instructions per tile instead of sixteen
+#pragma unroll
+        for (int rb = 0; rb < kTinyRPG; ++rb) {
+          const int rr = trow[b][16 * rb + m];
+          if (rr >= 0) {
+            float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + c4);
+            float4 v = make_float4(d[rb][0] + b4.x, d[rb][1] + b4.y, d[rb][2] + b4.z, d[rb][3] + b4.w);
+            if (a.accumulate) {
+              const float4 p = *dst;
+              v = make_float4(__fadd_rn(p.x, v.x), __fadd_rn(p.y, v.y), __fadd_rn(p.z, v.z), __fadd_rn(p.w, v.w));
+            }
+            if (a.relu) v = make_float4(fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f));
+            *dst = v;
+          }
+        }
+#else
 #pragma unroll
         for (int rb = 0; rb < kTinyRPG; ++rb)
 #pragma unroll
@@ -741,6 +778,7 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
               *dst = v;
             }
           }
+#endif
       }
       lds_barrier();
     }
@@ -1063,6 +1101,8 @@ extern "C" int kgx_spmm_gemm_ex3(int reduce, const int32_t* rowptr, const int32_
   KGX_REQUIRE(ld_x < (int64_t(1) << 31), KGX_ERR_ARG, "kgx_spmm_gemm: x leading dimension >= 2^31");
   KGX_REQUIRE(ld_x % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0 && ld_out >= F_out, KGX_ERR_ARG,
               "kgx_spmm_gemm: x must be 16-byte aligned with ld %% 4 == 0");
+  KGX_REQUIRE(ld_out % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0, KGX_ERR_ARG,
+              "kgx_spmm_gemm: out must be 16-byte aligned with ld %% 4 == 0 (row stores are dwordx4)");
   KGX_REQUIRE(!items || n_split == 0 || (split && partials), KGX_ERR_ARG,
               "kgx_spmm_gemm: split rows need split list and partials");
   FusedArgs a{};
