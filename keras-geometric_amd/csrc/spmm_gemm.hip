@@ -37,9 +37,14 @@ namespace {
 constexpr int kFin = 128;
 constexpr int kGroups = 16;       // rows per block iteration
 constexpr int kThreads = kGroups * 32;
-constexpr int kTileLd = kFin + 4;  // padded LDS row
+[[maybe_unused]] constexpr int kTileLd = kFin + 4;  // padded LDS row (the out-tile forms)
 #ifndef KGX_FUSED_BF16X3
 #define KGX_FUSED_BF16X3 1  // 0: f32-input MFMA (exact f32 products, 16x slower per clock)
+#endif
+// spmm_gemm_kernel's MFMA waves compute D^T and store four adjacent columns per
+// lane straight from the accumulators instead of through an f32 LDS out tile
+#ifndef KGX_FUSED_TSTORE
+#define KGX_FUSED_TSTORE 1
 #endif
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -165,7 +170,11 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
 #else
   __shared__ float tile[kGroups][kTileLd];
 #endif
+#if KGX_FUSED_TSTORE && KGX_FUSED_BF16X3
+  __shared__ __attribute__((aligned(16))) float sbias[kFin];  // read at the stores (4 VGPRs fewer than a register copy)
+#else
   __shared__ float otile[kGroups][kTileLd];  // MFMA results, re-read as whole rows
+#endif
   __shared__ int32_t tile_row[kGroups];
 
   const int tid = threadIdx.x;
@@ -206,7 +215,12 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
 #pragma unroll
   for (int s = 0; s < 32; ++s) wb[s] = mfma_wave ? a.W[int64_t(32 * q + s) * a.F_out + n_col] : 0.0f;
 #endif
+#if KGX_FUSED_TSTORE && KGX_FUSED_BF16X3
+  const int c4 = wave * 16 + 4 * q;
+  if (tid < kFin) sbias[tid] = (a.bias && tid < a.F_out) ? a.bias[tid] : 0.0f;  // first read after the tile barrier
+#else
   const float bcol = (mfma_wave && a.bias) ? a.bias[n_col] : 0.0f;
+#endif
 
   const int64_t n_work = a.items ? a.n_long : a.n_rows;
   const int64_t stride = int64_t(gridDim.x) * kGroups;
@@ -367,12 +381,21 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
         const bf16x8_t am = *reinterpret_cast<const bf16x8_t*>(&tile3[1][m][32 * q + 8 * s4]);
         const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(&tile3[2][m][32 * q + 8 * s4]);
         // small terms first
+#if KGX_FUSED_TSTORE  // D^T = W^T x^T (same products and k order)
+        d1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[s4], al, d1, 0, 0, 0);
+        d0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfl[s4], ah, d0, 0, 0, 0);
+        d1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfm[s4], am, d1, 0, 0, 0);
+        d0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[s4], am, d0, 0, 0, 0);
+        d1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfm[s4], ah, d1, 0, 0, 0);
+        d0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[s4], ah, d0, 0, 0, 0);
+#else
         d1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, wfh[s4], d1, 0, 0, 0);
         d0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfl[s4], d0, 0, 0, 0);
         d1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, wfm[s4], d1, 0, 0, 0);
         d0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, wfh[s4], d0, 0, 0, 0);
         d1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfm[s4], d1, 0, 0, 0);
         d0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfh[s4], d0, 0, 0, 0);
+#endif
       }
 #else
       constexpr int s_end = 32;
@@ -385,6 +408,26 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
         d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(t4.w, wb[s0 + 3], d1, 0, 0, 0);
       }
 #endif
+#if KGX_FUSED_TSTORE && KGX_FUSED_BF16X3
+      // straight from the accumulators: lane (m, q) writes columns 16 wave + 4 q .. + 3 of tile row m
+      const int rr = tile_row[m];
+      if (rr >= 0 && !(a.debug & 2)) {
+        float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + c4);
+        const float4 b4 = *reinterpret_cast<const float4*>(&sbias[c4]);
+        float4 v = make_float4((d0[0] + d1[0]) + b4.x, (d0[1] + d1[1]) + b4.y, (d0[2] + d1[2]) + b4.z,
+                               (d0[3] + d1[3]) + b4.w);
+        if (a.accumulate) {
+          const float4 p = *dst;
+          v = make_float4(__fadd_rn(p.x, v.x), __fadd_rn(p.y, v.y), __fadd_rn(p.z, v.z), __fadd_rn(p.w, v.w));
+        }
+        if (a.relu) v = make_float4(fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f));
+        *dst = v;
+      }
+    }
+    lds_barrier();  // every wave is done with the planes and tile_row before the next tile's are written
+  }
+}
+#else
 #pragma unroll
       for (int j = 0; j < 4; ++j) otile[4 * q + j][n_col] = (d0[j] + d1[j]) + bcol;
     }
@@ -405,6 +448,7 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
     }
   }
 }
+#endif
 
 // Rows of degree <= KGX_SHORT_ROW_MAX (the schedule's suffix; 78 % of an R-MAT graph's
 // rows, 11 % of its edges).  spmm_gemm_kernel gives each row-group ONE row per
@@ -421,6 +465,11 @@ static_assert(KGX_SHORT_ROW_MAX == 7, "the short kernel gathers two edges per ro
 #ifndef KGX_SHORT_PF
 #define KGX_SHORT_PF 3
 #endif
+// MFMA waves compute D^T and store four adjacent columns per lane straight from
+// the accumulators (no f32 LDS out tile, two barriers per tile instead of four)
+#ifndef KGX_SHORT_TSTORE
+#define KGX_SHORT_TSTORE 0  // measured +0.01 ms (0.99 vs 0.98): the out-tile form stays
+#endif
 constexpr int kRPG = KGX_SHORT_RPG;        // rows per group per tile
 constexpr int kSPF = KGX_SHORT_PF;         // edges per row gathered up front (all rows together)
 constexpr int kShortRows = kGroups * kRPG;
@@ -431,8 +480,12 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
   // split planes of the 64 aggregated rows; after the MFMAs the same bytes hold the f32 results
   __shared__ __attribute__((aligned(16))) short tile3[3][kShortRows][kFin + 8];
   __shared__ int32_t tile_row[kShortRows];
+#if KGX_SHORT_TSTORE
+  __shared__ __attribute__((aligned(16))) float sbias[kFin];  // read at the stores
+#else
   static_assert(sizeof(tile3) >= sizeof(float) * kShortRows * kTileLd, "output tile must fit the plane buffer");
   float(*otile)[kTileLd] = reinterpret_cast<float(*)[kTileLd]>(&tile3[0][0][0]);
+#endif
 
   const int tid = threadIdx.x;
   const int g = tid >> 5;
@@ -463,7 +516,12 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
     wfm[s] = __builtin_bit_cast(bf16x8_t, pm);
     wfl[s] = __builtin_bit_cast(bf16x8_t, pl);
   }
+#if KGX_SHORT_TSTORE
+  const int c4 = wave * 16 + 4 * q;
+  if (tid < kFin) sbias[tid] = (a.bias && tid < a.F_out) ? a.bias[tid] : 0.0f;  // first read after two barriers
+#else
   const float bcol = (mfma_wave && a.bias) ? a.bias[n_col] : 0.0f;
+#endif
 
   for (int64_t base = a.n_long + int64_t(blockIdx.x) * kShortRows; base < a.n_short_end;
        base += int64_t(gridDim.x) * kShortRows) {
@@ -592,15 +650,46 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
           const bf16x8_t ah = *reinterpret_cast<const bf16x8_t*>(&tile3[0][tr][32 * q + 8 * s4]);
           const bf16x8_t am = *reinterpret_cast<const bf16x8_t*>(&tile3[1][tr][32 * q + 8 * s4]);
           const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(&tile3[2][tr][32 * q + 8 * s4]);
+#if KGX_SHORT_TSTORE  // D^T = W^T x^T (same products and k order): lane (m, q) gets 4 adjacent columns of row m
+          d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[s4], al, d[rb], 0, 0, 0);
+          d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfl[s4], ah, d[rb], 0, 0, 0);
+          d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfm[s4], am, d[rb], 0, 0, 0);
+          d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[s4], am, d[rb], 0, 0, 0);
+          d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfm[s4], ah, d[rb], 0, 0, 0);
+          d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[s4], ah, d[rb], 0, 0, 0);
+#else
           d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, wfh[s4], d[rb], 0, 0, 0);
           d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfl[s4], d[rb], 0, 0, 0);
           d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, wfm[s4], d[rb], 0, 0, 0);
           d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, wfh[s4], d[rb], 0, 0, 0);
           d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfm[s4], d[rb], 0, 0, 0);
           d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfh[s4], d[rb], 0, 0, 0);
+#endif
         }
       }
     }
+#if KGX_SHORT_TSTORE
+    // straight from the accumulators: one dwordx4 per lane per 16-row block (the
+    // next tile's first barrier keeps the planes and tile_row until every wave is done)
+    if (mfma_wave && !(a.debug & 2)) {
+      const int m = wl & 15;
+#pragma unroll
+      for (int rb = 0; rb < kRPG; ++rb) {
+        const int rr = tile_row[16 * rb + m];
+        if (rr >= 0) {
+          float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + c4);
+          const float4 b4 = *reinterpret_cast<const float4*>(&sbias[c4]);
+          float4 v = make_float4(d[rb][0] + b4.x, d[rb][1] + b4.y, d[rb][2] + b4.z, d[rb][3] + b4.w);
+          if (a.accumulate) {
+            const float4 p = *dst;
+            v = make_float4(__fadd_rn(p.x, v.x), __fadd_rn(p.y, v.y), __fadd_rn(p.z, v.z), __fadd_rn(p.w, v.w));
+          }
+          if (a.relu) v = make_float4(fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f));
+          *dst = v;
+        }
+      }
+    }
+#else
     lds_barrier();  // every wave has read the planes: their bytes now take the f32 results
     if (mfma_wave) {
 #pragma unroll
@@ -626,6 +715,7 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
         }
       }
     }
+#endif
   }
 }
 
@@ -671,6 +761,11 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
   constexpr int kTinyRows = kTinyGroups * kTinyRPG;
   __shared__ __attribute__((aligned(16))) short planes[2][3][kTinyRows][kFin + 8];
   __shared__ int32_t trow[2][kTinyRows];
+#if KGX_TINY_TSTORE
+  __shared__ __attribute__((aligned(16))) float sbias[kFin];  // read at the stores
+  if (threadIdx.x < kFin)  // first read after a hand-off barrier
+    sbias[threadIdx.x] = (a.bias && int(threadIdx.x) < a.F_out) ? a.bias[threadIdx.x] : 0.0f;
+#endif
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t n_tiles = (a.n_tiny + kTinyRows - 1) / kTinyRows;
@@ -702,8 +797,6 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
     }
 #if KGX_TINY_TSTORE
     const int c4 = wave * 16 + 4 * q;
-    const float4 b4 = (mfma_wave && a.bias) ? make_float4(a.bias[c4], a.bias[c4 + 1], a.bias[c4 + 2], a.bias[c4 + 3])
-                                            : make_float4(0.f, 0.f, 0.f, 0.f);
 #else
     const float bcol = (mfma_wave && a.bias) ? a.bias[n_col] : 0.0f;
 #endif
@@ -755,6 +848,7 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
           const int rr = trow[b][16 * rb + m];
           if (rr >= 0) {
             float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + c4);
+            const float4 b4 = *reinterpret_cast<const float4*>(&sbias[c4]);
             float4 v = make_float4(d[rb][0] + b4.x, d[rb][1] + b4.y, d[rb][2] + b4.z, d[rb][3] + b4.w);
             if (a.accumulate) {
               const float4 p = *dst;
