@@ -380,6 +380,11 @@ def main() -> None:
     elif kind == "gat":  # one pass: h_src row per edge, h_dst row + output row per node
         balg = 4 * (n_rows + 1) + e_agg * (4 + 4 * f_out) + 8 * n_rows * f_out
         kernel = ("gatv2_kernel", "gatv2_fixup_kernel")
+    elif kind == "gin" and world == 1 and not args.exact and kops.fused_transform_supported(f_in, f_out):
+        # fused (1+eps) x_i + aggr -> Dense (kgx_spmm_gemm_f256): gathered rows F_in wide, the x_i root row,
+        # output rows F_out wide; no [N, F_in] intermediate
+        balg = b_alg_spmm(n_rows, e_agg, f_in, weighted=False, f_out=f_out) + 4 * n_rows * f_in
+        kernel = ("spmm_gemm256_kernel", "spmm_gemm256_fixup_kernel")
     else:  # GIN: + the x_i root row of the (1+eps) x_i + aggr epilogue; SAGE mean: plain gather-sum
         balg = b_alg_spmm(n_rows, e_agg, f_in, weighted=False) + (4 * n_rows * f_in if kind == "gin" else 0)
         kernel = ("spmm_kernel", "spmm_fixup_kernel")

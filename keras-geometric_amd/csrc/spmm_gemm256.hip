@@ -1,0 +1,476 @@
+// Fused aggregate -> dense transform for 256-wide rows (gfx950, wave64):
+//
+//   out[i, :] = bias + PRE( REDUCE_{e in CSR row i} x[col_e, :] * (w_e) ) @ W,   W [256, F_out <= 256]
+//
+// GINConv at BASELINE config C4 (F 256 -> 256, sum): (1+eps) x_i + aggr feeds
+// the MLP's Dense (gin_conv.py:216-225, 129-162).  Unfused, the aggregation
+// writes a [N, 256] intermediate that the dense kernel reads back (20.5 GB of
+// HBM traffic at 10M rows); here each aggregated row goes from registers to
+// LDS to the matrix cores and only the transformed row is written.
+//
+// Block = 1024 threads = 16 waves, one block per CU.  Per tile the block takes
+// 16 consecutive schedule items; wave w reduces item w's edges with 64 lanes x
+// float4 (one 1-KB row per gather, 4 gathers in flight, sequential RN adds as
+// in spmm_kernel) and writes the row, split three ways into bf16 hi/mid/lo
+// planes, to an LDS tile.  Then wave w computes output columns [16w, 16w + 16)
+// of the 16-row tile as D^T = W^T x^T with 48 v_mfma_f32_16x16x32_bf16 (the six
+// significant cross products of the split operands over K = 256; f32-accurate,
+// kgx_bf16x3.h).  W's split planes take 384 KB: the hi and mid B-fragments of a
+// wave's 16 columns live in 64 VGPRs for the whole kernel, the lo plane (used
+// by one product of the six) in 128 KB of LDS, read once per k-step.  The next
+// tile's first gathers are issued before the MFMA phase (LDS-only barriers keep
+// them in flight).  Hub-row chunks write raw partials; the fix-up kernel
+// combines them in order and applies W in f32 on the VALU.
+#include <cstdlib>
+
+#include "kgx_bf16x3.h"
+#include "kgx_internal.h"
+#include "kgx_red.h"
+#include "kgx_vec.h"
+
+namespace kgx {
+namespace {
+
+constexpr int kF = 256;            // F_in
+constexpr int kWaves = 8;          // waves per block (one block per CU, 2 waves per SIMD)
+constexpr int kRows = 2 * kWaves;  // rows per tile: two per wave
+constexpr int kColBlocks = 16;     // 16-column blocks of F_out: two per wave
+constexpr int kThreads = kWaves * 64;
+constexpr int kLd = kF + 8;        // LDS plane row (bf16): +16 B keeps the B-fragment reads conflict-free
+constexpr int kSteps = kF / 32;    // k-steps of 32 per MFMA chain
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short bf16x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+struct F256Args {
+  const int32_t* rowptr;
+  const int32_t* rows;
+  int64_t n_rows;
+  const int4* items;  // {row, beg, end, slot}
+  int64_t n_items;
+  const int4* split;  // {row, first slot, chunks, degree}
+  int64_t n_split;
+  const int32_t* idx;
+  const float* w;
+  const float* x;
+  int64_t ld_x;
+  const float* W;  // [256, F_out] row-major
+  int F_out;
+  const float* bias;
+  float* out;
+  int64_t ld_o;
+  float* partials;  // [n_slots, 256]
+  float* agg_out;   // optional [n, ld_agg]: PRE(REDUCE(...)) rows (backward's dW)
+  int64_t ld_agg;
+  int pre_gin;
+  int accumulate;
+  int relu;
+  float gin_scale;
+};
+
+// workgroup barrier for LDS hand-offs only (lgkmcnt, not vmcnt): gathers
+// prefetched for the next tile stay in flight across it
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int RED, bool WEIGHTED>
+__global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_kernel(F256Args a) {
+  using R = RowRed<RED>;
+#ifdef KGX_F256_U
+  constexpr int U = KGX_F256_U;
+#else
+  constexpr int U = 4;  // gathers in flight per row in the two-row loop (8 per wave)
+#endif
+  constexpr int PF = 4;  // first edges of each row gathered ahead, during the previous tile's MFMAs
+  __shared__ u32x4_t wlo[kColBlocks * kSteps * 64];                    // W lo-plane B-fragments, 128 KB
+  __shared__ __attribute__((aligned(16))) short tile3[3][kRows][kLd];  // hi / mid / lo planes of the tile's rows
+  __shared__ __attribute__((aligned(16))) float sbias[kF];
+  __shared__ int32_t tile_row[kRows];
+
+  const int wave = threadIdx.x >> 6;  // reduces tile rows 2 wave, 2 wave + 1; owns output columns [32 wave, +32)
+  const int wl = threadIdx.x & 63;
+  const int f = wl * 4;
+  const int cl = wl & 15;
+  const int q = wl >> 4;
+  const bool mf0 = 32 * wave < a.F_out, mf1 = 32 * wave + 16 < a.F_out;  // column blocks 2 wave, 2 wave + 1
+
+  // W fragments, k permuted: k-step s of lane group q covers k = 64 q + 8 s + j
+  // (j = 0..7), so each x fragment is 8 contiguous bf16 of a tile row
+  bf16x8_t wfh[2][kSteps], wfm[2][kSteps];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int n_col = 32 * wave + 16 * i + cl;
+    const bool on = i ? mf1 : mf0;
+#pragma unroll
+    for (int s = 0; s < kSteps; ++s) {
+      u32x4_t ph, pm, pl;
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        const int k = 64 * q + 8 * s + j;
+        const float v0 = on ? a.W[int64_t(k) * a.F_out + n_col] : 0.0f;
+        const float v1 = on ? a.W[int64_t(k + 1) * a.F_out + n_col] : 0.0f;
+        uint32_t h, m_, l;
+        split3_pair(v0, v1, h, m_, l);
+        ph[j / 2] = h;
+        pm[j / 2] = m_;
+        pl[j / 2] = l;
+      }
+      wfh[i][s] = __builtin_bit_cast(bf16x8_t, ph);
+      wfm[i][s] = __builtin_bit_cast(bf16x8_t, pm);
+      wlo[((2 * wave + i) * kSteps + s) * 64 + wl] = pl;
+    }
+  }
+  if (threadIdx.x < kF) sbias[threadIdx.x] = (a.bias && int(threadIdx.x) < a.F_out) ? a.bias[threadIdx.x] : 0.0f;
+  // (both are first read after the first tile's barrier)
+
+  const int64_t n_work = a.items ? a.n_items : a.n_rows;
+  const int64_t stride = int64_t(gridDim.x) * kRows;
+
+  int32_t row[2], beg[2], end[2], slot[2];
+  int pn[2];
+  float pv[2][PF][4], pw[2][PF];
+  // descriptors of items it, it + 1 and their first U gathers
+  auto fetch = [&](int64_t it) {
+    int32_t c[2][PF];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      row[r] = -1;
+      beg[r] = end[r] = 0;
+      slot[r] = -1;
+      if (it + r < n_work) {
+        if (a.items) {
+          const int4 v = a.items[it + r];
+          row[r] = v.x;
+          beg[r] = v.y;
+          end[r] = v.z;
+          slot[r] = v.w;
+        } else {
+          row[r] = a.rows[it + r];
+          beg[r] = a.rowptr[row[r]];
+          end[r] = a.rowptr[row[r] + 1];
+        }
+      }
+      pn[r] = (end[r] - beg[r]) < PF ? (end[r] - beg[r]) : PF;
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {  // clamped addresses (idx / w hold >= 1 element); masked at the fold
+        const int32_t ee = pn[r] > 0 ? beg[r] + (u < pn[r] ? u : pn[r] - 1) : 0;
+        const int32_t ci = a.idx[ee];
+        c[r][u] = pn[r] > 0 ? ci : 0;
+        if constexpr (WEIGHTED) pw[r][u] = a.w[ee];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int u = 0; u < PF; ++u)
+        if (u < pn[r]) vload<4>(pv[r][u], a.x + row_off(c[r][u], a.ld_x) + f);
+  };
+
+  fetch(int64_t(blockIdx.x) * kRows + 2 * wave);
+  for (int64_t base = int64_t(blockIdx.x) * kRows; base < n_work; base += stride) {
+    float acc[2][4];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[r][k] = R::init();
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int u = 0; u < PF; ++u)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float m = WEIGHTED ? __fmul_rn(pv[r][u][k], pw[r][u]) : pv[r][u][k];
+          acc[r][k] = R::combine(acc[r][k], u < pn[r] ? R::msg(m) : R::init());
+        }
+    // B edges of row r from edge e (the last ones clamped / masked when fewer remain)
+    auto block = [&](auto RR, auto UB, int32_t e) {
+      constexpr int r = decltype(RR)::value;
+      constexpr int B = decltype(UB)::value;
+      const int n = end[r] - e;
+      int32_t c[B];
+      float wt[B];
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const int32_t ee = u < n ? e + u : end[r] - 1;
+        c[u] = a.idx[ee];
+        if constexpr (WEIGHTED) wt[u] = a.w[ee];
+      }
+      float v[B][4];
+#pragma unroll
+      for (int u = 0; u < B; ++u) vload<4>(v[u], a.x + row_off(c[u], a.ld_x) + f);
+#pragma unroll
+      for (int u = 0; u < B; ++u)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float m = WEIGHTED ? __fmul_rn(v[u][k], wt[u]) : v[u][k];
+          acc[r][k] = R::combine(acc[r][k], u < n ? R::msg(m) : R::init());
+        }
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    int32_t e0 = beg[0] + PF, e1 = beg[1] + PF;
+    // both rows together (a tile's rows have similar degrees: degree-ordered schedule), then each alone
+    for (; e0 + U <= end[0] && e1 + U <= end[1]; e0 += U, e1 += U) {
+      int32_t c[2][U];
+      float wt[2][U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        c[0][u] = a.idx[e0 + u];
+        c[1][u] = a.idx[e1 + u];
+        if constexpr (WEIGHTED) {
+          wt[0][u] = a.w[e0 + u];
+          wt[1][u] = a.w[e1 + u];
+        }
+      }
+      float v[2][U][4];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        vload<4>(v[0][u], a.x + row_off(c[0][u], a.ld_x) + f);
+        vload<4>(v[1][u], a.x + row_off(c[1][u], a.ld_x) + f);
+      }
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            acc[r][k] = R::combine(acc[r][k], R::msg(WEIGHTED ? __fmul_rn(v[r][u][k], wt[r][u]) : v[r][u][k]));
+    }
+    for (; e0 + 8 <= end[0]; e0 += 8) block(I0{}, std::integral_constant<int, 8>{}, e0);
+    for (; e0 < end[0]; e0 += 4) block(I0{}, std::integral_constant<int, 4>{}, e0);
+    for (; e1 + 8 <= end[1]; e1 += 8) block(I1{}, std::integral_constant<int, 8>{}, e1);
+    for (; e1 < end[1]; e1 += 4) block(I1{}, std::integral_constant<int, 4>{}, e1);
+
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const bool full_row = row[r] >= 0 && slot[r] < 0;
+      if (row[r] >= 0 && slot[r] >= 0) vstore<4>(a.partials + int64_t(slot[r]) * kF + f, acc[r]);
+      float v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = full_row ? R::finish(acc[r][k], end[r] - beg[r]) : 0.0f;
+      if (full_row && a.pre_gin) {
+        float xv[4];
+        vload<4>(xv, a.x + int64_t(row[r]) * a.ld_x + f);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = __fadd_rn(__fmul_rn(a.gin_scale, xv[k]), v[k]);
+      }
+      if (full_row && a.agg_out) vstore<4>(a.agg_out + int64_t(row[r]) * a.ld_agg + f, v);
+      bf16x4_t ph, pm, pl;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        short h, m_, l;
+        split3_a(v[k], h, m_, l);
+        ph[k] = h;
+        pm[k] = m_;
+        pl[k] = l;
+      }
+      if (!split_fast_ok(v[0], v[1], v[2], v[3])) {  // inf / NaN / huge: non-finite values to the lo plane
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          short h, m_, l;
+          split3_a_lo(v[k], h, m_, l);
+          ph[k] = h;
+          pm[k] = m_;
+          pl[k] = l;
+        }
+      }
+      *reinterpret_cast<bf16x4_t*>(&tile3[0][2 * wave + r][f]) = ph;
+      *reinterpret_cast<bf16x4_t*>(&tile3[1][2 * wave + r][f]) = pm;
+      *reinterpret_cast<bf16x4_t*>(&tile3[2][2 * wave + r][f]) = pl;
+      if (wl == 0) tile_row[2 * wave + r] = full_row ? row[r] : -1;
+    }
+    lds_barrier();
+
+    fetch(base + stride + 2 * wave);  // the next tile's first gathers fly during the MFMAs
+
+    if (mf0) {
+      f32x4 d[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
+#pragma unroll
+      for (int s = 0; s < kSteps; ++s) {
+        const int kk = 64 * q + 8 * s;
+        const bf16x8_t xh = *reinterpret_cast<const bf16x8_t*>(&tile3[0][cl][kk]);
+        const bf16x8_t xm = *reinterpret_cast<const bf16x8_t*>(&tile3[1][cl][kk]);
+        const bf16x8_t xl = *reinterpret_cast<const bf16x8_t*>(&tile3[2][cl][kk]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          if (i == 1 && !mf1) break;
+          const bf16x8_t wf_lo = __builtin_bit_cast(bf16x8_t, wlo[((2 * wave + i) * kSteps + s) * 64 + wl]);
+          // D^T = W^T x^T; small terms first
+          d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[i][s], xl, d[i], 0, 0, 0);
+          d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf_lo, xh, d[i], 0, 0, 0);
+          d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfm[i][s], xm, d[i], 0, 0, 0);
+          d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[i][s], xm, d[i], 0, 0, 0);
+          d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfm[i][s], xh, d[i], 0, 0, 0);
+          d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[i][s], xh, d[i], 0, 0, 0);
+        }
+      }
+      // lane (cl, q) holds columns 32 wave + 16 i + 4 q .. + 3 of tile row cl
+      const int rr = tile_row[cl];
+      if (rr >= 0) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          if (i == 1 && !mf1) break;
+          const int c4 = 32 * wave + 16 * i + 4 * q;
+          float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + c4);
+          const float4 b4 = *reinterpret_cast<const float4*>(&sbias[c4]);
+          float4 v = make_float4(d[i][0] + b4.x, d[i][1] + b4.y, d[i][2] + b4.z, d[i][3] + b4.w);
+          if (a.accumulate) {
+            const float4 p = *dst;
+            v = make_float4(__fadd_rn(p.x, v.x), __fadd_rn(p.y, v.y), __fadd_rn(p.z, v.z), __fadd_rn(p.w, v.w));
+          }
+          if (a.relu) v = make_float4(fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f));
+          *dst = v;
+        }
+      }
+    }
+    lds_barrier();  // the planes and tile_row are free for the next tile
+  }
+}
+
+// Split hub rows: combine the chunk partials in order, finish, PRE, then
+// out = v @ W + b in f32 on the VALU (a few thousand rows per graph).
+template <int RED>
+__global__ __launch_bounds__(256) void spmm_gemm256_fixup_kernel(F256Args a) {
+  using R = RowRed<RED>;
+  __shared__ float vrow[4][kF];
+  const int g = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int64_t base = int64_t(blockIdx.x) * 4; base < a.n_split; base += int64_t(gridDim.x) * 4) {
+    const int64_t it = base + g;
+    int32_t row = -1;
+    if (it < a.n_split) {
+      const int4 s = a.split[it];
+      row = s.x;
+      float acc[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[k] = R::init();
+      constexpr int B = 8;  // chunk loads in flight, then the in-order combine
+      for (int32_t c0 = 0; c0 < s.z; c0 += B) {
+        float p[B][4];
+#pragma unroll
+        for (int u = 0; u < B; ++u)
+          vload<4>(p[u], a.partials + int64_t(s.y + (c0 + u < s.z ? c0 + u : s.z - 1)) * kF + lane * 4);
+#pragma unroll
+        for (int u = 0; u < B; ++u)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) acc[k] = c0 + u < s.z ? R::combine(acc[k], p[u][k]) : acc[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[k] = R::finish(acc[k], s.w);
+      if (a.pre_gin) {
+        float xv[4];
+        vload<4>(xv, a.x + int64_t(row) * a.ld_x + lane * 4);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[k] = __fadd_rn(__fmul_rn(a.gin_scale, xv[k]), acc[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) vrow[g][lane * 4 + k] = acc[k];
+      if (a.agg_out) vstore<4>(a.agg_out + int64_t(row) * a.ld_agg + lane * 4, acc);
+    }
+    __syncthreads();
+    if (row >= 0) {
+      for (int c = lane; c < a.F_out; c += 64) {
+        float s = 0.0f;
+        for (int k = 0; k < kF; ++k) s = fmaf(vrow[g][k], a.W[int64_t(k) * a.F_out + c], s);
+        float v = s + (a.bias ? a.bias[c] : 0.0f);
+        if (a.accumulate) v = __fadd_rn(a.out[int64_t(row) * a.ld_o + c], v);
+        if (a.relu) v = fmaxf(v, 0.0f);
+        a.out[int64_t(row) * a.ld_o + c] = v;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int RED, bool WT>
+int launch256(const F256Args& a, hipStream_t s) {
+  const int64_t work = a.items ? a.n_items : a.n_rows;
+  if (work > 0) {
+    auto k = spmm_gemm256_kernel<RED, WT>;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, 0) != hipSuccess || per_cu <= 0)
+      per_cu = 1;
+    const int64_t cap = int64_t(per_cu) * cu_count();
+    const int64_t need = (work + kRows - 1) / kRows;
+    hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kThreads), 0, s, a);
+    KGX_CHECK_LAUNCH();
+  }
+  if (a.items && a.n_split > 0) {
+    const int64_t blocks = (a.n_split + 3) / 4;
+    hipLaunchKernelGGL(spmm_gemm256_fixup_kernel<RED>, dim3(unsigned(blocks < 4096 ? blocks : 4096)), dim3(256), 0,
+                       s, a);
+    KGX_CHECK_LAUNCH();
+  }
+  return KGX_OK;
+}
+
+}  // namespace
+}  // namespace kgx
+
+using namespace kgx;
+
+extern "C" int kgx_spmm_gemm_f256(int reduce, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
+                                  const int32_t* items, int64_t n_items, const int32_t* split, int64_t n_split,
+                                  const int32_t* idx, const float* w, const float* x, int64_t ld_x, int64_t F_in,
+                                  const float* W, int64_t F_out, const float* bias, int flags, float gin_scale,
+                                  float* out, int64_t ld_out, float* partials, float* agg_out, int64_t ld_agg,
+                                  kgx_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  KGX_REQUIRE(reduce >= KGX_SUM && reduce <= KGX_MIN, KGX_ERR_ARG, "kgx_spmm_gemm_f256: reduce %d unsupported",
+              reduce);
+  KGX_REQUIRE(F_in == kF, KGX_ERR_UNSUPPORTED, "kgx_spmm_gemm_f256: F_in must be %d (got %lld)", kF,
+              (long long)F_in);
+  KGX_REQUIRE(F_out > 0 && F_out <= kF && F_out % 16 == 0, KGX_ERR_UNSUPPORTED,
+              "kgx_spmm_gemm_f256: F_out must be a multiple of 16 <= 256 (got %lld)", (long long)F_out);
+  KGX_REQUIRE(n_rows >= 0 && n_items >= 0 && n_split >= 0, KGX_ERR_ARG, "kgx_spmm_gemm_f256: negative size");
+  KGX_REQUIRE((flags & ~(KGX_FUSED_PRE_GIN | KGX_FUSED_ACCUMULATE | KGX_FUSED_SHARE_GPU | KGX_FUSED_RELU)) == 0,
+              KGX_ERR_ARG, "kgx_spmm_gemm_f256: unknown flags 0x%x", flags);
+  KGX_REQUIRE(!((flags & KGX_FUSED_RELU) && (flags & KGX_FUSED_ACCUMULATE)), KGX_ERR_ARG,
+              "kgx_spmm_gemm_f256: KGX_FUSED_RELU cannot be combined with KGX_FUSED_ACCUMULATE");
+  KGX_REQUIRE(!agg_out || (ld_agg >= F_in && reinterpret_cast<uintptr_t>(agg_out) % 16 == 0 && ld_agg % 4 == 0),
+              KGX_ERR_ARG, "kgx_spmm_gemm_f256: agg_out must be 16-byte aligned with ld >= F_in, ld %% 4 == 0");
+  if (n_rows == 0) return KGX_OK;
+  KGX_REQUIRE(rowptr && rows && idx && x && W && out, KGX_ERR_ARG, "kgx_spmm_gemm_f256: null pointer");
+  KGX_REQUIRE(ld_x < (int64_t(1) << 31), KGX_ERR_ARG, "kgx_spmm_gemm_f256: x leading dimension >= 2^31");
+  KGX_REQUIRE(ld_x % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0, KGX_ERR_ARG,
+              "kgx_spmm_gemm_f256: x must be 16-byte aligned with ld %% 4 == 0");
+  KGX_REQUIRE(ld_out >= F_out && ld_out % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0, KGX_ERR_ARG,
+              "kgx_spmm_gemm_f256: out must be 16-byte aligned with ld >= F_out, ld %% 4 == 0");
+  KGX_REQUIRE(!items || n_split == 0 || (split && partials), KGX_ERR_ARG,
+              "kgx_spmm_gemm_f256: split rows need split list and partials");
+  F256Args a{};
+  a.rowptr = rowptr;
+  a.rows = rows;
+  a.n_rows = n_rows;
+  a.items = reinterpret_cast<const int4*>(items);
+  a.n_items = items ? n_items : 0;
+  a.split = reinterpret_cast<const int4*>(split);
+  a.n_split = items ? n_split : 0;
+  a.idx = idx;
+  a.w = w;
+  a.x = x;
+  a.ld_x = ld_x;
+  a.W = W;
+  a.F_out = int(F_out);
+  a.bias = bias;
+  a.out = out;
+  a.ld_o = ld_out;
+  a.partials = partials;
+  a.agg_out = agg_out;
+  a.ld_agg = ld_agg;
+  a.pre_gin = (flags & KGX_FUSED_PRE_GIN) != 0;
+  a.accumulate = (flags & KGX_FUSED_ACCUMULATE) != 0;
+  a.relu = (flags & KGX_FUSED_RELU) != 0;
+  a.gin_scale = gin_scale;
+  const bool wt = w != nullptr;
+  switch (reduce) {
+    case KGX_SUM: return wt ? launch256<KGX_SUM, true>(a, stream) : launch256<KGX_SUM, false>(a, stream);
+    case KGX_MEAN: return wt ? launch256<KGX_MEAN, true>(a, stream) : launch256<KGX_MEAN, false>(a, stream);
+    case KGX_MAX: return wt ? launch256<KGX_MAX, true>(a, stream) : launch256<KGX_MAX, false>(a, stream);
+    default: return wt ? launch256<KGX_MIN, true>(a, stream) : launch256<KGX_MIN, false>(a, stream);
+  }
+}

@@ -78,7 +78,7 @@ class KgxBackend:
         return G.split_by_source_ranges(g, cuts, accumulate_from=1)
 
     def supports_fused(self, f_in: int, f_out: int) -> bool:
-        return kops.fused_transform_supported(f_in, f_out)
+        return kops.fused_transform_supported(f_in, f_out, two_table=True)  # the sharded passes' gathers
 
     def aggregate_transform(self, g, x, W, bias=None, out=None, x2=None, accumulate=True):
         """GCN sum with the edge weights, then @ W (+ bias); out += ... if given

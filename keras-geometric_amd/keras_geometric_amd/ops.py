@@ -203,6 +203,29 @@ def _x2_args(x, x2):
     return nat.ptr(x2), x.shape[0]
 
 
+F256 = 256  # F_in of kgx_spmm_gemm_f256 (GINConv C4: 256 -> 256)
+# layers take the 256-wide fused kernel by default only while it beats the
+# unfused pair (kgx_spmm + kgx_dense) at C4; KGX_FUSED256=1 forces it
+_F256_DEFAULT = "0"
+
+
+def _f256_call(reduce, rowptr, rows, n_dst, items, n_items, split, n_split, idx, w, x, x2, W, bias, flags, gin_scale,
+               out, partials, agg, dev):
+    """kgx_spmm_gemm_f256: the 256-wide fused kernel takes every item of the
+    schedule (no short / tiny tail kernels, no second table)."""
+    if x2 is not None:
+        raise NotImplementedError("spmm_gemm: two-table gathers are implemented for F_in = 128")
+    nat.check(
+        nat.lib().kgx_spmm_gemm_f256(
+            reduce, nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, nat.ptr(split), n_split,
+            nat.ptr(idx), nat.ptr(w), nat.ptr(x), x.stride(0), x.shape[1], nat.ptr(W), W.shape[1], nat.ptr(bias),
+            flags, float(gin_scale), nat.ptr(out), out.stride(0), nat.ptr(partials),
+            nat.ptr(agg), agg.stride(0) if agg is not None else 0, nat.stream(dev),
+        ),
+        "kgx_spmm_gemm_f256",
+    )
+
+
 def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale, save_agg,
                     relu=False, n_long=-1, tpack=None, tw=None, n_short_end=-1, n_tiny2=0, x2=None):
     x, w, W, bias, x2 = _f32c(x), _f32c(w), _f32c(W), _f32c(bias), _f32c(x2)
@@ -218,6 +241,11 @@ def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, b
     partials = None
     if items is not None and n_split > 0:
         partials = torch.empty((n_slots, x.shape[1]), dtype=torch.float32, device=dev)
+    flags = int(pre_gin) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0) | (nat.FUSED_RELU if relu else 0)
+    if x.shape[1] == F256:
+        _f256_call(reduce, rowptr, rows, n_dst, items, n_items, split, n_split, idx, w, x, x2, W, bias, flags,
+                   gin_scale, out, partials, agg if save_agg else None, dev)
+        return out, agg
     n_long = n_items if n_long < 0 or n_long > n_items else n_long
     n_se, tpack, tw, n_tiny2 = _tiny_abi(items, n_items, n_long, tpack, tw if w is not None else None, n_short_end,
                                          n_tiny2)
@@ -227,8 +255,7 @@ def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, b
             reduce, nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, n_long, n_se, nat.ptr(tpack),
             nat.ptr(tw), n_tiny2, nat.ptr(split), n_split,
             nat.ptr(idx), nat.ptr(w), nat.ptr(x), x.stride(0), x2p, n_x1, x.shape[1], nat.ptr(W), F_out, nat.ptr(bias),
-            int(pre_gin) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0) | (nat.FUSED_RELU if relu else 0),
-            float(gin_scale), nat.ptr(out), out.stride(0),
+            flags, float(gin_scale), nat.ptr(out), out.stride(0),
             nat.ptr(partials),
             nat.ptr(agg) if save_agg else None, agg.stride(0) if save_agg else 0, nat.stream(dev),
         ),
@@ -341,6 +368,11 @@ def spmm_gemm_acc_(
     partials = None
     if items is not None and n_split > 0:
         partials = torch.empty((n_slots, x.shape[1]), dtype=torch.float32, device=dev)
+    if x.shape[1] == F256:
+        _f256_call(reduce, rowptr, rows, n_dst, items, n_items, split, n_split, idx, w, x, x2, W, bias,
+                   (nat.FUSED_ACCUMULATE if accumulate else 0) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0), 1.0,
+                   out, partials, None, dev)
+        return
     n_long = n_items if n_long < 0 or n_long > n_items else n_long
     n_se, tpack, tw, n_tiny2 = _tiny_abi(items, n_items, n_long, tpack, tw if w is not None else None, n_short_end,
                                          n_tiny2)
@@ -362,13 +394,16 @@ def _spmm_gemm_acc_fake(out, x, rowptr, rows, items, split, idx, w, n_slots, red
     return None
 
 
-def fused_transform_supported(f_in: int, f_out: int) -> bool:
-    """Shapes kgx_spmm_gemm implements (aggregate-then-transform is also only
-    worth it when F_in <= F_out)."""
+def fused_transform_supported(f_in: int, f_out: int, two_table: bool = False) -> bool:
+    """Shapes kgx_spmm_gemm (F_in 128) and kgx_spmm_gemm_f256 (F_in 256; one
+    table) implement (aggregate-then-transform is also only worth it when
+    F_in <= F_out)."""
     import os
 
     if os.environ.get("KGX_FUSED", "1") in ("0", "false", "False"):
         return False
+    if f_in == F256 and not two_table:
+        return f_out == F256 and os.environ.get("KGX_FUSED256", _F256_DEFAULT) not in ("0", "false", "False")
     return f_in == 128 and f_out % 16 == 0 and 0 < f_out <= 128 and f_in <= f_out
 
 
