@@ -38,6 +38,11 @@ constexpr int kColBlocks = 16;     // 16-column blocks of F_out: two per wave
 constexpr int kThreads = kWaves * 64;
 constexpr int kLd = kF + 8;        // LDS plane row (bf16): +16 B keeps the B-fragment reads conflict-free
 constexpr int kSteps = kF / 32;    // k-steps of 32 per MFMA chain
+// cost-decomposition builds only (make variant NAME=.. DEFS=-DKGX_F256_DBG=n; changes results):
+// 1 = no MFMAs / fragment reads, 2 = no output stores, 4 = every gather reads row 0 (cache hits)
+#ifndef KGX_F256_DBG
+#define KGX_F256_DBG 0
+#endif
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short bf16x8_t __attribute__((ext_vector_type(8)));
@@ -50,6 +55,10 @@ struct F256Args {
   int64_t n_rows;
   const int4* items;  // {row, beg, end, slot}
   int64_t n_items;
+  int64_t n_work;     // items [0, n_work) to spmm_gemm256_kernel; [n_work, n_items) are the tiny records' rows
+  const int4* tpack;  // [n_tiny] {row, degree <= 2, col0, col1}
+  const float2* tw;   // [n_tiny] {w0, w1} (weighted)
+  int64_t n_tiny;
   const int4* split;  // {row, first slot, chunks, degree}
   int64_t n_split;
   const int32_t* idx;
@@ -78,34 +87,16 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int RED, bool WEIGHTED>
-__global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_kernel(F256Args a) {
-  using R = RowRed<RED>;
-#ifdef KGX_F256_U
-  constexpr int U = KGX_F256_U;
-#else
-  constexpr int U = 4;  // gathers in flight per row in the two-row loop (8 per wave)
-#endif
-  constexpr int PF = 4;  // first edges of each row gathered ahead, during the previous tile's MFMAs
-  __shared__ u32x4_t wlo[kColBlocks * kSteps * 64];                    // W lo-plane B-fragments, 128 KB
-  __shared__ __attribute__((aligned(16))) short tile3[3][kRows][kLd];  // hi / mid / lo planes of the tile's rows
-  __shared__ __attribute__((aligned(16))) float sbias[kF];
-  __shared__ int32_t tile_row[kRows];
-
-  const int wave = threadIdx.x >> 6;  // reduces tile rows 2 wave, 2 wave + 1; owns output columns [32 wave, +32)
-  const int wl = threadIdx.x & 63;
-  const int f = wl * 4;
-  const int cl = wl & 15;
-  const int q = wl >> 4;
-  const bool mf0 = 32 * wave < a.F_out, mf1 = 32 * wave + 16 < a.F_out;  // column blocks 2 wave, 2 wave + 1
-
-  // W fragments, k permuted: k-step s of lane group q covers k = 64 q + 8 s + j
-  // (j = 0..7), so each x fragment is 8 contiguous bf16 of a tile row
-  bf16x8_t wfh[2][kSteps], wfm[2][kSteps];
+// W fragments of this wave's two 16-column blocks, k permuted: k-step s of lane
+// group q covers k = 64 q + 8 s + j (j = 0..7), so each x fragment is 8
+// contiguous bf16 of a tile row.  hi / mid planes to registers, lo to LDS.
+__device__ __forceinline__ void load_w(const F256Args& a, int wave, int wl, bf16x8_t (&wfh)[2][kSteps],
+                                       bf16x8_t (&wfm)[2][kSteps], u32x4_t* wlo) {
+  const int cl = wl & 15, q = wl >> 4;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int n_col = 32 * wave + 16 * i + cl;
-    const bool on = i ? mf1 : mf0;
+    const bool on = n_col < a.F_out;  // F_out % 16 == 0: whole column blocks
 #pragma unroll
     for (int s = 0; s < kSteps; ++s) {
       u32x4_t ph, pm, pl;
@@ -125,16 +116,118 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_kernel(F256Args a) {
       wlo[((2 * wave + i) * kSteps + s) * 64 + wl] = pl;
     }
   }
+}
+
+// One aggregated row (this lane's 4 features) into the split planes of LDS tile row t.
+__device__ __forceinline__ void put_row(short (*tile3)[kRows][kLd], int t, int f, const float (&v)[4]) {
+  bf16x4_t ph, pm, pl;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    short h, m_, l;
+    split3_a(v[k], h, m_, l);
+    ph[k] = h;
+    pm[k] = m_;
+    pl[k] = l;
+  }
+  if (!split_fast_ok(v[0], v[1], v[2], v[3])) {  // inf / NaN / huge: non-finite values to the lo plane
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      short h, m_, l;
+      split3_a_lo(v[k], h, m_, l);
+      ph[k] = h;
+      pm[k] = m_;
+      pl[k] = l;
+    }
+  }
+  *reinterpret_cast<bf16x4_t*>(&tile3[0][t][f]) = ph;
+  *reinterpret_cast<bf16x4_t*>(&tile3[1][t][f]) = pm;
+  *reinterpret_cast<bf16x4_t*>(&tile3[2][t][f]) = pl;
+}
+
+// The 16-row tile in LDS times W: this wave's 32 output columns as D^T = W^T x^T
+// (six significant products per k-step, small terms first), stored from the
+// accumulators -- lane (cl, q) writes columns 32 wave + 16 i + 4 q .. + 3 of
+// tile row cl (rows with tile_row < 0 are not stored).
+// FAST (F_out = 256, no accumulate, every tile row valid): the stores are issued
+// unconditionally, so the wave's count of outstanding memory operations is the
+// same on every path and the compiler's waits stay partial (no vmcnt(0) at the
+// loop head that would drain the next tile's gathers).
+template <bool FAST = false>
+__device__ __forceinline__ void transform_tile(const F256Args& a, const short (*tile3)[kRows][kLd],
+                                               const bf16x8_t (&wfh)[2][kSteps], const bf16x8_t (&wfm)[2][kSteps],
+                                               const u32x4_t* wlo, const float* sbias, const int32_t* tile_row,
+                                               int wave, int wl) {
+  const int cl = wl & 15, q = wl >> 4;
+  const bool mf0 = FAST || 32 * wave < a.F_out, mf1 = FAST || 32 * wave + 16 < a.F_out;
+  if (!mf0) return;
+  f32x4 d[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
+#pragma unroll
+  for (int s = 0; s < ((KGX_F256_DBG & 1) ? 0 : kSteps); ++s) {
+    const int kk = 64 * q + 8 * s;
+    const bf16x8_t xh = *reinterpret_cast<const bf16x8_t*>(&tile3[0][cl][kk]);
+    const bf16x8_t xm = *reinterpret_cast<const bf16x8_t*>(&tile3[1][cl][kk]);
+    const bf16x8_t xl = *reinterpret_cast<const bf16x8_t*>(&tile3[2][cl][kk]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (i == 1 && !mf1) break;
+      const bf16x8_t wf_lo = __builtin_bit_cast(bf16x8_t, wlo[((2 * wave + i) * kSteps + s) * 64 + wl]);
+      d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[i][s], xl, d[i], 0, 0, 0);
+      d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf_lo, xh, d[i], 0, 0, 0);
+      d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfm[i][s], xm, d[i], 0, 0, 0);
+      d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[i][s], xm, d[i], 0, 0, 0);
+      d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfm[i][s], xh, d[i], 0, 0, 0);
+      d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[i][s], xh, d[i], 0, 0, 0);
+    }
+  }
+  const int rr = tile_row[cl];
+  if (!FAST && rr < 0) return;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    if (i == 1 && !mf1) break;
+    const int c4 = 32 * wave + 16 * i + 4 * q;
+    float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + c4);
+    const float4 b4 = *reinterpret_cast<const float4*>(&sbias[c4]);
+    float4 v = make_float4(d[i][0] + b4.x, d[i][1] + b4.y, d[i][2] + b4.z, d[i][3] + b4.w);
+    if (!FAST && a.accumulate) {
+      const float4 p = *dst;
+      v = make_float4(__fadd_rn(p.x, v.x), __fadd_rn(p.y, v.y), __fadd_rn(p.z, v.z), __fadd_rn(p.w, v.w));
+    }
+    if (a.relu) v = make_float4(fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f));
+    if (!(KGX_F256_DBG & 2)) *dst = v;
+  }
+}
+
+// Items [0, n_work): hub-row chunks, long rows and rows of degree 3..7 (the
+// degree <= 2 tail goes to spmm_gemm256_tiny_kernel when its records exist).
+template <int RED, bool WEIGHTED>
+__global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_kernel(F256Args a) {
+  using R = RowRed<RED>;
+#ifdef KGX_F256_U
+  constexpr int U = KGX_F256_U;
+#else
+  constexpr int U = 4;  // gathers in flight per row in the two-row loop (8 per wave)
+#endif
+  constexpr int PF = 4;  // first edges of each row gathered ahead, during the previous tile's MFMAs
+  __shared__ u32x4_t wlo[kColBlocks * kSteps * 64];                    // W lo-plane B-fragments, 128 KB
+  __shared__ __attribute__((aligned(16))) short tile3[3][kRows][kLd];  // hi / mid / lo planes of the tile's rows
+  __shared__ __attribute__((aligned(16))) float sbias[kF];
+  __shared__ int32_t tile_row[kRows];
+
+  const int wave = threadIdx.x >> 6;  // reduces tile rows 2 wave, 2 wave + 1; owns output columns [32 wave, +32)
+  const int wl = threadIdx.x & 63;
+  const int f = wl * 4;
+  bf16x8_t wfh[2][kSteps], wfm[2][kSteps];
+  load_w(a, wave, wl, wfh, wfm, wlo);
   if (threadIdx.x < kF) sbias[threadIdx.x] = (a.bias && int(threadIdx.x) < a.F_out) ? a.bias[threadIdx.x] : 0.0f;
   // (both are first read after the first tile's barrier)
 
-  const int64_t n_work = a.items ? a.n_items : a.n_rows;
+  const int64_t n_work = a.items ? a.n_work : a.n_rows;
   const int64_t stride = int64_t(gridDim.x) * kRows;
 
   int32_t row[2], beg[2], end[2], slot[2];
   int pn[2];
   float pv[2][PF][4], pw[2][PF];
-  // descriptors of items it, it + 1 and their first U gathers
+  // descriptors of items it, it + 1 and their first PF gathers
   auto fetch = [&](int64_t it) {
     int32_t c[2][PF];
 #pragma unroll
@@ -260,75 +353,134 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_kernel(F256Args a) {
         for (int k = 0; k < 4; ++k) v[k] = __fadd_rn(__fmul_rn(a.gin_scale, xv[k]), v[k]);
       }
       if (full_row && a.agg_out) vstore<4>(a.agg_out + int64_t(row[r]) * a.ld_agg + f, v);
-      bf16x4_t ph, pm, pl;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        short h, m_, l;
-        split3_a(v[k], h, m_, l);
-        ph[k] = h;
-        pm[k] = m_;
-        pl[k] = l;
-      }
-      if (!split_fast_ok(v[0], v[1], v[2], v[3])) {  // inf / NaN / huge: non-finite values to the lo plane
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          short h, m_, l;
-          split3_a_lo(v[k], h, m_, l);
-          ph[k] = h;
-          pm[k] = m_;
-          pl[k] = l;
-        }
-      }
-      *reinterpret_cast<bf16x4_t*>(&tile3[0][2 * wave + r][f]) = ph;
-      *reinterpret_cast<bf16x4_t*>(&tile3[1][2 * wave + r][f]) = pm;
-      *reinterpret_cast<bf16x4_t*>(&tile3[2][2 * wave + r][f]) = pl;
+      put_row(tile3, 2 * wave + r, f, v);
       if (wl == 0) tile_row[2 * wave + r] = full_row ? row[r] : -1;
     }
     lds_barrier();
-
     fetch(base + stride + 2 * wave);  // the next tile's first gathers fly during the MFMAs
-
-    if (mf0) {
-      f32x4 d[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
-#pragma unroll
-      for (int s = 0; s < kSteps; ++s) {
-        const int kk = 64 * q + 8 * s;
-        const bf16x8_t xh = *reinterpret_cast<const bf16x8_t*>(&tile3[0][cl][kk]);
-        const bf16x8_t xm = *reinterpret_cast<const bf16x8_t*>(&tile3[1][cl][kk]);
-        const bf16x8_t xl = *reinterpret_cast<const bf16x8_t*>(&tile3[2][cl][kk]);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          if (i == 1 && !mf1) break;
-          const bf16x8_t wf_lo = __builtin_bit_cast(bf16x8_t, wlo[((2 * wave + i) * kSteps + s) * 64 + wl]);
-          // D^T = W^T x^T; small terms first
-          d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[i][s], xl, d[i], 0, 0, 0);
-          d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf_lo, xh, d[i], 0, 0, 0);
-          d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfm[i][s], xm, d[i], 0, 0, 0);
-          d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[i][s], xm, d[i], 0, 0, 0);
-          d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfm[i][s], xh, d[i], 0, 0, 0);
-          d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[i][s], xh, d[i], 0, 0, 0);
-        }
-      }
-      // lane (cl, q) holds columns 32 wave + 16 i + 4 q .. + 3 of tile row cl
-      const int rr = tile_row[cl];
-      if (rr >= 0) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          if (i == 1 && !mf1) break;
-          const int c4 = 32 * wave + 16 * i + 4 * q;
-          float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + c4);
-          const float4 b4 = *reinterpret_cast<const float4*>(&sbias[c4]);
-          float4 v = make_float4(d[i][0] + b4.x, d[i][1] + b4.y, d[i][2] + b4.z, d[i][3] + b4.w);
-          if (a.accumulate) {
-            const float4 p = *dst;
-            v = make_float4(__fadd_rn(p.x, v.x), __fadd_rn(p.y, v.y), __fadd_rn(p.z, v.z), __fadd_rn(p.w, v.w));
-          }
-          if (a.relu) v = make_float4(fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f));
-          *dst = v;
-        }
-      }
-    }
+    transform_tile(a, tile3, wfh, wfm, wlo, sbias, tile_row, wave, wl);
     lds_barrier();  // the planes and tile_row are free for the next tile
+  }
+}
+
+// The schedule's tail of rows of degree <= 2 from packed records {row, degree,
+// col0, col1} (+ {w0, w1}; tiny.py): one 16-row MFMA tile per block iteration,
+// two rows per wave.  One dependent load per row (record -> source rows),
+// software-pipelined: while the MFMAs of tile t run, tile t+1's source rows
+// (and, with the GIN epilogue, its x_i rows) are in flight and tile t+2's
+// records are loaded.  Loads are unconditional (col1 = col0 for degree 1, 0 for
+// degree 0 and past the end; masked at the fold) and, with FAST, so are the
+// stores of every full tile: the memory-operation count per iteration is
+// path-independent, so the waits before the fold are partial.
+template <int RED, bool WEIGHTED, bool GIN, bool FAST>
+__global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny_kernel(F256Args a) {
+  using R = RowRed<RED>;
+  constexpr int RPW = 2;  // rows per wave per tile
+  __shared__ u32x4_t wlo[kColBlocks * kSteps * 64];
+  __shared__ __attribute__((aligned(16))) short tile3[3][kRows][kLd];
+  __shared__ __attribute__((aligned(16))) float sbias[kF];
+  __shared__ int32_t tile_row[kRows];
+
+  const int wave = threadIdx.x >> 6;
+  const int wl = threadIdx.x & 63;
+  const int f = wl * 4;
+  bf16x8_t wfh[2][kSteps], wfm[2][kSteps];
+  load_w(a, wave, wl, wfh, wfm, wlo);
+  if (threadIdx.x < kF) sbias[threadIdx.x] = (a.bias && int(threadIdx.x) < a.F_out) ? a.bias[threadIdx.x] : 0.0f;
+
+  const int64_t n = a.n_tiny;
+  const int64_t stride = int64_t(gridDim.x) * kRows;
+  // two pipeline stages: the rows (id, degree) and gathers of tiles t+1 and
+  // t+2 are in flight while tile t is folded and transformed; two record
+  // buffers: body(S) loads tile t+3's records into rec[S] BEFORE issuing tile
+  // t+2's gathers from rec[S^1] (loaded a tile ago), so waiting for a record
+  // never waits for the gathers issued after it (memory counters are in order)
+  int32_t rid[2][RPW], rdeg[2][RPW];
+  float pv[2][RPW][2][4], px[2][RPW][4], pw[2][RPW][2];
+  int4 rec[2][RPW];
+  float2 rw[2][RPW];
+  bool rval[2][RPW];
+  auto load_rec = [&](auto BT, int64_t it) {  // records of rows it, it + 1 (clamped load, marked past the end)
+    constexpr int B = decltype(BT)::value;
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      rval[B][r] = it + r < n;
+      const int64_t i = rval[B][r] ? it + r : n - 1;
+      rec[B][r] = a.tpack[i];
+      if constexpr (WEIGHTED) rw[B][r] = a.tw[i];
+    }
+  };
+  auto issue = [&](auto ST, auto BT) {  // gathers of the rows in rec[B] into stage S
+    constexpr int S = decltype(ST)::value;
+    constexpr int B = decltype(BT)::value;
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      rid[S][r] = rval[B][r] ? rec[B][r].x : -1;
+      rdeg[S][r] = rval[B][r] ? rec[B][r].y : 0;
+      if constexpr (WEIGHTED) {
+        pw[S][r][0] = rw[B][r].x;
+        pw[S][r][1] = rw[B][r].y;
+      }
+      constexpr int Z = (KGX_F256_DBG & 4) ? 0 : 1;
+      vload<4>(pv[S][r][0], a.x + row_off(Z * rec[B][r].z, a.ld_x) + f);
+      vload<4>(pv[S][r][1], a.x + row_off(Z * rec[B][r].w, a.ld_x) + f);
+      if constexpr (GIN) vload<4>(px[S][r], a.x + row_off(Z * rec[B][r].x, a.ld_x) + f);
+    }
+  };
+  // one tile over rows [base, base + 16) from stage S: FULL = every row valid (FAST stores)
+  auto body = [&](auto ST, auto FULLTAG, int64_t base) {
+    constexpr int S = decltype(ST)::value;
+    constexpr bool FULL = decltype(FULLTAG)::value;
+    load_rec(ST, base + 3 * stride + RPW * wave);  // tile t+3's records
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      float val[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float acc = R::init();
+        const float m0 = WEIGHTED ? __fmul_rn(pv[S][r][0][k], pw[S][r][0]) : pv[S][r][0][k];
+        const float m1 = WEIGHTED ? __fmul_rn(pv[S][r][1][k], pw[S][r][1]) : pv[S][r][1][k];
+        acc = R::combine(acc, rdeg[S][r] > 0 ? R::msg(m0) : R::init());
+        acc = R::combine(acc, rdeg[S][r] > 1 ? R::msg(m1) : R::init());
+        float v = R::finish(acc, rdeg[S][r]);
+        if constexpr (GIN) v = __fadd_rn(__fmul_rn(a.gin_scale, px[S][r][k]), v);
+        val[k] = rid[S][r] >= 0 ? v : 0.0f;
+      }
+      if (!FAST && rid[S][r] >= 0 && a.agg_out) vstore<4>(a.agg_out + int64_t(rid[S][r]) * a.ld_agg + f, val);
+      put_row(tile3, RPW * wave + r, f, val);
+      if (wl == 0) tile_row[RPW * wave + r] = rid[S][r];
+    }
+    lds_barrier();
+    issue(ST, std::integral_constant<int, S ^ 1>{});  // tile t+2's rows, from the records loaded a tile ago
+    transform_tile<FAST && FULL>(a, tile3, wfh, wfm, wlo, sbias, tile_row, wave, wl);
+    lds_barrier();
+  };
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+
+  const int64_t first = int64_t(blockIdx.x) * kRows + RPW * wave;
+  load_rec(S0{}, first);
+  issue(S0{}, S0{});
+  load_rec(S0{}, first + stride);
+  issue(S1{}, S0{});
+  load_rec(S1{}, first + 2 * stride);
+  int64_t base = int64_t(blockIdx.x) * kRows;
+  int par = 0;
+  for (;;) {
+    if (base + kRows > n) break;
+    body(S0{}, std::true_type{}, base);
+    base += stride;
+    par = 1;
+    if (base + kRows > n) break;
+    body(S1{}, std::true_type{}, base);
+    base += stride;
+    par = 0;
+  }
+  if (base < n) {  // the one partial tile (last block only)
+    if (par == 0)
+      body(S0{}, std::false_type{}, base);
+    else
+      body(S1{}, std::false_type{}, base);
   }
 }
 
@@ -386,17 +538,27 @@ __global__ __launch_bounds__(256) void spmm_gemm256_fixup_kernel(F256Args a) {
   }
 }
 
+template <typename K>
+unsigned grid256(K k, int64_t tiles) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, 0) != hipSuccess || per_cu <= 0) per_cu = 1;
+  const int64_t cap = int64_t(per_cu) * cu_count();
+  return unsigned(tiles < cap ? tiles : cap);
+}
+
 template <int RED, bool WT>
 int launch256(const F256Args& a, hipStream_t s) {
-  const int64_t work = a.items ? a.n_items : a.n_rows;
+  const int64_t work = a.items ? a.n_work : a.n_rows;
   if (work > 0) {
     auto k = spmm_gemm256_kernel<RED, WT>;
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, 0) != hipSuccess || per_cu <= 0)
-      per_cu = 1;
-    const int64_t cap = int64_t(per_cu) * cu_count();
-    const int64_t need = (work + kRows - 1) / kRows;
-    hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL(k, dim3(grid256(k, (work + kRows - 1) / kRows)), dim3(kThreads), 0, s, a);
+    KGX_CHECK_LAUNCH();
+  }
+  if (a.tpack && a.n_tiny > 0) {
+    const bool fast = a.F_out == kF && !a.accumulate && !a.agg_out;
+    auto k = a.pre_gin ? (fast ? spmm_gemm256_tiny_kernel<RED, WT, true, true> : spmm_gemm256_tiny_kernel<RED, WT, true, false>)
+                       : (fast ? spmm_gemm256_tiny_kernel<RED, WT, false, true> : spmm_gemm256_tiny_kernel<RED, WT, false, false>);
+    hipLaunchKernelGGL(k, dim3(grid256(k, (a.n_tiny + kRows - 1) / kRows)), dim3(kThreads), 0, s, a);
     KGX_CHECK_LAUNCH();
   }
   if (a.items && a.n_split > 0) {
@@ -414,7 +576,8 @@ int launch256(const F256Args& a, hipStream_t s) {
 using namespace kgx;
 
 extern "C" int kgx_spmm_gemm_f256(int reduce, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
-                                  const int32_t* items, int64_t n_items, const int32_t* split, int64_t n_split,
+                                  const int32_t* items, int64_t n_items, int64_t n_short_end,
+                                  const int32_t* tiny_pack, const float* tiny_w, const int32_t* split, int64_t n_split,
                                   const int32_t* idx, const float* w, const float* x, int64_t ld_x, int64_t F_in,
                                   const float* W, int64_t F_out, const float* bias, int flags, float gin_scale,
                                   float* out, int64_t ld_out, float* partials, float* agg_out, int64_t ld_agg,
@@ -427,6 +590,11 @@ extern "C" int kgx_spmm_gemm_f256(int reduce, const int32_t* rowptr, const int32
   KGX_REQUIRE(F_out > 0 && F_out <= kF && F_out % 16 == 0, KGX_ERR_UNSUPPORTED,
               "kgx_spmm_gemm_f256: F_out must be a multiple of 16 <= 256 (got %lld)", (long long)F_out);
   KGX_REQUIRE(n_rows >= 0 && n_items >= 0 && n_split >= 0, KGX_ERR_ARG, "kgx_spmm_gemm_f256: negative size");
+  KGX_REQUIRE(!items || tiny_pack || n_short_end == n_items, KGX_ERR_ARG,
+              "kgx_spmm_gemm_f256: without tiny_pack, n_short_end must equal n_items");
+  KGX_REQUIRE(!tiny_pack || (items && n_short_end >= 0 && n_short_end <= n_items && (w == nullptr || tiny_w)),
+              KGX_ERR_ARG, "kgx_spmm_gemm_f256: the tiny-row records need the schedule, 0 <= n_short_end <= n_items "
+              "(and weights when weighted)");
   KGX_REQUIRE((flags & ~(KGX_FUSED_PRE_GIN | KGX_FUSED_ACCUMULATE | KGX_FUSED_SHARE_GPU | KGX_FUSED_RELU)) == 0,
               KGX_ERR_ARG, "kgx_spmm_gemm_f256: unknown flags 0x%x", flags);
   KGX_REQUIRE(!((flags & KGX_FUSED_RELU) && (flags & KGX_FUSED_ACCUMULATE)), KGX_ERR_ARG,
@@ -448,6 +616,10 @@ extern "C" int kgx_spmm_gemm_f256(int reduce, const int32_t* rowptr, const int32
   a.n_rows = n_rows;
   a.items = reinterpret_cast<const int4*>(items);
   a.n_items = items ? n_items : 0;
+  a.n_work = items ? (tiny_pack ? n_short_end : n_items) : 0;
+  a.tpack = items ? reinterpret_cast<const int4*>(tiny_pack) : nullptr;
+  a.tw = reinterpret_cast<const float2*>(tiny_w);
+  a.n_tiny = (items && tiny_pack) ? n_items - n_short_end : 0;
   a.split = reinterpret_cast<const int4*>(split);
   a.n_split = items ? n_split : 0;
   a.idx = idx;

@@ -5,10 +5,11 @@ h'_i = MLP((1+eps) * x_i + AGG_{j->i} x_j)   (gin_conv.py:216-225)
 kgx forward: ONE fused kernel gathers x_j rows, reduces (sum/mean/max) in the
 reference's edge order and applies the (1+eps)*x_i + aggr epilogue; the MLP's
 Dense layers run on kgx_dense (bf16x3-split MFMA, f32-accurate; the library
-fp32 GEMM only past its K/N <= 256 shapes).  When F_in == 128 and the MLP's first
-Dense fits the fused kernel (<= 128 units, bias, none/ReLU), that Dense runs in
-the aggregation's epilogue on MFMA too (kgx_spmm_gemm with KGX_FUSED_PRE_GIN;
-EXACT mode keeps the separate, bit-exact aggregation).
+fp32 GEMM only past its K/N <= 256 shapes).  When the MLP's first Dense fits a
+fused kernel (F_in 128 -> <= 128 units: kgx_spmm_gemm; F_in 256 -> 256 units,
+BASELINE config C4: kgx_spmm_gemm_f256; bias, none/ReLU), that Dense runs in the
+aggregation's epilogue on MFMA too (KGX_FUSED_PRE_GIN), so the [N, F_in]
+aggregate is never written; EXACT mode keeps the separate, bit-exact aggregation.
 """
 
 from __future__ import annotations

@@ -204,20 +204,22 @@ def _x2_args(x, x2):
 
 
 F256 = 256  # F_in of kgx_spmm_gemm_f256 (GINConv C4: 256 -> 256)
-# layers take the 256-wide fused kernel by default only while it beats the
-# unfused pair (kgx_spmm + kgx_dense) at C4; KGX_FUSED256=1 forces it
-_F256_DEFAULT = "0"
+# layers take the 256-wide fused kernels by default: at C4 they beat the unfused
+# pair (kgx_spmm + kgx_dense), 22.0 vs 24.5 ms; KGX_FUSED256=0 turns them off
+_F256_DEFAULT = "1"
 
 
 def _f256_call(reduce, rowptr, rows, n_dst, items, n_items, split, n_split, idx, w, x, x2, W, bias, flags, gin_scale,
-               out, partials, agg, dev):
-    """kgx_spmm_gemm_f256: the 256-wide fused kernel takes every item of the
-    schedule (no short / tiny tail kernels, no second table)."""
+               out, partials, agg, dev, tpack=None, tw=None, n_short_end=-1):
+    """kgx_spmm_gemm_f256: the 256-wide fused kernels (main + the degree <= 2
+    tail from the packed records; one feature table)."""
     if x2 is not None:
         raise NotImplementedError("spmm_gemm: two-table gathers are implemented for F_in = 128")
+    n_se, tpack, tw, _ = _tiny_abi(items, n_items, 0, tpack, tw if w is not None else None, n_short_end, 0)
     nat.check(
         nat.lib().kgx_spmm_gemm_f256(
-            reduce, nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, nat.ptr(split), n_split,
+            reduce, nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, n_se, nat.ptr(tpack), nat.ptr(tw),
+            nat.ptr(split), n_split,
             nat.ptr(idx), nat.ptr(w), nat.ptr(x), x.stride(0), x.shape[1], nat.ptr(W), W.shape[1], nat.ptr(bias),
             flags, float(gin_scale), nat.ptr(out), out.stride(0), nat.ptr(partials),
             nat.ptr(agg), agg.stride(0) if agg is not None else 0, nat.stream(dev),
@@ -244,7 +246,7 @@ def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, b
     flags = int(pre_gin) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0) | (nat.FUSED_RELU if relu else 0)
     if x.shape[1] == F256:
         _f256_call(reduce, rowptr, rows, n_dst, items, n_items, split, n_split, idx, w, x, x2, W, bias, flags,
-                   gin_scale, out, partials, agg if save_agg else None, dev)
+                   gin_scale, out, partials, agg if save_agg else None, dev, tpack, tw, n_short_end)
         return out, agg
     n_long = n_items if n_long < 0 or n_long > n_items else n_long
     n_se, tpack, tw, n_tiny2 = _tiny_abi(items, n_items, n_long, tpack, tw if w is not None else None, n_short_end,
@@ -371,7 +373,7 @@ def spmm_gemm_acc_(
     if x.shape[1] == F256:
         _f256_call(reduce, rowptr, rows, n_dst, items, n_items, split, n_split, idx, w, x, x2, W, bias,
                    (nat.FUSED_ACCUMULATE if accumulate else 0) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0), 1.0,
-                   out, partials, None, dev)
+                   out, partials, None, dev, tpack, tw, n_short_end)
         return
     n_long = n_items if n_long < 0 or n_long > n_items else n_long
     n_se, tpack, tw, n_tiny2 = _tiny_abi(items, n_items, n_long, tpack, tw if w is not None else None, n_short_end,

@@ -185,3 +185,40 @@ def test_fused256_backward(dev):
         got = got.cpu().double()
         scale = ref.abs().max().clamp_min(1.0)
         assert float((got - ref).abs().max() / scale) <= 2e-5
+
+
+@pytest.mark.parametrize("red,weighted,gin", [("sum", False, True), ("sum", True, False), ("mean", False, False),
+                                              ("max", False, True)])
+def test_fused256_tiny_tail_bit_identical(dev, red, weighted, gin):
+    """The degree <= 2 tail from the packed records (spmm_gemm256_tiny_kernel)
+    gives the same bits as the same rows through the item path: each output
+    row depends only on its own aggregated row and W."""
+    N = 40000
+    s, d = _graph(11, N, 90000)
+    rng = np.random.default_rng(11)
+    x = T(rng.standard_normal((N, F)).astype(np.float32)).to(dev)
+    W = T((rng.standard_normal((F, F)) * 0.06).astype(np.float32)).to(dev)
+    b = T(rng.standard_normal(F).astype(np.float32)).to(dev)
+    g = build(np.stack([s, d]), N, dev, self_loops=True, gcn_norm=True)
+    tpack, tw, n_se, n2 = kops._tiny_of(g, g.items)
+    assert tpack is not None and g.n_items - n_se > 20000  # most rows take the record kernel
+    w = g.w if weighted else None
+    rid = kops._reduce_id(red)
+    op = torch.ops.kgx.spmm_gemm
+    with torch.no_grad():
+        y = op(x, g.rowptr, g.rows, g.items, g.split, g.col, w, g.n_slots, rid, W, b, gin, 1.25, False, -1, tpack, tw,
+               n_se, n2)
+        y0 = op(x, g.rowptr, g.rows, g.items, g.split, g.col, w, g.n_slots, rid, W, b, gin, 1.25)
+    assert torch.equal(y, y0)
+    ei_l = R.add_self_loops(T(np.stack([s, d])), N)
+    xs = x.cpu()
+    msg = xs[ei_l[0].long()]
+    if weighted:
+        rows = np.repeat(np.arange(N), g.deg.cpu().numpy())
+        aggr = np.zeros((N, F))
+        np.add.at(aggr, rows, xs.numpy()[g.col.cpu().numpy()].astype(np.float64) * g.w.cpu().numpy()[:, None])
+    else:
+        aggr = R.aggregate(red, msg, ei_l[1], N).numpy().astype(np.float64)
+    if gin:
+        aggr = np.float32(1.25) * xs.numpy().astype(np.float64) + aggr
+    assert_dot_bound(y.cpu().numpy(), aggr, W.cpu().double().numpy(), b.cpu().double().numpy(), k_eps=3e-5)

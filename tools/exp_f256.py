@@ -44,18 +44,23 @@ def main(n=10_000_000, e=100_000_000, f=256):
     x = torch.randn(n, f, device=dev)
     W = torch.randn(f, f, device=dev) * (1.0 / f) ** 0.5
     b = torch.randn(f, device=dev)
-    short = g.items[g.n_long:].contiguous()
+    tpack, tw, n_se, n2 = kops._tiny_of(g, g.items)
     long_ = g.items[:g.n_long].contiguous()
+    mid = g.items[g.n_long:n_se].contiguous()  # unsplit rows of degree 3..7
+    tail = g.items[n_se:].contiguous()          # degree <= 2: the tiny-record kernel
     op = torch.ops.kgx.spmm_gemm
-    res = {"lib": os.path.basename(os.environ.get("KGX_LIB", "libkgx.so")), "n_long": g.n_long,
+    res = {"lib": os.path.basename(os.environ.get("KGX_LIB", "libkgx.so")), "n_long": g.n_long, "n_short_end": n_se,
            "n_items": g.n_items, "n_split": g.n_split}
     with torch.no_grad():
         res["fused_ms"] = timeit(lambda: op(x, g.rowptr, g.rows, g.items, g.split, g.col, None, g.n_slots, 0, W, b,
-                                            True, 1.25))
+                                            True, 1.25, False, -1, tpack, tw, n_se, n2))
+        res["fused_notiny_ms"] = timeit(lambda: op(x, g.rowptr, g.rows, g.items, g.split, g.col, None, g.n_slots, 0,
+                                                   W, b, True, 1.25))
         res["fused_long_ms"] = timeit(lambda: op(x, g.rowptr, g.rows, long_, g.split, g.col, None, g.n_slots, 0, W, b,
                                                  True, 1.25))
-        res["fused_short_ms"] = timeit(lambda: op(x, g.rowptr, g.rows, short, None, g.col, None, 0, 0, W, b, True,
-                                                  1.25))
+        res["fused_mid_ms"] = timeit(lambda: op(x, g.rowptr, g.rows, mid, None, g.col, None, 0, 0, W, b, True, 1.25))
+        res["fused_tiny_ms"] = timeit(lambda: op(x, g.rowptr, g.rows, tail, None, g.col, None, 0, 0, W, b, True, 1.25,
+                                                 False, -1, tpack, tw, 0, n2))
         if os.environ.get("KGX_EXP_UNFUSED", "1") == "1":
             h = kops.aggregate(g, x, "sum", epilogue=nat.EPI_GIN, xroot=x, gin_scale=1.25)
             res["unfused_agg_ms"] = timeit(lambda: kops.aggregate(g, x, "sum", epilogue=nat.EPI_GIN, xroot=x,
