@@ -1,4 +1,4 @@
-# Bench lines (PMC traffic attached from profiles/r02) for NS and the C3/C4/C5 configs.
+# Bench lines (PMC traffic attached from the newest profiles/r*) for NS and the C3/C4/C5 configs.
 set -o pipefail
 mkdir -p gpurun_out/lines
 timeout -k 10 600 python bench.py --steps 20 --warmup 3 > gpurun_out/lines/bench_ns.json 2> gpurun_out/lines/bench_ns.err || exit $?
