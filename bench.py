@@ -376,7 +376,7 @@ def main() -> None:
         balg = b_alg_spmm(n_rows, e_agg, f_in if fused else f_out, weighted=True, f_out=f_out)
         # the fused op: long rows, the short-row suffix (degree <= 7) and the hub fix-up
         kernel = ("spmm_gemm_kernel", "spmm_gemm_short_kernel", "spmm_gemm_tiny_kernel", "spmm_gemm_fixup_kernel") if fused \
-            else ("spmm_kernel", "spmm_fixup_kernel")
+            else ("spmm_kernel", "spmm_short_kernel", "spmm_hub_kernel", "spmm_fixup_kernel")
     elif kind == "gat":  # one pass: h_src row per edge, h_dst row + output row per node
         balg = 4 * (n_rows + 1) + e_agg * (4 + 4 * f_out) + 8 * n_rows * f_out
         kernel = ("gatv2_kernel", "gatv2_fixup_kernel")
@@ -387,7 +387,7 @@ def main() -> None:
         kernel = ("spmm_gemm256_kernel", "spmm_gemm256_tiny_kernel", "spmm_gemm256_fixup_kernel")
     else:  # GIN: + the x_i root row of the (1+eps) x_i + aggr epilogue; SAGE mean: plain gather-sum
         balg = b_alg_spmm(n_rows, e_agg, f_in, weighted=False) + (4 * n_rows * f_in if kind == "gin" else 0)
-        kernel = ("spmm_kernel", "spmm_fixup_kernel")
+        kernel = ("spmm_kernel", "spmm_short_kernel", "spmm_fixup_kernel")
     achieved = balg / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
     mine = {"rank": rank, "e_agg": e_agg, "rows": n_rows, "ms_per_step": elapsed / args.steps * 1e3,
             "aggregation_ms": kern_ms, "launches_per_step": launches, "roofline_achieved_GBps": achieved,
