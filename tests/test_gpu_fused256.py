@@ -209,7 +209,14 @@ def test_fused256_tiny_tail_bit_identical(dev, red, weighted, gin):
         y = op(x, g.rowptr, g.rows, g.items, g.split, g.col, w, g.n_slots, rid, W, b, gin, 1.25, False, -1, tpack, tw,
                n_se, n2)
         y0 = op(x, g.rowptr, g.rows, g.items, g.split, g.col, w, g.n_slots, rid, W, b, gin, 1.25)
+        # the saved-aggregate form (training forward: agg_out stores, non-FAST tail)
+        ys, agg = torch.ops.kgx.spmm_gemm_save(x, g.rowptr, g.rows, g.items, g.split, g.col, w, g.n_slots, rid, W, b,
+                                               gin, 1.25, -1, tpack, tw, n_se, n2)
+        want = kops.aggregate(g, x, red, weighted=weighted, epilogue=nat.EPI_GIN if gin else nat.EPI_NONE,
+                              xroot=x if gin else None, gin_scale=1.25)
     assert torch.equal(y, y0)
+    assert torch.equal(ys, y)
+    assert torch.equal(agg, want)
     ei_l = R.add_self_loops(T(np.stack([s, d])), N)
     xs = x.cpu()
     msg = xs[ei_l[0].long()]
