@@ -71,3 +71,25 @@ def test_cache_key_tracks_version():
     t[0, 0] = 1
     assert G.cache_key(t, 1) != k1
     assert G.cache_key(np.zeros((2, 4)), 1) is None
+
+
+def test_fused_shape_routing(monkeypatch):
+    """Which shapes take a fused aggregate -> transform kernel: F_in 128 ->
+    128 (kgx_spmm_gemm), 256 -> 256 (kgx_spmm_gemm_f256, one table only:
+    the sharded passes' two-table gathers stay on F_in 128); KGX_FUSED256=0 /
+    KGX_FUSED=0 turn them off."""
+    from keras_geometric_amd import ops as kops
+
+    monkeypatch.delenv("KGX_FUSED", raising=False)
+    monkeypatch.delenv("KGX_FUSED256", raising=False)
+    assert kops.fused_transform_supported(128, 128)
+    assert not kops.fused_transform_supported(128, 64)  # F_out < F_in: transform first, gather the narrower rows
+    assert not kops.fused_transform_supported(128, 256)  # F_in <= F_out but the 128 kernel stops at 128
+    assert kops.fused_transform_supported(256, 256)
+    assert not kops.fused_transform_supported(256, 128)  # transform first: narrower rows to gather
+    assert not kops.fused_transform_supported(256, 256, two_table=True)
+    assert kops.fused_transform_supported(128, 128, two_table=True)
+    monkeypatch.setenv("KGX_FUSED256", "0")
+    assert not kops.fused_transform_supported(256, 256) and kops.fused_transform_supported(128, 128)
+    monkeypatch.setenv("KGX_FUSED", "0")
+    assert not kops.fused_transform_supported(128, 128)
