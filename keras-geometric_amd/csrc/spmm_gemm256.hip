@@ -43,6 +43,10 @@ constexpr int kSteps = kF / 32;    // k-steps of 32 per MFMA chain
 #ifndef KGX_F256_DBG
 #define KGX_F256_DBG 0
 #endif
+// degree <= 2 tail kernel: 1 = spmm_gemm256_tiny_kernel, 2 = the double-buffered spmm_gemm256_tiny2_kernel
+#ifndef KGX_F256_TINY
+#define KGX_F256_TINY 2
+#endif
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short bf16x8_t __attribute__((ext_vector_type(8)));
@@ -119,29 +123,26 @@ __device__ __forceinline__ void load_w(const F256Args& a, int wave, int wl, bf16
 }
 
 // One aggregated row (this lane's 4 features) into the split planes of LDS tile row t.
+// Fast path: split3_pair_rn (three packed conversions per pair, equal to
+// split3_a whenever both bf16 values are finite, which split_fast_ok checks);
+// otherwise the per-value split3_a_lo (non-finite values to the lo plane).
 __device__ __forceinline__ void put_row(short (*tile3)[kRows][kLd], int t, int f, const float (&v)[4]) {
-  bf16x4_t ph, pm, pl;
+  uint32_t h0, m0, l0, h1, m1, l1;
+  split3_pair_rn(v[0], v[1], h0, m0, l0);
+  split3_pair_rn(v[2], v[3], h1, m1, l1);
+  uint2 ph = make_uint2(h0, h1), pm = make_uint2(m0, m1), pl = make_uint2(l0, l1);
+  if (!split_fast_ok(v[0], v[1], v[2], v[3])) {  // inf / NaN / huge
+    short h[4], m_[4], l[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    short h, m_, l;
-    split3_a(v[k], h, m_, l);
-    ph[k] = h;
-    pm[k] = m_;
-    pl[k] = l;
+    for (int k = 0; k < 4; ++k) split3_a_lo(v[k], h[k], m_[k], l[k]);
+    auto pk = [](short a, short b) { return uint32_t(uint16_t(a)) | (uint32_t(uint16_t(b)) << 16); };
+    ph = make_uint2(pk(h[0], h[1]), pk(h[2], h[3]));
+    pm = make_uint2(pk(m_[0], m_[1]), pk(m_[2], m_[3]));
+    pl = make_uint2(pk(l[0], l[1]), pk(l[2], l[3]));
   }
-  if (!split_fast_ok(v[0], v[1], v[2], v[3])) {  // inf / NaN / huge: non-finite values to the lo plane
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      short h, m_, l;
-      split3_a_lo(v[k], h, m_, l);
-      ph[k] = h;
-      pm[k] = m_;
-      pl[k] = l;
-    }
-  }
-  *reinterpret_cast<bf16x4_t*>(&tile3[0][t][f]) = ph;
-  *reinterpret_cast<bf16x4_t*>(&tile3[1][t][f]) = pm;
-  *reinterpret_cast<bf16x4_t*>(&tile3[2][t][f]) = pl;
+  *reinterpret_cast<uint2*>(&tile3[0][t][f]) = ph;
+  *reinterpret_cast<uint2*>(&tile3[1][t][f]) = pm;
+  *reinterpret_cast<uint2*>(&tile3[2][t][f]) = pl;
 }
 
 // The 16-row tile in LDS times W: this wave's 32 output columns as D^T = W^T x^T
@@ -484,6 +485,211 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny_kernel(F256Args
   }
 }
 
+// Tail kernel, double-buffered form (KGX_F256_TINY = 2, the default).  W's lo
+// plane is split: k-steps 0..3 in 32 VGPRs, 4..7 in 64 KB of LDS, which leaves
+// room for two 16-row plane tiles.  One barrier per tile period: in period t
+// every wave runs tile t's MFMAs (buffer t & 1) and prepares tile t+1 (fold,
+// split, planes into buffer (t+1) & 1, then issues tile t+2's gathers and
+// loads tile t+3's records).  Waves 0-3 run the MFMAs first, waves 4-7 the
+// preparation first, so the two waves sharing a SIMD keep its matrix pipe and
+// its VALU busy at the same time.  One gather stage: tile t+2's rows are issued
+// right after tile t+1's are folded and have a whole period to land.
+template <int RED, bool WEIGHTED, bool GIN, bool FAST>
+__global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Args a) {
+  using R = RowRed<RED>;
+  constexpr int RPW = 2;  // rows per wave per tile
+  constexpr int kHalf = kSteps / 2;
+  __shared__ u32x4_t wlo[kColBlocks * kHalf * 64];                        // lo plane, k-steps 4..7: 64 KB
+  __shared__ __attribute__((aligned(16))) short tile3[2][3][kRows][kLd];  // two tiles of hi / mid / lo planes
+  __shared__ __attribute__((aligned(16))) float sbias[kF];
+  __shared__ int32_t tile_row[2][kRows];
+
+  const int wave = threadIdx.x >> 6;
+  const int wl = threadIdx.x & 63;
+  const int f = wl * 4;
+  const int cl = wl & 15, q = wl >> 4;
+  bf16x8_t wfh[2][kSteps], wfm[2][kSteps], wfl[2][kHalf];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int n_col = 32 * wave + 16 * i + cl;
+    const bool on = n_col < a.F_out;
+#pragma unroll
+    for (int st = 0; st < kSteps; ++st) {
+      u32x4_t ph, pm, pl;
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        const int k = 64 * q + 8 * st + j;
+        const float v0 = on ? a.W[int64_t(k) * a.F_out + n_col] : 0.0f;
+        const float v1 = on ? a.W[int64_t(k + 1) * a.F_out + n_col] : 0.0f;
+        uint32_t h, m_, l;
+        split3_pair(v0, v1, h, m_, l);
+        ph[j / 2] = h;
+        pm[j / 2] = m_;
+        pl[j / 2] = l;
+      }
+      wfh[i][st] = __builtin_bit_cast(bf16x8_t, ph);
+      wfm[i][st] = __builtin_bit_cast(bf16x8_t, pm);
+      if (st < kHalf)
+        wfl[i][st] = __builtin_bit_cast(bf16x8_t, pl);
+      else
+        wlo[((2 * wave + i) * kHalf + st - kHalf) * 64 + wl] = pl;
+    }
+  }
+  if (threadIdx.x < kF) sbias[threadIdx.x] = (a.bias && int(threadIdx.x) < a.F_out) ? a.bias[threadIdx.x] : 0.0f;
+
+  const int64_t n = a.n_tiny;
+  const int64_t stride = int64_t(gridDim.x) * kRows;
+  int32_t rid[RPW], rdeg[RPW];
+  float pv[RPW][2][4], px[RPW][4], pw[RPW][2];
+  int4 rec[2][RPW];
+  float2 rw[2][RPW];
+  bool rval[2][RPW];
+  auto load_rec = [&](int b, int64_t it) {  // records of rows it, it + 1 into buffer b (clamped, marked when used)
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const bool v = it + r < n;
+      const int64_t i = v ? it + r : n - 1;
+      if (b == 0) {
+        rval[0][r] = v;
+        rec[0][r] = a.tpack[i];
+        if constexpr (WEIGHTED) rw[0][r] = a.tw[i];
+      } else {
+        rval[1][r] = v;
+        rec[1][r] = a.tpack[i];
+        if constexpr (WEIGHTED) rw[1][r] = a.tw[i];
+      }
+    }
+  };
+  auto issue = [&](auto BT) {  // the gathers of the rows in record buffer B (one dependent load each)
+    constexpr int B = decltype(BT)::value;
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      rid[r] = rval[B][r] ? rec[B][r].x : -1;
+      rdeg[r] = rval[B][r] ? rec[B][r].y : 0;
+      if constexpr (WEIGHTED) {
+        pw[r][0] = rw[B][r].x;
+        pw[r][1] = rw[B][r].y;
+      }
+      vload<4>(pv[r][0], a.x + row_off(rec[B][r].z, a.ld_x) + f);
+      vload<4>(pv[r][1], a.x + row_off(rec[B][r].w, a.ld_x) + f);
+      if constexpr (GIN) vload<4>(px[r], a.x + row_off(rec[B][r].x, a.ld_x) + f);
+    }
+  };
+  // fold the gathered rows, split them into plane buffer pb; tile_row too
+  auto put = [&](int pb) {
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      float val[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float acc = R::init();
+        const float m0 = WEIGHTED ? __fmul_rn(pv[r][0][k], pw[r][0]) : pv[r][0][k];
+        const float m1 = WEIGHTED ? __fmul_rn(pv[r][1][k], pw[r][1]) : pv[r][1][k];
+        acc = R::combine(acc, rdeg[r] > 0 ? R::msg(m0) : R::init());
+        acc = R::combine(acc, rdeg[r] > 1 ? R::msg(m1) : R::init());
+        float v = R::finish(acc, rdeg[r]);
+        if constexpr (GIN) v = __fadd_rn(__fmul_rn(a.gin_scale, px[r][k]), v);
+        val[k] = rid[r] >= 0 ? v : 0.0f;
+      }
+      if (!FAST && rid[r] >= 0 && a.agg_out) vstore<4>(a.agg_out + int64_t(rid[r]) * a.ld_agg + f, val);
+      put_row(tile3[pb], RPW * wave + r, f, val);
+      if (wl == 0) tile_row[pb][RPW * wave + r] = rid[r];
+    }
+  };
+  // tile in plane buffer pb times W; FASTS = unconditional stores (every row valid)
+  auto mfma = [&](auto FT, int pb) {
+    constexpr bool FASTS = decltype(FT)::value;
+    const short(*t3)[kRows][kLd] = tile3[pb];
+    const bool mf0 = FASTS || 32 * wave < a.F_out, mf1 = FASTS || 32 * wave + 16 < a.F_out;
+    if (!mf0) return;
+    f32x4 d[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
+#pragma unroll
+    for (int st = 0; st < ((KGX_F256_DBG & 1) ? 0 : kSteps); ++st) {
+      const int kk = 64 * q + 8 * st;
+      const bf16x8_t xh = *reinterpret_cast<const bf16x8_t*>(&t3[0][cl][kk]);
+      const bf16x8_t xm = *reinterpret_cast<const bf16x8_t*>(&t3[1][cl][kk]);
+      const bf16x8_t xl = *reinterpret_cast<const bf16x8_t*>(&t3[2][cl][kk]);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        if (i == 1 && !mf1) break;
+        const bf16x8_t wf_lo = st < kHalf ? wfl[i][st < kHalf ? st : 0]
+                                          : __builtin_bit_cast(bf16x8_t, wlo[((2 * wave + i) * kHalf + (st >= kHalf ? st - kHalf : 0)) * 64 + wl]);
+        d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[i][st], xl, d[i], 0, 0, 0);
+        d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf_lo, xh, d[i], 0, 0, 0);
+        d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfm[i][st], xm, d[i], 0, 0, 0);
+        d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[i][st], xm, d[i], 0, 0, 0);
+        d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfm[i][st], xh, d[i], 0, 0, 0);
+        d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[i][st], xh, d[i], 0, 0, 0);
+      }
+    }
+    const int rr = tile_row[pb][cl];
+    if (!FASTS && rr < 0) return;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (i == 1 && !mf1) break;
+      const int c4 = 32 * wave + 16 * i + 4 * q;
+      float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + c4);
+      const float4 b4 = *reinterpret_cast<const float4*>(&sbias[c4]);
+      float4 v = make_float4(d[i][0] + b4.x, d[i][1] + b4.y, d[i][2] + b4.z, d[i][3] + b4.w);
+      if (!FASTS && a.accumulate) {
+        const float4 p = *dst;
+        v = make_float4(__fadd_rn(p.x, v.x), __fadd_rn(p.y, v.y), __fadd_rn(p.z, v.z), __fadd_rn(p.w, v.w));
+      }
+      if (a.relu) v = make_float4(fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f));
+      if (!(KGX_F256_DBG & 2)) *dst = v;
+    }
+  };
+  // period t (parity p): tile t's MFMAs; tile t+1 folded into buffer p^1; tile
+  // t+2's gathers issued from record buffer p; tile t+3's records into buffer p^1
+  const bool mfma_first = wave < kWaves / 2;
+  auto period = [&](auto FT, auto PT, int64_t base) {
+    constexpr int P = decltype(PT)::value;
+    auto prep = [&]() {
+      put(P ^ 1);
+      issue(std::integral_constant<int, P>{});
+      load_rec(P ^ 1, base + 3 * stride + RPW * wave);
+    };
+    if (mfma_first) {
+      mfma(FT, P);
+      prep();
+    } else {
+      prep();
+      mfma(FT, P);
+    }
+    lds_barrier();
+  };
+  using P0 = std::integral_constant<int, 0>;
+  using P1 = std::integral_constant<int, 1>;
+
+  const int64_t first = int64_t(blockIdx.x) * kRows + RPW * wave;
+  // prologue: tile 0 into plane buffer 0, tile 1's gathers in flight, tile 2's records loaded
+  load_rec(0, first);
+  issue(P0{});
+  load_rec(1, first + stride);
+  put(0);
+  issue(P1{});
+  load_rec(0, first + 2 * stride);
+  lds_barrier();
+  int64_t base = int64_t(blockIdx.x) * kRows;
+  int par = 0;
+  for (;;) {
+    if (base + kRows > n) break;
+    period(std::integral_constant<bool, FAST>{}, P0{}, base);
+    base += stride;
+    par = 1;
+    if (base + kRows > n) break;
+    period(std::integral_constant<bool, FAST>{}, P1{}, base);
+    base += stride;
+    par = 0;
+  }
+  if (base < n) {  // the one partial tile (last block only)
+    if (par == 0)
+      period(std::false_type{}, P0{}, base);
+    else
+      period(std::false_type{}, P1{}, base);
+  }
+}
+
 // Split hub rows: combine the chunk partials in order, finish, PRE, then
 // out = v @ W + b in f32 on the VALU (a few thousand rows per graph).
 template <int RED>
@@ -556,8 +762,13 @@ int launch256(const F256Args& a, hipStream_t s) {
   }
   if (a.tpack && a.n_tiny > 0) {
     const bool fast = a.F_out == kF && !a.accumulate && !a.agg_out;
+#if KGX_F256_TINY == 1
     auto k = a.pre_gin ? (fast ? spmm_gemm256_tiny_kernel<RED, WT, true, true> : spmm_gemm256_tiny_kernel<RED, WT, true, false>)
                        : (fast ? spmm_gemm256_tiny_kernel<RED, WT, false, true> : spmm_gemm256_tiny_kernel<RED, WT, false, false>);
+#else
+    auto k = a.pre_gin ? (fast ? spmm_gemm256_tiny2_kernel<RED, WT, true, true> : spmm_gemm256_tiny2_kernel<RED, WT, true, false>)
+                       : (fast ? spmm_gemm256_tiny2_kernel<RED, WT, false, true> : spmm_gemm256_tiny2_kernel<RED, WT, false, false>);
+#endif
     hipLaunchKernelGGL(k, dim3(grid256(k, (a.n_tiny + kRows - 1) / kRows)), dim3(kThreads), 0, s, a);
     KGX_CHECK_LAUNCH();
   }
