@@ -384,7 +384,8 @@ def main() -> None:
         # fused (1+eps) x_i + aggr -> Dense (kgx_spmm_gemm_f256): gathered rows F_in wide, the x_i root row,
         # output rows F_out wide; no [N, F_in] intermediate
         balg = b_alg_spmm(n_rows, e_agg, f_in, weighted=False, f_out=f_out) + 4 * n_rows * f_in
-        kernel = ("spmm_gemm256_kernel", "spmm_gemm256_tiny_kernel", "spmm_gemm256_fixup_kernel")
+        kernel = ("spmm_gemm256_kernel", "spmm_gemm256_tiny2_kernel", "spmm_gemm256_tiny_kernel",
+                  "spmm_gemm256_fixup_kernel")
     else:  # GIN: + the x_i root row of the (1+eps) x_i + aggr epilogue; SAGE mean: plain gather-sum
         balg = b_alg_spmm(n_rows, e_agg, f_in, weighted=False) + (4 * n_rows * f_in if kind == "gin" else 0)
         kernel = ("spmm_kernel", "spmm_short_kernel", "spmm_fixup_kernel")
