@@ -8,19 +8,20 @@
 // HBM traffic at 10M rows); here each aggregated row goes from registers to
 // LDS to the matrix cores and only the transformed row is written.
 //
-// Block = 1024 threads = 16 waves, one block per CU.  Per tile the block takes
-// 16 consecutive schedule items; wave w reduces item w's edges with 64 lanes x
-// float4 (one 1-KB row per gather, 4 gathers in flight, sequential RN adds as
-// in spmm_kernel) and writes the row, split three ways into bf16 hi/mid/lo
-// planes, to an LDS tile.  Then wave w computes output columns [16w, 16w + 16)
-// of the 16-row tile as D^T = W^T x^T with 48 v_mfma_f32_16x16x32_bf16 (the six
-// significant cross products of the split operands over K = 256; f32-accurate,
-// kgx_bf16x3.h).  W's split planes take 384 KB: the hi and mid B-fragments of a
-// wave's 16 columns live in 64 VGPRs for the whole kernel, the lo plane (used
-// by one product of the six) in 128 KB of LDS, read once per k-step.  The next
-// tile's first gathers are issued before the MFMA phase (LDS-only barriers keep
-// them in flight).  Hub-row chunks write raw partials; the fix-up kernel
-// combines them in order and applies W in f32 on the VALU.
+// Block = 512 threads = 8 waves (2 per SIMD, 256 VGPRs each), one block per CU.
+// Per tile the block takes 16 consecutive schedule items; wave w reduces items
+// 2w, 2w+1 with 64 lanes x float4 (one 1-KB row per gather, both rows' edges in
+// flight together, sequential RN adds as in spmm_kernel) and writes the rows,
+// split three ways into bf16 hi/mid/lo planes, to an LDS tile.  Then wave w
+// computes output columns [32w, 32w + 32) of the 16-row tile as D^T = W^T x^T
+// with 96 v_mfma_f32_16x16x32_bf16 (the six significant cross products of the
+// split operands over K = 256; f32-accurate, kgx_bf16x3.h).  W's split planes
+// take 384 KB: the hi and mid B-fragments of a wave's 32 columns live in 128
+// VGPRs for the whole kernel, the lo plane (used by one product of the six) in
+// 128 KB of LDS, read once per k-step.  The next tile's first gathers are
+// issued before the MFMA phase (LDS-only barriers keep them in flight).  Hub-row
+// chunks write raw partials; the fix-up kernel combines them in order and
+// applies W in f32 on the VALU.  The degree <= 2 tail has its own kernel below.
 #include <cstdlib>
 
 #include "kgx_bf16x3.h"
@@ -42,10 +43,6 @@ constexpr int kSteps = kF / 32;    // k-steps of 32 per MFMA chain
 // 1 = no MFMAs / fragment reads, 2 = no output stores, 4 = every gather reads row 0 (cache hits)
 #ifndef KGX_F256_DBG
 #define KGX_F256_DBG 0
-#endif
-// degree <= 2 tail kernel: 1 = spmm_gemm256_tiny_kernel, 2 = the double-buffered spmm_gemm256_tiny2_kernel
-#ifndef KGX_F256_TINY
-#define KGX_F256_TINY 2
 #endif
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -149,17 +146,12 @@ __device__ __forceinline__ void put_row(short (*tile3)[kRows][kLd], int t, int f
 // (six significant products per k-step, small terms first), stored from the
 // accumulators -- lane (cl, q) writes columns 32 wave + 16 i + 4 q .. + 3 of
 // tile row cl (rows with tile_row < 0 are not stored).
-// FAST (F_out = 256, no accumulate, every tile row valid): the stores are issued
-// unconditionally, so the wave's count of outstanding memory operations is the
-// same on every path and the compiler's waits stay partial (no vmcnt(0) at the
-// loop head that would drain the next tile's gathers).
-template <bool FAST = false>
 __device__ __forceinline__ void transform_tile(const F256Args& a, const short (*tile3)[kRows][kLd],
                                                const bf16x8_t (&wfh)[2][kSteps], const bf16x8_t (&wfm)[2][kSteps],
                                                const u32x4_t* wlo, const float* sbias, const int32_t* tile_row,
                                                int wave, int wl) {
   const int cl = wl & 15, q = wl >> 4;
-  const bool mf0 = FAST || 32 * wave < a.F_out, mf1 = FAST || 32 * wave + 16 < a.F_out;
+  const bool mf0 = 32 * wave < a.F_out, mf1 = 32 * wave + 16 < a.F_out;
   if (!mf0) return;
   f32x4 d[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
 #pragma unroll
@@ -181,7 +173,7 @@ __device__ __forceinline__ void transform_tile(const F256Args& a, const short (*
     }
   }
   const int rr = tile_row[cl];
-  if (!FAST && rr < 0) return;
+  if (rr < 0) return;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     if (i == 1 && !mf1) break;
@@ -189,7 +181,7 @@ __device__ __forceinline__ void transform_tile(const F256Args& a, const short (*
     float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + c4);
     const float4 b4 = *reinterpret_cast<const float4*>(&sbias[c4]);
     float4 v = make_float4(d[i][0] + b4.x, d[i][1] + b4.y, d[i][2] + b4.z, d[i][3] + b4.w);
-    if (!FAST && a.accumulate) {
+    if (a.accumulate) {
       const float4 p = *dst;
       v = make_float4(__fadd_rn(p.x, v.x), __fadd_rn(p.y, v.y), __fadd_rn(p.z, v.z), __fadd_rn(p.w, v.w));
     }
@@ -199,7 +191,7 @@ __device__ __forceinline__ void transform_tile(const F256Args& a, const short (*
 }
 
 // Items [0, n_work): hub-row chunks, long rows and rows of degree 3..7 (the
-// degree <= 2 tail goes to spmm_gemm256_tiny_kernel when its records exist).
+// degree <= 2 tail goes to spmm_gemm256_tiny2_kernel when its records exist).
 template <int RED, bool WEIGHTED>
 __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_kernel(F256Args a) {
   using R = RowRed<RED>;
@@ -364,128 +356,8 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_kernel(F256Args a) {
   }
 }
 
-// The schedule's tail of rows of degree <= 2 from packed records {row, degree,
-// col0, col1} (+ {w0, w1}; tiny.py): one 16-row MFMA tile per block iteration,
-// two rows per wave.  One dependent load per row (record -> source rows),
-// software-pipelined: while the MFMAs of tile t run, tile t+1's source rows
-// (and, with the GIN epilogue, its x_i rows) are in flight and tile t+2's
-// records are loaded.  Loads are unconditional (col1 = col0 for degree 1, 0 for
-// degree 0 and past the end; masked at the fold) and, with FAST, so are the
-// stores of every full tile: the memory-operation count per iteration is
-// path-independent, so the waits before the fold are partial.
-template <int RED, bool WEIGHTED, bool GIN, bool FAST>
-__global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny_kernel(F256Args a) {
-  using R = RowRed<RED>;
-  constexpr int RPW = 2;  // rows per wave per tile
-  __shared__ u32x4_t wlo[kColBlocks * kSteps * 64];
-  __shared__ __attribute__((aligned(16))) short tile3[3][kRows][kLd];
-  __shared__ __attribute__((aligned(16))) float sbias[kF];
-  __shared__ int32_t tile_row[kRows];
-
-  const int wave = threadIdx.x >> 6;
-  const int wl = threadIdx.x & 63;
-  const int f = wl * 4;
-  bf16x8_t wfh[2][kSteps], wfm[2][kSteps];
-  load_w(a, wave, wl, wfh, wfm, wlo);
-  if (threadIdx.x < kF) sbias[threadIdx.x] = (a.bias && int(threadIdx.x) < a.F_out) ? a.bias[threadIdx.x] : 0.0f;
-
-  const int64_t n = a.n_tiny;
-  const int64_t stride = int64_t(gridDim.x) * kRows;
-  // two pipeline stages: the rows (id, degree) and gathers of tiles t+1 and
-  // t+2 are in flight while tile t is folded and transformed; two record
-  // buffers: body(S) loads tile t+3's records into rec[S] BEFORE issuing tile
-  // t+2's gathers from rec[S^1] (loaded a tile ago), so waiting for a record
-  // never waits for the gathers issued after it (memory counters are in order)
-  int32_t rid[2][RPW], rdeg[2][RPW];
-  float pv[2][RPW][2][4], px[2][RPW][4], pw[2][RPW][2];
-  int4 rec[2][RPW];
-  float2 rw[2][RPW];
-  bool rval[2][RPW];
-  auto load_rec = [&](auto BT, int64_t it) {  // records of rows it, it + 1 (clamped load, marked past the end)
-    constexpr int B = decltype(BT)::value;
-#pragma unroll
-    for (int r = 0; r < RPW; ++r) {
-      rval[B][r] = it + r < n;
-      const int64_t i = rval[B][r] ? it + r : n - 1;
-      rec[B][r] = a.tpack[i];
-      if constexpr (WEIGHTED) rw[B][r] = a.tw[i];
-    }
-  };
-  auto issue = [&](auto ST, auto BT) {  // gathers of the rows in rec[B] into stage S
-    constexpr int S = decltype(ST)::value;
-    constexpr int B = decltype(BT)::value;
-#pragma unroll
-    for (int r = 0; r < RPW; ++r) {
-      rid[S][r] = rval[B][r] ? rec[B][r].x : -1;
-      rdeg[S][r] = rval[B][r] ? rec[B][r].y : 0;
-      if constexpr (WEIGHTED) {
-        pw[S][r][0] = rw[B][r].x;
-        pw[S][r][1] = rw[B][r].y;
-      }
-      constexpr int Z = (KGX_F256_DBG & 4) ? 0 : 1;
-      vload<4>(pv[S][r][0], a.x + row_off(Z * rec[B][r].z, a.ld_x) + f);
-      vload<4>(pv[S][r][1], a.x + row_off(Z * rec[B][r].w, a.ld_x) + f);
-      if constexpr (GIN) vload<4>(px[S][r], a.x + row_off(Z * rec[B][r].x, a.ld_x) + f);
-    }
-  };
-  // one tile over rows [base, base + 16) from stage S: FULL = every row valid (FAST stores)
-  auto body = [&](auto ST, auto FULLTAG, int64_t base) {
-    constexpr int S = decltype(ST)::value;
-    constexpr bool FULL = decltype(FULLTAG)::value;
-    load_rec(ST, base + 3 * stride + RPW * wave);  // tile t+3's records
-#pragma unroll
-    for (int r = 0; r < RPW; ++r) {
-      float val[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float acc = R::init();
-        const float m0 = WEIGHTED ? __fmul_rn(pv[S][r][0][k], pw[S][r][0]) : pv[S][r][0][k];
-        const float m1 = WEIGHTED ? __fmul_rn(pv[S][r][1][k], pw[S][r][1]) : pv[S][r][1][k];
-        acc = R::combine(acc, rdeg[S][r] > 0 ? R::msg(m0) : R::init());
-        acc = R::combine(acc, rdeg[S][r] > 1 ? R::msg(m1) : R::init());
-        float v = R::finish(acc, rdeg[S][r]);
-        if constexpr (GIN) v = __fadd_rn(__fmul_rn(a.gin_scale, px[S][r][k]), v);
-        val[k] = rid[S][r] >= 0 ? v : 0.0f;
-      }
-      if (!FAST && rid[S][r] >= 0 && a.agg_out) vstore<4>(a.agg_out + int64_t(rid[S][r]) * a.ld_agg + f, val);
-      put_row(tile3, RPW * wave + r, f, val);
-      if (wl == 0) tile_row[RPW * wave + r] = rid[S][r];
-    }
-    lds_barrier();
-    issue(ST, std::integral_constant<int, S ^ 1>{});  // tile t+2's rows, from the records loaded a tile ago
-    transform_tile<FAST && FULL>(a, tile3, wfh, wfm, wlo, sbias, tile_row, wave, wl);
-    lds_barrier();
-  };
-  using S0 = std::integral_constant<int, 0>;
-  using S1 = std::integral_constant<int, 1>;
-
-  const int64_t first = int64_t(blockIdx.x) * kRows + RPW * wave;
-  load_rec(S0{}, first);
-  issue(S0{}, S0{});
-  load_rec(S0{}, first + stride);
-  issue(S1{}, S0{});
-  load_rec(S1{}, first + 2 * stride);
-  int64_t base = int64_t(blockIdx.x) * kRows;
-  int par = 0;
-  for (;;) {
-    if (base + kRows > n) break;
-    body(S0{}, std::true_type{}, base);
-    base += stride;
-    par = 1;
-    if (base + kRows > n) break;
-    body(S1{}, std::true_type{}, base);
-    base += stride;
-    par = 0;
-  }
-  if (base < n) {  // the one partial tile (last block only)
-    if (par == 0)
-      body(S0{}, std::false_type{}, base);
-    else
-      body(S1{}, std::false_type{}, base);
-  }
-}
-
-// Tail kernel, double-buffered form (KGX_F256_TINY = 2, the default).  W's lo
+// The schedule's tail of rows of degree <= 2, from the packed records {row,
+// degree, col0, col1} (+ {w0, w1}; tiny.py), double-buffered.  W's lo
 // plane is split: k-steps 0..3 in 32 VGPRs, 4..7 in 64 KB of LDS, which leaves
 // room for two 16-row plane tiles.  One barrier per tile period: in period t
 // every wave runs tile t's MFMAs (buffer t & 1) and prepares tile t+1 (fold,
@@ -493,7 +365,13 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny_kernel(F256Args
 // loads tile t+3's records).  Waves 0-3 run the MFMAs first, waves 4-7 the
 // preparation first, so the two waves sharing a SIMD keep its matrix pipe and
 // its VALU busy at the same time.  One gather stage: tile t+2's rows are issued
-// right after tile t+1's are folded and have a whole period to land.
+// right after tile t+1's are folded and have a whole period to land.  Loads are
+// unconditional (col1 = col0 for degree 1, 0 for degree 0 and past the end;
+// masked at the fold), records are marked past the end only where used (a
+// select right after the load would make hipcc wait for it), and with FAST
+// (F_out = 256, no accumulate, no saved aggregate) every full tile's stores are
+// unconditional too: the count of memory operations in flight is then the same
+// on every path, so the compiler's waits before a fold stay partial.
 template <int RED, bool WEIGHTED, bool GIN, bool FAST>
 __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Args a) {
   using R = RowRed<RED>;
@@ -762,13 +640,8 @@ int launch256(const F256Args& a, hipStream_t s) {
   }
   if (a.tpack && a.n_tiny > 0) {
     const bool fast = a.F_out == kF && !a.accumulate && !a.agg_out;
-#if KGX_F256_TINY == 1
-    auto k = a.pre_gin ? (fast ? spmm_gemm256_tiny_kernel<RED, WT, true, true> : spmm_gemm256_tiny_kernel<RED, WT, true, false>)
-                       : (fast ? spmm_gemm256_tiny_kernel<RED, WT, false, true> : spmm_gemm256_tiny_kernel<RED, WT, false, false>);
-#else
     auto k = a.pre_gin ? (fast ? spmm_gemm256_tiny2_kernel<RED, WT, true, true> : spmm_gemm256_tiny2_kernel<RED, WT, true, false>)
                        : (fast ? spmm_gemm256_tiny2_kernel<RED, WT, false, true> : spmm_gemm256_tiny2_kernel<RED, WT, false, false>);
-#endif
     hipLaunchKernelGGL(k, dim3(grid256(k, (a.n_tiny + kRows - 1) / kRows)), dim3(kThreads), 0, s, a);
     KGX_CHECK_LAUNCH();
   }
