@@ -370,6 +370,8 @@ def main() -> None:
     launches = len(events) // args.steps
 
     fused = kind == "gcn" and not args.exact and kops.fused_transform_supported(f_in, f_out)
+    # GINConv's (1+eps) x_i + aggr -> Dense in one launch (1 GPU; the sharded passes stay unfused)
+    fused_gin = kind == "gin" and world == 1 and not args.exact and kops.fused_transform_supported(f_in, f_out)
     if kind == "gcn":
         # SURVEY.md §8d per rank; at N>1 the accumulating halo-chunk passes' re-reads
         # of the rows they add to are implementation overhead, not algorithmic bytes
@@ -380,7 +382,7 @@ def main() -> None:
     elif kind == "gat":  # one pass: h_src row per edge, h_dst row + output row per node
         balg = 4 * (n_rows + 1) + e_agg * (4 + 4 * f_out) + 8 * n_rows * f_out
         kernel = ("gatv2_kernel", "gatv2_fixup_kernel")
-    elif kind == "gin" and world == 1 and not args.exact and kops.fused_transform_supported(f_in, f_out):
+    elif fused_gin:
         # fused (1+eps) x_i + aggr -> Dense (kgx_spmm_gemm_f256): gathered rows F_in wide, the x_i root row,
         # output rows F_out wide; no [N, F_in] intermediate
         balg = b_alg_spmm(n_rows, e_agg, f_in, weighted=False, f_out=f_out) + 4 * n_rows * f_in
@@ -452,7 +454,8 @@ def main() -> None:
             "max_in_degree": max_deg,
             "features": [f_in, f_out],
             "mode": ("exact" if args.exact else "split-hub")
-                    + (", fused aggregate->transform (W on bf16x3-split MFMA, f32-accurate)" if fused else ""),
+                    + (", fused aggregate->transform (W on bf16x3-split MFMA, f32-accurate)" if fused or fused_gin
+                       else ""),
             "parallelism": f"dst-shard{world}" if world > 1 else "single",
         },
         "edges_per_s_aggregation_kernel": e_total / (kern_ms * 1e-3) if kern_ms > 0 else None,
