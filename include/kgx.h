@@ -277,12 +277,14 @@ int kgx_spmm_gemm_ex3(int reduce, const int32_t* rowptr, const int32_t* rows, in
  * (1+eps) x + aggr -> Dense at BASELINE config C4 (gin_conv.py:216-225,
  * 129-162) and GCNConv 256 -> 256 (gcn_conv.py:233-272) without the [N, 256]
  * aggregate written and read back.  Items [0, n_short_end) go to the main
- * kernel; with tiny_pack, the schedule's tail [n_short_end, n_items) of rows of
+ * kernel (as two launches when 0 <= n_long_items < n_short_end: the hub chunks
+ * and rows of degree > KGX_SHORT_ROW_MAX first, then the rows of degree <=
+ * KGX_SHORT_ROW_MAX, gathered whole a tile ahead; -1: one launch); with tiny_pack, the schedule's tail [n_short_end, n_items) of rows of
  * degree <= 2 comes from the packed records of kgx_spmm_gemm_ex2 (tiny_pack
  * NULL: n_short_end must equal n_items).  One feature table; same flags,
  * argument meaning and error behaviour as kgx_spmm_gemm. */
 int kgx_spmm_gemm_f256(int reduce, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
-                       const int32_t* items, int64_t n_items, int64_t n_short_end,
+                       const int32_t* items, int64_t n_items, int64_t n_long_items, int64_t n_short_end,
                        const int32_t* tiny_pack, const float* tiny_w, const int32_t* split, int64_t n_split,
                        const int32_t* idx, const float* w, const float* x, int64_t ld_x, int64_t F_in,
                        const float* W, int64_t F_out, const float* bias, int flags, float gin_scale,

@@ -57,6 +57,7 @@ struct F256Args {
   const int4* items;  // {row, beg, end, slot}
   int64_t n_items;
   int64_t n_work;     // items [0, n_work) to spmm_gemm256_kernel; [n_work, n_items) are the tiny records' rows
+  int64_t n_long;     // items [0, n_long): hub chunks and rows of degree > 7 (-1: not given)
   const int4* tpack;  // [n_tiny] {row, degree <= 2, col0, col1}
   const float2* tw;   // [n_tiny] {w0, w1} (weighted)
   int64_t n_tiny;
@@ -192,7 +193,14 @@ __device__ __forceinline__ void transform_tile(const F256Args& a, const short (*
 
 // Items [0, n_work): hub-row chunks, long rows and rows of degree 3..7 (the
 // degree <= 2 tail goes to spmm_gemm256_tiny2_kernel when its records exist).
-template <int RED, bool WEIGHTED>
+// PF = edges per row gathered ahead, during the previous tile's MFMAs: 4 for the
+// long rows; KGX_F256_MID_PF for the schedule's rows of degree 3..7 (a second
+// launch over items [n_long, n_work)), most of which are then gathered whole a
+// tile ahead.
+#ifndef KGX_F256_MID_PF
+#define KGX_F256_MID_PF 6
+#endif
+template <int RED, bool WEIGHTED, int PF>
 __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_kernel(F256Args a) {
   using R = RowRed<RED>;
 #ifdef KGX_F256_U
@@ -200,7 +208,6 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_kernel(F256Args a) {
 #else
   constexpr int U = 4;  // gathers in flight per row in the two-row loop (8 per wave)
 #endif
-  constexpr int PF = 4;  // first edges of each row gathered ahead, during the previous tile's MFMAs
   __shared__ u32x4_t wlo[kColBlocks * kSteps * 64];                    // W lo-plane B-fragments, 128 KB
   __shared__ __attribute__((aligned(16))) short tile3[3][kRows][kLd];  // hi / mid / lo planes of the tile's rows
   __shared__ __attribute__((aligned(16))) float sbias[kF];
@@ -633,9 +640,22 @@ unsigned grid256(K k, int64_t tiles) {
 template <int RED, bool WT>
 int launch256(const F256Args& a, hipStream_t s) {
   const int64_t work = a.items ? a.n_work : a.n_rows;
-  if (work > 0) {
-    auto k = spmm_gemm256_kernel<RED, WT>;
-    hipLaunchKernelGGL(k, dim3(grid256(k, (work + kRows - 1) / kRows)), dim3(kThreads), 0, s, a);
+  // long rows and hub chunks [0, n_long), then the rows of degree 3..7 [n_long, n_work)
+  const int64_t n_long = (a.items && a.n_long >= 0 && a.n_long < work) ? a.n_long : work;
+  if (n_long > 0) {
+    F256Args b = a;
+    b.n_work = n_long;
+    if (!a.items) b.n_rows = n_long;
+    auto k = spmm_gemm256_kernel<RED, WT, 4>;
+    hipLaunchKernelGGL(k, dim3(grid256(k, (n_long + kRows - 1) / kRows)), dim3(kThreads), 0, s, b);
+    KGX_CHECK_LAUNCH();
+  }
+  if (work > n_long) {
+    F256Args b = a;
+    b.items = a.items + n_long;
+    b.n_work = work - n_long;
+    auto k = spmm_gemm256_kernel<RED, WT, KGX_F256_MID_PF>;
+    hipLaunchKernelGGL(k, dim3(grid256(k, (b.n_work + kRows - 1) / kRows)), dim3(kThreads), 0, s, b);
     KGX_CHECK_LAUNCH();
   }
   if (a.tpack && a.n_tiny > 0) {
@@ -660,7 +680,7 @@ int launch256(const F256Args& a, hipStream_t s) {
 using namespace kgx;
 
 extern "C" int kgx_spmm_gemm_f256(int reduce, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
-                                  const int32_t* items, int64_t n_items, int64_t n_short_end,
+                                  const int32_t* items, int64_t n_items, int64_t n_long_items, int64_t n_short_end,
                                   const int32_t* tiny_pack, const float* tiny_w, const int32_t* split, int64_t n_split,
                                   const int32_t* idx, const float* w, const float* x, int64_t ld_x, int64_t F_in,
                                   const float* W, int64_t F_out, const float* bias, int flags, float gin_scale,
@@ -701,6 +721,7 @@ extern "C" int kgx_spmm_gemm_f256(int reduce, const int32_t* rowptr, const int32
   a.items = reinterpret_cast<const int4*>(items);
   a.n_items = items ? n_items : 0;
   a.n_work = items ? (tiny_pack ? n_short_end : n_items) : 0;
+  a.n_long = items ? n_long_items : -1;
   a.tpack = items ? reinterpret_cast<const int4*>(tiny_pack) : nullptr;
   a.tw = reinterpret_cast<const float2*>(tiny_w);
   a.n_tiny = (items && tiny_pack) ? n_items - n_short_end : 0;

@@ -82,7 +82,7 @@ _SIGNATURES = {
         _f32p, _i64, _f32p, _f32p, _i64, ctypes.c_void_p,
     ],
     "kgx_spmm_gemm_f256": [
-        _int, _i32p, _i32p, _i64, _i32p, _i64, _i64, _i32p, _f32p, _i32p, _i64,
+        _int, _i32p, _i32p, _i64, _i32p, _i64, _i64, _i64, _i32p, _f32p, _i32p, _i64,
         _i32p, _f32p, _f32p, _i64, _i64, _f32p, _i64, _f32p, _int, ctypes.c_float,
         _f32p, _i64, _f32p, _f32p, _i64, ctypes.c_void_p,
     ],

@@ -210,7 +210,7 @@ _F256_DEFAULT = "1"
 
 
 def _f256_call(reduce, rowptr, rows, n_dst, items, n_items, split, n_split, idx, w, x, x2, W, bias, flags, gin_scale,
-               out, partials, agg, dev, tpack=None, tw=None, n_short_end=-1):
+               out, partials, agg, dev, tpack=None, tw=None, n_short_end=-1, n_long=-1):
     """kgx_spmm_gemm_f256: the 256-wide fused kernels (main + the degree <= 2
     tail from the packed records; one feature table)."""
     if x2 is not None:
@@ -218,7 +218,8 @@ def _f256_call(reduce, rowptr, rows, n_dst, items, n_items, split, n_split, idx,
     n_se, tpack, tw, _ = _tiny_abi(items, n_items, 0, tpack, tw if w is not None else None, n_short_end, 0)
     nat.check(
         nat.lib().kgx_spmm_gemm_f256(
-            reduce, nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, n_se, nat.ptr(tpack), nat.ptr(tw),
+            reduce, nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items,
+            n_long if items is not None and 0 <= n_long <= n_se else -1, n_se, nat.ptr(tpack), nat.ptr(tw),
             nat.ptr(split), n_split,
             nat.ptr(idx), nat.ptr(w), nat.ptr(x), x.stride(0), x.shape[1], nat.ptr(W), W.shape[1], nat.ptr(bias),
             flags, float(gin_scale), nat.ptr(out), out.stride(0), nat.ptr(partials),
@@ -246,7 +247,7 @@ def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, b
     flags = int(pre_gin) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0) | (nat.FUSED_RELU if relu else 0)
     if x.shape[1] == F256:
         _f256_call(reduce, rowptr, rows, n_dst, items, n_items, split, n_split, idx, w, x, x2, W, bias, flags,
-                   gin_scale, out, partials, agg if save_agg else None, dev, tpack, tw, n_short_end)
+                   gin_scale, out, partials, agg if save_agg else None, dev, tpack, tw, n_short_end, n_long)
         return out, agg
     n_long = n_items if n_long < 0 or n_long > n_items else n_long
     n_se, tpack, tw, n_tiny2 = _tiny_abi(items, n_items, n_long, tpack, tw if w is not None else None, n_short_end,
@@ -373,7 +374,7 @@ def spmm_gemm_acc_(
     if x.shape[1] == F256:
         _f256_call(reduce, rowptr, rows, n_dst, items, n_items, split, n_split, idx, w, x, x2, W, bias,
                    (nat.FUSED_ACCUMULATE if accumulate else 0) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0), 1.0,
-                   out, partials, None, dev, tpack, tw, n_short_end)
+                   out, partials, None, dev, tpack, tw, n_short_end, n_long)
         return
     n_long = n_items if n_long < 0 or n_long > n_items else n_long
     n_se, tpack, tw, n_tiny2 = _tiny_abi(items, n_items, n_long, tpack, tw if w is not None else None, n_short_end,

@@ -53,12 +53,13 @@ def main(n=10_000_000, e=100_000_000, f=256):
            "n_items": g.n_items, "n_split": g.n_split}
     with torch.no_grad():
         res["fused_ms"] = timeit(lambda: op(x, g.rowptr, g.rows, g.items, g.split, g.col, None, g.n_slots, 0, W, b,
-                                            True, 1.25, False, -1, tpack, tw, n_se, n2))
+                                            True, 1.25, False, g.n_long, tpack, tw, n_se, n2))
         res["fused_notiny_ms"] = timeit(lambda: op(x, g.rowptr, g.rows, g.items, g.split, g.col, None, g.n_slots, 0,
                                                    W, b, True, 1.25))
         res["fused_long_ms"] = timeit(lambda: op(x, g.rowptr, g.rows, long_, g.split, g.col, None, g.n_slots, 0, W, b,
                                                  True, 1.25))
-        res["fused_mid_ms"] = timeit(lambda: op(x, g.rowptr, g.rows, mid, None, g.col, None, 0, 0, W, b, True, 1.25))
+        res["fused_mid_ms"] = timeit(lambda: op(x, g.rowptr, g.rows, mid, None, g.col, None, 0, 0, W, b, True, 1.25,
+                                                False, 0))  # n_long = 0: the degree 3-7 launch
         res["fused_tiny_ms"] = timeit(lambda: op(x, g.rowptr, g.rows, tail, None, g.col, None, 0, 0, W, b, True, 1.25,
                                                  False, -1, tpack, tw, 0, n2))
         if os.environ.get("KGX_EXP_UNFUSED", "1") == "1":
