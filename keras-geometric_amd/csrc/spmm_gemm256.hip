@@ -369,10 +369,9 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_kernel(F256Args a) {
 // room for two 16-row plane tiles.  One barrier per tile period: in period t
 // every wave runs tile t's MFMAs (buffer t & 1) and prepares tile t+1 (fold,
 // split, planes into buffer (t+1) & 1, then issues tile t+2's gathers and
-// loads tile t+3's records).  Waves 0-3 run the MFMAs first, waves 4-7 the
-// preparation first, so the two waves sharing a SIMD keep its matrix pipe and
-// its VALU busy at the same time.  One gather stage: tile t+2's rows are issued
-// right after tile t+1's are folded and have a whole period to land.  Loads are
+// loads tile t+3's records), preparation first.  One gather stage: tile t+2's
+// rows are issued right after tile t+1's are folded and have a whole period to
+// land.  Loads are
 // unconditional (col1 = col0 for degree 1, 0 for degree 0 and past the end;
 // masked at the fold), records are marked past the end only where used (a
 // select right after the load would make hipcc wait for it), and with FAST
@@ -526,7 +525,6 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Arg
   };
   // period t (parity p): tile t's MFMAs; tile t+1 folded into buffer p^1; tile
   // t+2's gathers issued from record buffer p; tile t+3's records into buffer p^1
-  const bool mfma_first = wave < kWaves / 2;
   auto period = [&](auto FT, auto PT, int64_t base) {
     constexpr int P = decltype(PT)::value;
     auto prep = [&]() {
@@ -534,13 +532,11 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Arg
       issue(std::integral_constant<int, P>{});
       load_rec(P ^ 1, base + 3 * stride + RPW * wave);
     };
-    if (mfma_first) {
-      mfma(FT, P);
-      prep();
-    } else {
-      prep();
-      mfma(FT, P);
-    }
+    // prepare first: tile t+2's gathers are issued as early as possible and have
+    // the whole period; measured against MFMA-first and a half / half split of
+    // the waves (tools/gpu_jobs/gpu_r3_order.sh), this order was fastest
+    prep();
+    mfma(FT, P);
     lds_barrier();
   };
   using P0 = std::integral_constant<int, 0>;
