@@ -171,6 +171,14 @@ def cpu_baseline(device: torch.device, repeats: int = 3) -> dict:
     }
 
 
+def _rccl_version():
+    try:
+        v = torch.cuda.nccl.version()
+        return ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
+    except Exception:  # noqa: BLE001 -- diagnostics only
+        return None
+
+
 def _free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -236,6 +244,37 @@ def _build_sharded(kind: str, n_global: int, e_global: int, f_in: int, f_out: in
     else:
         layer = kd.ShardedSAGEConv(f_out, sg, aggregator="mean")
     return sg, x, layer
+
+
+def shard_summary(sg, kind: str, f_in: int, f_out: int, exact: bool) -> dict:
+    """This rank's exchange, as the N > 1 line reports it per rank: the process
+    group as torch.distributed reports it (backend, world size), the exchange
+    the tuner chose (kind, K, merge unit) with every candidate's agreed time and
+    the tuner's own wall time, and the halo sizes."""
+    from keras_geometric_amd import ops as kops
+
+    world = sg.world
+    pp = sg._pp  # exchange plan of the default path (None: pull-only table path or EXACT)
+    if pp is not None and pp.kind == "allgather":  # every rank's rows; this rank's own slice is not moved
+        n_moved = pp.n_rows * (world - 1) // world
+    else:
+        n_moved = pp.n_rows if pp is not None else sg.n_halo
+    # exchanged row width: X rows (F_in) on the aggregate-first paths, X W rows
+    # (F_out) when the GCN layer transforms first (shapes the fused kernel does not take)
+    transform_first = kind == "gcn" and (exact or not kops.fused_transform_supported(f_in, f_out) and f_out < f_in)
+    f_x = f_out if transform_first else f_in
+    init = dist.is_available() and dist.is_initialized()
+    return {"backend": dist.get_backend() if init else None,
+            "world_size_reported": dist.get_world_size() if init else None,
+            "exchange": pp.kind if pp is not None else "pull-table",
+            "halo_rows_pull_only": sg.n_halo, "halo_rows": n_moved,
+            "halo_rows_pushed_partials": pp.n_push if pp is not None else 0,
+            "halo_MB_per_layer": n_moved * f_x * 4 / 1e6,
+            "halo_chunks": sg.halo_k if sg.halo_k is not None else (len(pp.chunks) if pp else len(sg.chunks)),
+            "merge_unit": sg.merge_unit,
+            "exchange_tuning_s": sg.tuning,
+            "exchange_tuning_total_s": sg.tuning_s,
+            "exchange_tuning_skipped": sg.tuning_skipped}
 
 
 def main() -> None:
@@ -330,22 +369,7 @@ def main() -> None:
             with torch.no_grad():
                 return layer(x)
 
-        pp = sg._pp  # exchange plan of the default path (None: pull-only table path or EXACT)
-        if pp is not None and pp.kind == "allgather":  # every rank's rows; this rank's own slice is not moved
-            n_moved = pp.n_rows * (world - 1) // world
-        else:
-            n_moved = pp.n_rows if pp is not None else sg.n_halo
-        # exchanged row width: X rows (F_in) on the aggregate-first paths, X W rows
-        # (F_out) when the GCN layer transforms first (shapes the fused kernel does not take)
-        transform_first = kind == "gcn" and (args.exact or not kops.fused_transform_supported(f_in, f_out)
-                                             and f_out < f_in)
-        f_x = f_out if transform_first else f_in
-        shard_info = {"exchange": pp.kind if pp is not None else "pull-table",
-                      "halo_rows_pull_only": sg.n_halo, "halo_rows": n_moved,
-                      "halo_rows_pushed_partials": pp.n_push if pp is not None else 0,
-                      "halo_MB_per_layer": n_moved * f_x * 4 / 1e6,
-                      "halo_chunks": sg.halo_k if sg.halo_k is not None else (len(pp.chunks) if pp else len(sg.chunks)),
-                      "exchange_tuning_s": sg.tuning}
+        shard_info = shard_summary(sg, kind, f_in, f_out, args.exact)
 
     for _ in range(args.warmup):
         step()
@@ -473,10 +497,18 @@ def main() -> None:
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
             "traffic_source": traffic_src,
+            # FETCH_SIZE x 2 + WRITE_SIZE: L2 <-> fabric bytes, Infinity-Cache (MALL) hits included
+            "traffic_kind": "L2-fabric bytes (TCC FETCH_SIZE/WRITE_SIZE, MALL hits included)" if traffic else None,
             "algorithmic_bytes_per_launch": balg,
         },
         **({"per_rank": ranks} if ranks is not None else shard_info),
     }
+    if world > 1:  # self-diagnosing multi-GPU line: the process group as the library reports it
+        result["distributed"] = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                                 "rccl_version": _rccl_version() if dist.get_backend() == "nccl" else None,
+                                 "exchange": shard_info.get("exchange"), "halo_chunks": shard_info.get("halo_chunks"),
+                                 "merge_unit": shard_info.get("merge_unit"),
+                                 "tuning_s": max((r.get("exchange_tuning_total_s") or 0.0) for r in ranks)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and kind == "gcn" and args.config != "tiny":
         log("timing the CPU baseline (oracle, C2-sized sample)")
         del x, layer, ei

@@ -367,7 +367,8 @@ extern "C" int kgx_gatv2(const int32_t* rowptr, const int32_t* rows, int64_t n_r
       const char* h = getenv("KGX_GAT_K");
       return h ? atoi(h) : 0;
     }();
-    if (found && (kf == 4 || kf == 8 || kf == 16) && channels % kf == 0) K = kf;
+    if (found && (kf == 4 || kf == 8 || kf == 16) && channels % kf == 0 && heads * next_pow2(channels / kf) <= 64)
+      K = kf;  // same lane budget as the automatic choice
   }
   GatArgs a{};
   a.rowptr = rowptr;

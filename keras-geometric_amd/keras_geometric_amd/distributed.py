@@ -324,6 +324,8 @@ class ShardedGraph:
     tuning: dict | None = None  # K (or "exchange:K") -> slowest rank's forward seconds
     exchange: str | None = None  # "halo" / "allgather"; None: not chosen yet (push-pull halo until tuned)
     merge_unit: str | None = None  # merged_passes' unit ("step" / "chunk" / "none"); None: KGX_HALO_MERGE or "step"
+    tuning_s: float | None = None  # wall time tune_exchange took on this rank
+    tuning_skipped: int = 0  # candidates left untimed once KGX_TUNE_BUDGET_S was spent
 
     @property
     def lo(self) -> int:
@@ -641,22 +643,34 @@ class ShardedGraph:
             return self.allgather_plan(n_chunks or self.halo_k or len(self.chunks), weighted)
         return self.push_pull_plan(n_chunks, weighted)
 
-    def exchange_candidates(self, feature_bytes: int, halo_ks=(1, 2, 4), gather_ks=(1, 2, 4),
-                            units=("step", "chunk", "none")) -> list:
+    def exchange_candidates(self, halo_ks=(1, 2, 4), gather_ks=(1, 2, 4), units=("step", "chunk", "none")) -> list:
         """(exchange, K, merge unit) triples worth timing: the push-pull halo at
         each K and merge unit (merged_passes), and the all-gather when its table
-        is at most 4x the pull-only halo's bytes (weak-scaled shards, whose halo
-        is a small part of the global graph, skip it without a run).
+        (every rank's rows) is at most 4x the largest pull-only halo over the
+        ranks (weak-scaled shards, whose halo is a small part of the global
+        graph, skip it without a run).  Collective: the halo size is agreed by
+        one all-to-all (its max over ranks), so every rank lists the same
+        candidates -- tune_exchange runs their collectives in lock step.
         KGX_EXCHANGE / KGX_HALO_MERGE restrict the set."""
         fixed = os.environ.get("KGX_EXCHANGE")
         fixed_unit = os.environ.get("KGX_HALO_MERGE")
-        units = (fixed_unit,) if fixed_unit else units
-        cands = [("halo", k, u) for k in halo_ks for u in units]
-        if fixed == "allgather" or (fixed is None and self.n_global <= 4 * max(self.n_halo, 1)):
+        units = (fixed_unit,) if fixed_unit else tuple(units)
+        # without merged passes the halo path ignores the unit: time each K once
+        halo_units = units if use_merged_halo() else ("none",)
+        cands = [("halo", k, u) for k in halo_ks for u in dict.fromkeys(halo_units)]
+        n = torch.full((self.world,), self.n_halo, dtype=torch.long, device=self.graph.col.device)
+        every = torch.empty_like(n)
+        self.comm.all_to_all_single(every, n)
+        max_halo = int(every.max())
+        if fixed == "allgather" or (fixed is None and self.n_global <= 4 * max(max_halo, 1)):
             # one step per all-gather chunk: "step" and "chunk" coincide
-            cands += [("allgather", k, u) for k in gather_ks for u in units if u != "chunk"]
+            g_units = dict.fromkeys("step" if u == "chunk" else u for u in units)
+            cands += [("allgather", k, u) for k in gather_ks for u in g_units]
         if fixed:
             cands = [c for c in cands if c[0] == fixed]
+        if not cands:
+            raise ValueError(f"exchange_candidates: nothing to time (KGX_EXCHANGE={fixed!r}, "
+                             f"KGX_HALO_MERGE={fixed_unit!r})")
         return cands
 
     def tune_exchange(self, run, candidates) -> tuple:
@@ -666,13 +680,21 @@ class ShardedGraph:
         the slowest rank's time counts (one all-to-all of the times).  Like a
         library autotuner: the best choice depends on the links' rate, which
         only the machine knows (tools/shard_sim.py: exchange-free, merging a
-        chunk's steps wins; with 400 GB/s links, merging only its pulled rows)."""
+        chunk's steps wins; with 400 GB/s links, merging only its pulled rows).
+        Bounded: once the agreed (slowest-rank) time spent passes
+        KGX_TUNE_BUDGET_S (default 60 s) the remaining candidates are left
+        untimed (inf); `tuning_s` / `tuning_skipped` record it."""
         dev = self.graph.col.device
-        times = []
+        budget = float(os.environ.get("KGX_TUNE_BUDGET_S", "60"))
+        worst, spent, t_start = [], 0.0, time.perf_counter()
         for kind, K, unit in candidates:
+            if spent > budget:  # every rank sees the same agreed times, so all stop at the same candidate
+                worst.append(float("inf"))
+                continue
             self.exchange, self.halo_k, self.merge_unit = kind, K, unit
+            t_plan = time.perf_counter()
             self.exchange_plan(K)
-            best = float("inf")
+            best, total = float("inf"), time.perf_counter() - t_plan
             for _ in range(2):
                 if dev.type == "cuda":
                     torch.cuda.synchronize(dev)
@@ -681,14 +703,19 @@ class ShardedGraph:
                 if dev.type == "cuda":
                     torch.cuda.synchronize(dev)
                 best = min(best, time.perf_counter() - t0)
-            times.append(best)
-        t = torch.tensor(times, dtype=torch.float64, device=dev)
-        every = torch.empty(self.world * t.numel(), dtype=torch.float64, device=dev)
-        self.comm.all_to_all_single(every, t.repeat(self.world).contiguous())
-        worst = every.view(self.world, -1).max(0).values.cpu()
-        i = int(torch.argmin(worst))
+                total += time.perf_counter() - t0
+            # agree on (best, time spent) now: the slowest rank's counts for both
+            t = torch.tensor([best, total], dtype=torch.float64, device=dev)
+            every = torch.empty(self.world * 2, dtype=torch.float64, device=dev)
+            self.comm.all_to_all_single(every, t.repeat(self.world).contiguous())
+            mx = every.view(self.world, 2).max(0).values.cpu()
+            worst.append(float(mx[0]))
+            spent += float(mx[1])
+        i = min(range(len(worst)), key=worst.__getitem__)
         self.exchange, self.halo_k, self.merge_unit = candidates[i]
-        self.tuning = {f"{kind}:{K}:{unit}": float(v) for (kind, K, unit), v in zip(candidates, worst)}
+        self.tuning = {f"{kind}:{K}:{unit}": v for (kind, K, unit), v in zip(candidates, worst)}
+        self.tuning_s = time.perf_counter() - t_start
+        self.tuning_skipped = sum(1 for v in worst if v == float("inf"))
         self.exchange_plan(self.halo_k)
         return candidates[i]
 
@@ -976,7 +1003,7 @@ class ShardedGCNConv(Layer):
 
     def tune(self, x_local: torch.Tensor) -> int | None:
         """Time the exchanges once (ShardedGraph.tune_exchange: the push-pull
-        halo at K = 1 / 2 / 4 / 8 chunks, and the all-gather where its table is
+        halo at K = 1 / 2 / 4 chunks, and the all-gather where its table is
         not far larger); a no-op when K is fixed, on one rank, or off the
         default path."""
         sg = self.sg
@@ -989,7 +1016,7 @@ class ShardedGCNConv(Layer):
             return sg.halo_k
         with torch.no_grad():
             sg.tune_exchange(lambda kind, K: self._forward_overlapped(x_local, self.bias if use_b else None, K),
-                             sg.exchange_candidates(4 * x_local.shape[1]))
+                             sg.exchange_candidates())
         return sg.halo_k
 
     def _forward_overlapped(self, x_local: torch.Tensor, bias, n_chunks: int | None = None) -> torch.Tensor:
@@ -1124,7 +1151,7 @@ class _ShardedWrap(Layer):
             return
         with torch.no_grad():
             sg.tune_exchange(lambda kind, K: self._forward_impl(x_local, None),
-                             sg.exchange_candidates(4 * x_local.shape[1], halo_ks=(1, 2, 4)))
+                             sg.exchange_candidates())
 
 
 class ShardedGINConv(_ShardedWrap):

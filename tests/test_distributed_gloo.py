@@ -215,7 +215,7 @@ def _worker(rank, world, chunks, port, q):
                 y_pull = layer(torch.from_numpy(x[lo:hi]))  # pull-only halo
         finally:
             del os.environ["KGX_HALO_PUSH"]
-        # K left open: the first forward times K = 1 / 2 / 4 / 8 (collective) and keeps the fastest
+        # K left open: the first forward times K = 1 / 2 / 4 (collective) and keeps the fastest
         sg2 = kd.ShardedGraph.build(torch.from_numpy(s[keep]), torch.from_numpy(d[keep]), bounds,
                                     backend=OracleBackend(), n_features=F_OUT)
         layer2 = kd.ShardedGCNConv(F_OUT, sg2)
@@ -472,3 +472,82 @@ def test_sharded_no_halo():
     h = R.gin_forward(X, EI, [(w[0], w[1], None)], "sum", eps=0.5).numpy()
     got = np.concatenate([res[r][3] for r in range(world)])
     assert (np.abs(got - h) / np.maximum(1, np.abs(h))).max() <= 1e-5
+
+
+def _uneven_graph():
+    """Rank 0's rows draw every edge from rank 1's nodes, rank 1's rows only from
+    their own: one rank has a large halo, the other none."""
+    s, d, x, W, b = _graph()
+    half = N // 2
+    s = np.where(d < half, half + s % half, half + s % half).astype(s.dtype)
+    return s, d, x, W, b
+
+
+def _uneven_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        s, d, x, W, b = _uneven_graph()
+        bounds = kd.equal_bounds(N, world)
+        lo, hi = bounds[rank], bounds[rank + 1]
+        keep = (d >= lo) & (d < hi)
+        sg = kd.ShardedGraph.build(torch.from_numpy(s[keep]), torch.from_numpy(d[keep]), bounds,
+                                   backend=OracleBackend(), n_features=F_OUT)
+        os.environ.update(KGX_EXCHANGE="allgather", KGX_HALO_MERGE="chunk")
+        try:  # the all-gather's "chunk" unit maps to "step" instead of emptying the list
+            fixed = sg.exchange_candidates()
+        finally:
+            del os.environ["KGX_EXCHANGE"], os.environ["KGX_HALO_MERGE"]
+        layer = kd.ShardedGCNConv(F_OUT, sg)
+        layer._build_device = torch.device("cpu")
+        layer.build((hi - lo, F_IN))
+        with torch.no_grad():
+            layer.kernel.copy_(torch.from_numpy(W))
+            layer.bias.copy_(torch.from_numpy(b))
+            y = layer(torch.from_numpy(x[lo:hi]))  # first forward: the collective tuner
+        import bench  # the N > 1 line's per-rank diagnostics (bench.shard_summary)
+
+        info = bench.shard_summary(sg, "gcn", F_IN, F_OUT, False)
+        q.put((rank, sg.n_halo, sorted(sg.tuning), (sg.exchange, sg.halo_k, sg.merge_unit), fixed, y.numpy(),
+               sg.tuning_s, info))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_sharded_uneven_halo_tuner_agrees():
+    """One rank with a large halo, one with none: every rank lists and times the
+    same exchange candidates (the all-gather included, decided on the largest
+    halo), agrees on the choice, and the layer equals the oracle."""
+    if torch.cuda.is_initialized():
+        pytest.skip("never start processes from a process that has initialised the GPU")
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_uneven_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r = q.get(timeout=120)
+        res[r[0]] = r[1:]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][0] > 4 * max(res[1][0], 1)  # very uneven halos
+    assert res[0][1] == res[1][1] and any(k.startswith("allgather:") for k in res[0][1])
+    assert res[0][2] == res[1][2]
+    assert res[0][3] == res[1][3] == [("allgather", k, "step") for k in (1, 2, 4)]
+    assert res[0][5] is not None and res[0][5] >= 0
+    for r in range(world):  # what the N > 1 bench line reports per rank
+        info = res[r][6]
+        assert info["backend"] == "gloo" and info["world_size_reported"] == world
+        assert (info["exchange"], info["halo_chunks"], info["merge_unit"]) == res[r][2]
+        assert sorted(info["exchange_tuning_s"]) == res[r][1]
+        assert info["exchange_tuning_total_s"] > 0 and info["exchange_tuning_skipped"] == 0
+    s, d, x, W, b = _uneven_graph()
+    y = R.gcn_forward(torch.from_numpy(x), torch.from_numpy(np.stack([s, d])), torch.from_numpy(W),
+                      torch.from_numpy(b)).numpy()
+    got = np.concatenate([res[r][4] for r in range(world)])
+    assert (np.abs(got - y) / np.maximum(1, np.abs(y))).max() <= 1e-5
