@@ -124,7 +124,7 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
   __shared__ float Ob[LS ? OCOLS : 1];  // LS: this block's bias columns (read beside the out rows)
 
   const int tid = threadIdx.x;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: roles branch on SCC, not exec
 
   int cg = 0;
   int64_t pid = blockIdx.x, n_pairs = gridDim.x;
@@ -342,23 +342,32 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
     // buffer and refill that set with tile i + 1 + NSETS.  Outstanding loads,
     // oldest first, are the sets in cyclic order, so a set's wait leaves the
     // other NSETS - 1 sets in flight.
+    // The last step leaves both loops straight to the epilogue (goto), so the
+    // loop's back edge is taken only after all NSETS steps issued their loads:
+    // every path into a step's wait has the same loads outstanding (what the
+    // counted waits assume; tools/isa_hazard_check.py proves it on the ISA).
     for (int64_t i = 0; i < my_tiles; i += NSETS, t += NSETS * n_pairs) {
-      bool done = false;
 #pragma unroll
       for (int k = 0; k < NSETS; ++k) {
-        if (!done) {
-          if (pstore) wait_set(P[k], Q[k], OthersP{});
-          else wait_set(P[k], Q[k], Others{});
-          stage(P[k], Q[k], int((i + k + 1) & 1));
-          if (pstore) store_out(i + k - 1);  // the tile the consumers finished at the last barrier
-          load_tile(P[k], Q[k], t + (k + 1 + NSETS) * n_pairs);
-          lds_barrier();
-          done = i + k + 1 >= my_tiles;
-        }
+        if (pstore) wait_set(P[k], Q[k], OthersP{});
+        else wait_set(P[k], Q[k], Others{});
+        stage(P[k], Q[k], int((i + k + 1) & 1));
+        if (pstore) store_out(i + k - 1);  // the tile the consumers finished at the last barrier
+        load_tile(P[k], Q[k], t + (k + 1 + NSETS) * n_pairs);
+        lds_barrier();
+        if (i + k + 1 >= my_tiles) goto producer_done;
       }
     }
+  producer_done:
+    // The last steps' prefetches (tiles past the end, read as zeros) are still
+    // landing in the now-dead sets, and hipcc, which cannot see inline asm's
+    // loads as pending, hands dead registers to store_out's values: so wait for
+    // them first, and fence the scheduler so none of store_out's arithmetic is
+    // hoisted above the wait (tools/isa_hazard_check.py found both: store_out
+    // after the loop, and its row address computed above a bare wait).
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
     if (pstore) store_out(my_tiles - 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no loads in flight at exit
     return;
   }
 
