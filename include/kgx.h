@@ -291,6 +291,21 @@ int kgx_spmm_gemm_f256(int reduce, const int32_t* rowptr, const int32_t* rows, i
                        float* out, int64_t ld_out, float* partials, float* agg_out, int64_t ld_agg,
                        kgx_stream_t stream);
 
+/* kgx_spmm_gemm_f256_ex: kgx_spmm_gemm_f256 gathering from TWO feature tables,
+ * as kgx_spmm_gemm_ex3: source columns c < n_x1 are rows of x, c >= n_x1 rows
+ * c - n_x1 of x2 (same ld_x, 16-byte aligned); pre_gin's root rows are rows of
+ * x.  The sharded GINConv's merged halo pass at C4: a row's own-source and
+ * halo edges in one launch, (1+eps) x_i + aggr -> Dense, the row written once
+ * (distributed.py; gin_conv.py:216-225 per shard).  Sum only with x2; x2 NULL:
+ * kgx_spmm_gemm_f256. */
+int kgx_spmm_gemm_f256_ex(int reduce, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
+                          const int32_t* items, int64_t n_items, int64_t n_long_items, int64_t n_short_end,
+                          const int32_t* tiny_pack, const float* tiny_w, const int32_t* split, int64_t n_split,
+                          const int32_t* idx, const float* w, const float* x, int64_t ld_x, const float* x2,
+                          int64_t n_x1, int64_t F_in, const float* W, int64_t F_out, const float* bias, int flags,
+                          float gin_scale, float* out, int64_t ld_out, float* partials, float* agg_out,
+                          int64_t ld_agg, kgx_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * Backward of the segment max / min reduction (autograd of kgx_spmm MAX/MIN).
  * torch's scatter_reduce amax/amin backward, under the reference's isinf

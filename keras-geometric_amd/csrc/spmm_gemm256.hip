@@ -79,7 +79,20 @@ struct F256Args {
   int accumulate;
   int relu;
   float gin_scale;
+  // two-table gathers (kgx_spmm_gemm_f256_ex): source columns c >= n_x1 are rows
+  // c - n_x1 of a second table x2 (same ld_x); x2b = x2 - n_x1 * ld_x (host
+  // address math), so a gather's address is one select of the base
+  const float* x2b;
+  int32_t n_x1;
 };
+
+// Source row of column c: x[c], or with TWO x2[c - n_x1].  Root rows (pre_gin's
+// x_i) are always rows of x.
+template <bool TWO>
+__device__ __forceinline__ const float* gsrc256(const F256Args& a, int32_t c) {
+  if constexpr (TWO) return (c >= a.n_x1 ? a.x2b : a.x) + row_off(c, a.ld_x);
+  return a.x + row_off(c, a.ld_x);
+}
 
 // workgroup barrier for LDS hand-offs only (lgkmcnt, not vmcnt): gathers
 // prefetched for the next tile stay in flight across it
@@ -200,7 +213,7 @@ __device__ __forceinline__ void transform_tile(const F256Args& a, const short (*
 #ifndef KGX_F256_MID_PF
 #define KGX_F256_MID_PF 6
 #endif
-template <int RED, bool WEIGHTED, int PF>
+template <int RED, bool WEIGHTED, int PF, bool TWO>
 __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_kernel(F256Args a) {
   using R = RowRed<RED>;
 #ifdef KGX_F256_U
@@ -261,7 +274,7 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_kernel(F256Args a) {
     for (int r = 0; r < 2; ++r)
 #pragma unroll
       for (int u = 0; u < PF; ++u)
-        if (u < pn[r]) vload<4>(pv[r][u], a.x + row_off(c[r][u], a.ld_x) + f);
+        if (u < pn[r]) vload<4>(pv[r][u], gsrc256<TWO>(a, c[r][u]) + f);
   };
 
   fetch(int64_t(blockIdx.x) * kRows + 2 * wave);
@@ -295,7 +308,7 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_kernel(F256Args a) {
       }
       float v[B][4];
 #pragma unroll
-      for (int u = 0; u < B; ++u) vload<4>(v[u], a.x + row_off(c[u], a.ld_x) + f);
+      for (int u = 0; u < B; ++u) vload<4>(v[u], gsrc256<TWO>(a, c[u]) + f);
 #pragma unroll
       for (int u = 0; u < B; ++u)
 #pragma unroll
@@ -323,8 +336,8 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_kernel(F256Args a) {
       float v[2][U][4];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        vload<4>(v[0][u], a.x + row_off(c[0][u], a.ld_x) + f);
-        vload<4>(v[1][u], a.x + row_off(c[1][u], a.ld_x) + f);
+        vload<4>(v[0][u], gsrc256<TWO>(a, c[0][u]) + f);
+        vload<4>(v[1][u], gsrc256<TWO>(a, c[1][u]) + f);
       }
 #pragma unroll
       for (int r = 0; r < 2; ++r)
@@ -378,7 +391,7 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_kernel(F256Args a) {
 // (F_out = 256, no accumulate, no saved aggregate) every full tile's stores are
 // unconditional too: the count of memory operations in flight is then the same
 // on every path, so the compiler's waits before a fold stay partial.
-template <int RED, bool WEIGHTED, bool GIN, bool FAST>
+template <int RED, bool WEIGHTED, bool GIN, bool FAST, bool TWO>
 __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Args a) {
   using R = RowRed<RED>;
   constexpr int RPW = 2;  // rows per wave per tile
@@ -454,8 +467,8 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Arg
         pw[r][0] = rw[B][r].x;
         pw[r][1] = rw[B][r].y;
       }
-      vload<4>(pv[r][0], a.x + row_off(rec[B][r].z, a.ld_x) + f);
-      vload<4>(pv[r][1], a.x + row_off(rec[B][r].w, a.ld_x) + f);
+      vload<4>(pv[r][0], gsrc256<TWO>(a, rec[B][r].z) + f);
+      vload<4>(pv[r][1], gsrc256<TWO>(a, rec[B][r].w) + f);
       if constexpr (GIN) vload<4>(px[r], a.x + row_off(rec[B][r].x, a.ld_x) + f);
     }
   };
@@ -633,7 +646,7 @@ unsigned grid256(K k, int64_t tiles) {
   return unsigned(tiles < cap ? tiles : cap);
 }
 
-template <int RED, bool WT>
+template <int RED, bool WT, bool TWO>
 int launch256(const F256Args& a, hipStream_t s) {
   const int64_t work = a.items ? a.n_work : a.n_rows;
   // long rows and hub chunks [0, n_long), then the rows of degree 3..7 [n_long, n_work)
@@ -642,7 +655,7 @@ int launch256(const F256Args& a, hipStream_t s) {
     F256Args b = a;
     b.n_work = n_long;
     if (!a.items) b.n_rows = n_long;
-    auto k = spmm_gemm256_kernel<RED, WT, 4>;
+    auto k = spmm_gemm256_kernel<RED, WT, 4, TWO>;
     hipLaunchKernelGGL(k, dim3(grid256(k, (n_long + kRows - 1) / kRows)), dim3(kThreads), 0, s, b);
     KGX_CHECK_LAUNCH();
   }
@@ -650,14 +663,16 @@ int launch256(const F256Args& a, hipStream_t s) {
     F256Args b = a;
     b.items = a.items + n_long;
     b.n_work = work - n_long;
-    auto k = spmm_gemm256_kernel<RED, WT, KGX_F256_MID_PF>;
+    auto k = spmm_gemm256_kernel<RED, WT, KGX_F256_MID_PF, TWO>;
     hipLaunchKernelGGL(k, dim3(grid256(k, (b.n_work + kRows - 1) / kRows)), dim3(kThreads), 0, s, b);
     KGX_CHECK_LAUNCH();
   }
   if (a.tpack && a.n_tiny > 0) {
     const bool fast = a.F_out == kF && !a.accumulate && !a.agg_out;
-    auto k = a.pre_gin ? (fast ? spmm_gemm256_tiny2_kernel<RED, WT, true, true> : spmm_gemm256_tiny2_kernel<RED, WT, true, false>)
-                       : (fast ? spmm_gemm256_tiny2_kernel<RED, WT, false, true> : spmm_gemm256_tiny2_kernel<RED, WT, false, false>);
+    auto k = a.pre_gin
+                 ? (fast ? spmm_gemm256_tiny2_kernel<RED, WT, true, true, TWO> : spmm_gemm256_tiny2_kernel<RED, WT, true, false, TWO>)
+                 : (fast ? spmm_gemm256_tiny2_kernel<RED, WT, false, true, TWO>
+                         : spmm_gemm256_tiny2_kernel<RED, WT, false, false, TWO>);
     hipLaunchKernelGGL(k, dim3(grid256(k, (a.n_tiny + kRows - 1) / kRows)), dim3(kThreads), 0, s, a);
     KGX_CHECK_LAUNCH();
   }
@@ -675,13 +690,14 @@ int launch256(const F256Args& a, hipStream_t s) {
 
 using namespace kgx;
 
-extern "C" int kgx_spmm_gemm_f256(int reduce, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
-                                  const int32_t* items, int64_t n_items, int64_t n_long_items, int64_t n_short_end,
-                                  const int32_t* tiny_pack, const float* tiny_w, const int32_t* split, int64_t n_split,
-                                  const int32_t* idx, const float* w, const float* x, int64_t ld_x, int64_t F_in,
-                                  const float* W, int64_t F_out, const float* bias, int flags, float gin_scale,
-                                  float* out, int64_t ld_out, float* partials, float* agg_out, int64_t ld_agg,
-                                  kgx_stream_t stream_) {
+extern "C" int kgx_spmm_gemm_f256_ex(int reduce, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
+                                     const int32_t* items, int64_t n_items, int64_t n_long_items, int64_t n_short_end,
+                                     const int32_t* tiny_pack, const float* tiny_w, const int32_t* split,
+                                     int64_t n_split, const int32_t* idx, const float* w, const float* x,
+                                     int64_t ld_x, const float* x2, int64_t n_x1, int64_t F_in, const float* W,
+                                     int64_t F_out, const float* bias, int flags, float gin_scale, float* out,
+                                     int64_t ld_out, float* partials, float* agg_out, int64_t ld_agg,
+                                     kgx_stream_t stream_) {
   hipStream_t stream = as_stream(stream_);
   KGX_REQUIRE(reduce >= KGX_SUM && reduce <= KGX_MIN, KGX_ERR_ARG, "kgx_spmm_gemm_f256: reduce %d unsupported",
               reduce);
@@ -701,6 +717,10 @@ extern "C" int kgx_spmm_gemm_f256(int reduce, const int32_t* rowptr, const int32
               "kgx_spmm_gemm_f256: KGX_FUSED_RELU cannot be combined with KGX_FUSED_ACCUMULATE");
   KGX_REQUIRE(!agg_out || (ld_agg >= F_in && reinterpret_cast<uintptr_t>(agg_out) % 16 == 0 && ld_agg % 4 == 0),
               KGX_ERR_ARG, "kgx_spmm_gemm_f256: agg_out must be 16-byte aligned with ld >= F_in, ld %% 4 == 0");
+  KGX_REQUIRE(!x2 || (n_x1 >= 0 && n_x1 < (int64_t(1) << 31) && reinterpret_cast<uintptr_t>(x2) % 16 == 0),
+              KGX_ERR_ARG, "kgx_spmm_gemm_f256: x2 must be 16-byte aligned and 0 <= n_x1 < 2^31");
+  KGX_REQUIRE(!x2 || reduce == KGX_SUM, KGX_ERR_UNSUPPORTED,
+              "kgx_spmm_gemm_f256: two-table gathers are implemented for the sum");
   if (n_rows == 0) return KGX_OK;
   KGX_REQUIRE(rowptr && rows && idx && x && W && out, KGX_ERR_ARG, "kgx_spmm_gemm_f256: null pointer");
   KGX_REQUIRE(ld_x < (int64_t(1) << 31), KGX_ERR_ARG, "kgx_spmm_gemm_f256: x leading dimension >= 2^31");
@@ -739,11 +759,29 @@ extern "C" int kgx_spmm_gemm_f256(int reduce, const int32_t* rowptr, const int32
   a.accumulate = (flags & KGX_FUSED_ACCUMULATE) != 0;
   a.relu = (flags & KGX_FUSED_RELU) != 0;
   a.gin_scale = gin_scale;
+  a.n_x1 = x2 ? int32_t(n_x1) : INT32_MAX;
+  // x2 - n_x1 * ld_x as an address (modular): gsrc256 adds row_off(c) for c >= n_x1
+  a.x2b = x2 ? reinterpret_cast<const float*>(reinterpret_cast<uintptr_t>(x2) -
+                                               uintptr_t(n_x1) * uintptr_t(ld_x) * sizeof(float))
+             : nullptr;
   const bool wt = w != nullptr;
+  if (x2) return wt ? launch256<KGX_SUM, true, true>(a, stream) : launch256<KGX_SUM, false, true>(a, stream);
   switch (reduce) {
-    case KGX_SUM: return wt ? launch256<KGX_SUM, true>(a, stream) : launch256<KGX_SUM, false>(a, stream);
-    case KGX_MEAN: return wt ? launch256<KGX_MEAN, true>(a, stream) : launch256<KGX_MEAN, false>(a, stream);
-    case KGX_MAX: return wt ? launch256<KGX_MAX, true>(a, stream) : launch256<KGX_MAX, false>(a, stream);
-    default: return wt ? launch256<KGX_MIN, true>(a, stream) : launch256<KGX_MIN, false>(a, stream);
+    case KGX_SUM: return wt ? launch256<KGX_SUM, true, false>(a, stream) : launch256<KGX_SUM, false, false>(a, stream);
+    case KGX_MEAN: return wt ? launch256<KGX_MEAN, true, false>(a, stream) : launch256<KGX_MEAN, false, false>(a, stream);
+    case KGX_MAX: return wt ? launch256<KGX_MAX, true, false>(a, stream) : launch256<KGX_MAX, false, false>(a, stream);
+    default: return wt ? launch256<KGX_MIN, true, false>(a, stream) : launch256<KGX_MIN, false, false>(a, stream);
   }
+}
+
+extern "C" int kgx_spmm_gemm_f256(int reduce, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
+                                  const int32_t* items, int64_t n_items, int64_t n_long_items, int64_t n_short_end,
+                                  const int32_t* tiny_pack, const float* tiny_w, const int32_t* split, int64_t n_split,
+                                  const int32_t* idx, const float* w, const float* x, int64_t ld_x, int64_t F_in,
+                                  const float* W, int64_t F_out, const float* bias, int flags, float gin_scale,
+                                  float* out, int64_t ld_out, float* partials, float* agg_out, int64_t ld_agg,
+                                  kgx_stream_t stream) {
+  return kgx_spmm_gemm_f256_ex(reduce, rowptr, rows, n_rows, items, n_items, n_long_items, n_short_end, tiny_pack,
+                               tiny_w, split, n_split, idx, w, x, ld_x, nullptr, 0, F_in, W, F_out, bias, flags,
+                               gin_scale, out, ld_out, partials, agg_out, ld_agg, stream);
 }

@@ -86,6 +86,11 @@ _SIGNATURES = {
         _i32p, _f32p, _f32p, _i64, _i64, _f32p, _i64, _f32p, _int, ctypes.c_float,
         _f32p, _i64, _f32p, _f32p, _i64, ctypes.c_void_p,
     ],
+    "kgx_spmm_gemm_f256_ex": [
+        _int, _i32p, _i32p, _i64, _i32p, _i64, _i64, _i64, _i32p, _f32p, _i32p, _i64,
+        _i32p, _f32p, _f32p, _i64, _f32p, _i64, _i64, _f32p, _i64, _f32p, _int, ctypes.c_float,
+        _f32p, _i64, _f32p, _f32p, _i64, ctypes.c_void_p,
+    ],
     "kgx_spmm_gemm_ex3": [
         _int, _i32p, _i32p, _i64, _i32p, _i64, _i64, _i64, _i32p, _f32p, _i64, _i32p, _i64,
         _i32p, _f32p, _f32p, _i64, _f32p, _i64, _i64, _f32p, _i64, _f32p, _int, ctypes.c_float,

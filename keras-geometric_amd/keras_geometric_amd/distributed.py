@@ -41,7 +41,7 @@ import torch.distributed as dist
 from . import _native as nat
 from . import graph as G
 from . import ops as kops
-from .layers.base import Layer, get_initializer
+from .layers.base import Dropout, Layer, get_initializer
 
 
 class KgxBackend:
@@ -80,12 +80,15 @@ class KgxBackend:
     def supports_fused(self, f_in: int, f_out: int) -> bool:
         return kops.fused_transform_supported(f_in, f_out, two_table=True)  # the sharded passes' gathers
 
-    def aggregate_transform(self, g, x, W, bias=None, out=None, x2=None, accumulate=True):
-        """GCN sum with the edge weights, then @ W (+ bias); out += ... if given
-        (accumulate=False: g's scheduled rows of out overwritten).  x2: second
-        table for sources >= x.shape[0] (two-table gathers)."""
-        return kops.aggregate_transform(g, x, W, "sum", weighted=True, bias=bias, out=out, x2=x2,
-                                        accumulate=accumulate)
+    def aggregate_transform(self, g, x, W, bias=None, out=None, x2=None, accumulate=True, weighted=True,
+                            pre_gin=False, gin_scale=1.0, relu=False):
+        """Sum (with the GCN edge weights unless weighted=False), then @ W (+
+        bias); out += ... if given (accumulate=False: g's scheduled rows of out
+        overwritten).  x2: second table for sources >= x.shape[0] (two-table
+        gathers).  pre_gin: GIN's gin_scale * x_i + aggr before the product
+        (root rows of x); relu: max(., 0) at the store (overwriting launches)."""
+        return kops.aggregate_transform(g, x, W, "sum", weighted=weighted, bias=bias, out=out, x2=x2,
+                                        accumulate=accumulate, pre_gin=pre_gin, gin_scale=gin_scale, relu=relu)
 
     def restrict_rows(self, g, row_mask):
         return G.restrict_rows(g, row_mask)
@@ -1175,16 +1178,77 @@ class ShardedGINConv(_ShardedWrap):
         self._maybe_tune(x_local.contiguous())
         return self._forward_impl(x_local, training)
 
+    def _fused(self, x_local: torch.Tensor) -> bool:
+        """Whether (1+eps) x_i + aggr -> the MLP's first Dense runs fused into the
+        pipelined passes (sum, a linear or ReLU first Dense, a shape the fused
+        kernels take with two tables: C4's 256 -> 256)."""
+        first = self.conv.mlp.layers[0]
+        return (self._pipelined() and self.conv.aggregator == "sum" and first.activation in (None, torch.relu)
+                and self.sg.backend.supports_fused(x_local.shape[1], first.units))
+
     def _forward_impl(self, x_local: torch.Tensor, training=None) -> torch.Tensor:
         sg, conv = self.sg, self.conv
         x_local = x_local.contiguous()
         with torch.no_grad():
+            if self._fused(x_local):
+                h = self._forward_fused(x_local)
+                for layer in conv.mlp.layers[1:]:
+                    h = layer(h, training=training) if isinstance(layer, Dropout) else layer(h)
+                return h
             if self._pipelined():  # halo pipelined under the own-source pass
                 h = sg.propagate_overlapped(x_local, conv.aggregator, gin_scale=float(conv._scale()))
             else:
                 h = sg.propagate(x_local, conv.aggregator, epilogue=nat.EPI_GIN, xroot=x_local,
                                  gin_scale=conv._scale())
             return conv.mlp(h, training=training)
+
+    def _forward_fused(self, x_local: torch.Tensor) -> torch.Tensor:
+        """The pipelined GIN-sum passes with the MLP's first Dense fused in, as
+        ShardedGCNConv._forward_merged (gin_conv.py:216-225 per shard):
+        side stream: pack + exchange; main stream: out[rows not in H] =
+        b + (s x_i + A_own x) W while the exchange is in flight; out[H] =
+        b + (s x_i + A_own x + A_0 halo_0) W in one two-table launch once the
+        first group has landed; out += (A_k halo_k) W per later group.  No
+        [n_local, F_in] aggregate is written or read back.  The first Dense's
+        ReLU goes into the overwriting launches when no later group adds to the
+        rows, else onto out at the end (max(., 0) after the whole sum)."""
+        sg, conv = self.sg, self.conv
+        first = conv.mlp.layers[0]
+        W, b = first.kernel, (first.bias if first.use_bias else None)
+        pp = sg.exchange_plan(weighted=False)
+        halo = sg.halo_buffer(x_local.shape[1], x_local, pp.n_rows)
+        unit = None if (use_merged_halo() or pp.kind == "allgather") else "none"
+        g_a, g_b, later, first_wait = sg.merged_passes(pp, unit)
+        steps = [st for c in pp.chunks for st in c.steps]
+        relu = first.activation is torch.relu
+        kw = dict(weighted=False, pre_gin=True, gin_scale=float(conv._scale()), relu=relu and not later)
+        works = sg.start_halo_exchange(x_local, halo, pp.chunks)
+        handles = []
+        for w, c in zip(works, pp.chunks):
+            handles.extend(w.handles if w is not None else [None] * len(c.steps))
+        waited = set()
+
+        def wait_step(i):
+            for j in range(i + 1):  # steps land in issue order on the comm stream
+                if j not in waited:
+                    waited.add(j)
+                    if handles[j] is not None:
+                        handles[j].wait()
+
+        with kops.sharing_gpu():  # the exchange's packing and RCCL kernels run beside this pass
+            out = sg.backend.aggregate_transform(g_a, x_local, W, bias=b, **kw)
+        if g_b is not None:
+            wait_step(first_wait)
+            with kops.sharing_gpu() if later else contextlib.nullcontext():
+                sg.backend.aggregate_transform(g_b, x_local, W, bias=b, out=out, x2=halo, accumulate=False, **kw)
+        for n, (i, g, lo, hi) in enumerate(later):
+            wait_step(i)
+            with kops.sharing_gpu() if n + 1 < len(later) else contextlib.nullcontext():
+                sg.backend.aggregate_transform(g, halo[lo: hi], W, out=out, weighted=False)
+        wait_step(len(steps) - 1)  # also orders the side stream's reads of x_local
+        if relu and later:
+            out = torch.relu_(out)
+        return out
 
 
 class ShardedSAGEConv(_ShardedWrap):

@@ -211,17 +211,18 @@ _F256_DEFAULT = "1"
 
 def _f256_call(reduce, rowptr, rows, n_dst, items, n_items, split, n_split, idx, w, x, x2, W, bias, flags, gin_scale,
                out, partials, agg, dev, tpack=None, tw=None, n_short_end=-1, n_long=-1):
-    """kgx_spmm_gemm_f256: the 256-wide fused kernels (main + the degree <= 2
-    tail from the packed records; one feature table)."""
-    if x2 is not None:
-        raise NotImplementedError("spmm_gemm: two-table gathers are implemented for F_in = 128")
+    """kgx_spmm_gemm_f256_ex: the 256-wide fused kernels (main + the degree <= 2
+    tail from the packed records); x2: second feature table for sources >=
+    x.shape[0] (the sharded GIN layer's merged halo pass; sum only)."""
     n_se, tpack, tw, _ = _tiny_abi(items, n_items, 0, tpack, tw if w is not None else None, n_short_end, 0)
+    x2p, n_x1 = _x2_args(x, x2)
     nat.check(
-        nat.lib().kgx_spmm_gemm_f256(
+        nat.lib().kgx_spmm_gemm_f256_ex(
             reduce, nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items,
             n_long if items is not None and 0 <= n_long <= n_se else -1, n_se, nat.ptr(tpack), nat.ptr(tw),
             nat.ptr(split), n_split,
-            nat.ptr(idx), nat.ptr(w), nat.ptr(x), x.stride(0), x.shape[1], nat.ptr(W), W.shape[1], nat.ptr(bias),
+            nat.ptr(idx), nat.ptr(w), nat.ptr(x), x.stride(0), x2p, n_x1, x.shape[1], nat.ptr(W), W.shape[1],
+            nat.ptr(bias),
             flags, float(gin_scale), nat.ptr(out), out.stride(0), nat.ptr(partials),
             nat.ptr(agg), agg.stride(0) if agg is not None else 0, nat.stream(dev),
         ),
@@ -355,10 +356,14 @@ def spmm_gemm_acc_(
     n_tiny2: int = 0,
     x2: Optional[torch.Tensor] = None,
     accumulate: bool = True,
+    flags: int = 0,
+    gin_scale: float = 1.0,
 ) -> None:
     """out += bias + REDUCE(...) @ W (KGX_FUSED_ACCUMULATE), in place; with
     accumulate=False the scheduled rows of out are overwritten instead (and the
-    rest left untouched): two launches over disjoint row sets fill one output."""
+    rest left untouched): two launches over disjoint row sets fill one output.
+    flags: KGX_FUSED_PRE_GIN / KGX_FUSED_RELU for an overwriting launch (the
+    sharded GIN layer's passes: (1+eps) x_i + aggr -> Dense)."""
     x, w, W, bias, x2 = _f32c(x), _f32c(w), _f32c(W), _f32c(bias), _f32c(x2)
     dev = nat.require_device(out, x, rowptr, rows, idx, w, W, bias, items, split, x2)
     n_dst = rowptr.numel() - 1
@@ -373,8 +378,8 @@ def spmm_gemm_acc_(
         partials = torch.empty((n_slots, x.shape[1]), dtype=torch.float32, device=dev)
     if x.shape[1] == F256:
         _f256_call(reduce, rowptr, rows, n_dst, items, n_items, split, n_split, idx, w, x, x2, W, bias,
-                   (nat.FUSED_ACCUMULATE if accumulate else 0) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0), 1.0,
-                   out, partials, None, dev, tpack, tw, n_short_end, n_long)
+                   (nat.FUSED_ACCUMULATE if accumulate else 0) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0) | flags,
+                   gin_scale, out, partials, None, dev, tpack, tw, n_short_end, n_long)
         return
     n_long = n_items if n_long < 0 or n_long > n_items else n_long
     n_se, tpack, tw, n_tiny2 = _tiny_abi(items, n_items, n_long, tpack, tw if w is not None else None, n_short_end,
@@ -385,7 +390,8 @@ def spmm_gemm_acc_(
             reduce, nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, n_long, n_se, nat.ptr(tpack),
             nat.ptr(tw), n_tiny2, nat.ptr(split), n_split,
             nat.ptr(idx), nat.ptr(w), nat.ptr(x), x.stride(0), x2p, n_x1, x.shape[1], nat.ptr(W), W.shape[1],
-            nat.ptr(bias), (nat.FUSED_ACCUMULATE if accumulate else 0) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0), 1.0, nat.ptr(out), out.stride(0), nat.ptr(partials), None, 0, nat.stream(dev),
+            nat.ptr(bias), (nat.FUSED_ACCUMULATE if accumulate else 0) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0) | flags,
+            float(gin_scale), nat.ptr(out), out.stride(0), nat.ptr(partials), None, 0, nat.stream(dev),
         ),
         "kgx_spmm_gemm",
     )
@@ -393,19 +399,20 @@ def spmm_gemm_acc_(
 
 @spmm_gemm_acc_.register_fake
 def _spmm_gemm_acc_fake(out, x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, n_long=-1, tpack=None,
-                        tw=None, n_short_end=-1, n_tiny2=0, x2=None, accumulate=True):
+                        tw=None, n_short_end=-1, n_tiny2=0, x2=None, accumulate=True, flags=0, gin_scale=1.0):
     return None
 
 
 def fused_transform_supported(f_in: int, f_out: int, two_table: bool = False) -> bool:
-    """Shapes kgx_spmm_gemm (F_in 128) and kgx_spmm_gemm_f256 (F_in 256; one
-    table) implement (aggregate-then-transform is also only worth it when
-    F_in <= F_out)."""
+    """Shapes kgx_spmm_gemm (F_in 128) and kgx_spmm_gemm_f256 (F_in 256)
+    implement, with one feature table or two (two_table: the sharded layers'
+    merged halo passes, sum only; aggregate-then-transform is also only worth
+    it when F_in <= F_out)."""
     import os
 
     if os.environ.get("KGX_FUSED", "1") in ("0", "false", "False"):
         return False
-    if f_in == F256 and not two_table:
+    if f_in == F256:
         return f_out == F256 and os.environ.get("KGX_FUSED256", _F256_DEFAULT) not in ("0", "false", "False")
     return f_in == 128 and f_out % 16 == 0 and 0 < f_out <= 128 and f_in <= f_out
 
@@ -827,15 +834,19 @@ def aggregate_transform(
     if x2 is not None and _needs_grad(x, x2, W, bias):
         raise NotImplementedError("aggregate_transform(x2=...) is a forward-only (no_grad) path")
     if out is not None:  # accumulate into `out` (sum only: the caller splits a row's edges)
-        if pre_gin or relu or red != nat.SUM:
+        if red != nat.SUM:
             raise ValueError("aggregate_transform(out=...) accumulates plain sums only")
+        if (pre_gin or relu) and accumulate:
+            raise ValueError("aggregate_transform(out=...): pre_gin / relu only with accumulate=False (overwrite)")
         if _needs_grad(x, W, bias, out):
             raise NotImplementedError("aggregate_transform(out=...) is a forward-only (no_grad) path")
         items, _, split, _, n_slots = g.work(exact)
         w = g.w if weighted else None
+        flags = (nat.FUSED_PRE_GIN if pre_gin else 0) | (nat.FUSED_RELU if relu else 0)
         _timed(lambda: torch.ops.kgx.spmm_gemm_acc_(out, x, g.rowptr, g.rows, items, split, g.col, w, n_slots, red,
                                                    W, bias, g.n_long if items is not None else -1,
-                                                   *_tiny_of(g, items), x2, bool(accumulate)))
+                                                   *_tiny_of(g, items), x2, bool(accumulate), int(flags),
+                                                   float(gin_scale)))
         return out
     if x2 is not None:
         return _aggregate_transform_raw(g, x, W, red, weighted, bias, pre_gin, gin_scale, exact, relu, x2)

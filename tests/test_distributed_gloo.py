@@ -80,15 +80,22 @@ class OracleBackend:
     def restrict_rows(self, g, row_mask):
         return SimpleNamespace(**vars(g), row_mask=row_mask)
 
-    def aggregate_transform(self, g, x, W, bias=None, out=None, x2=None, accumulate=True):
-        """sum_e w_e x[col_e] in CSR order, then @ W (+ bias); out += ... if given
-        (accumulate=False: overwrite); x2: sources >= len(x) are rows of x2.  A
-        row-restricted graph (restrict_rows) writes only its rows; the others
-        come out NaN (unwritten) so a pass that misses a row fails the test."""
+    def aggregate_transform(self, g, x, W, bias=None, out=None, x2=None, accumulate=True, weighted=True,
+                            pre_gin=False, gin_scale=1.0, relu=False):
+        """sum_e (w_e) x[col_e] in CSR order (pre_gin: gin_scale x_i + that, root
+        rows of x), then @ W (+ bias, ReLU); out += ... if given (accumulate=False:
+        overwrite); x2: sources >= len(x) are rows of x2.  A row-restricted graph
+        (restrict_rows) writes only its rows; the others come out NaN (unwritten)
+        so a pass that misses a row fails the test."""
         table = x if x2 is None else torch.cat([x, x2])
-        y = torch.matmul(self.aggregate(g, table, "sum", weighted=True), W)
+        agg = self.aggregate(g, table, "sum", weighted=weighted)
+        if pre_gin:  # (1+eps) x_i + aggr (gin_conv.py:216-222)
+            agg = torch.tensor(gin_scale, dtype=torch.float32) * x[: g.n_dst] + agg
+        y = torch.matmul(agg, W)
         if bias is not None:
             y = K.add(y, bias)
+        if relu:
+            y = torch.relu(y)
         mask = getattr(g, "row_mask", None)
         if mask is None:
             mask = torch.ones(g.n_dst, dtype=torch.bool)
@@ -347,6 +354,8 @@ def _conv_worker(rank, world, port, q):
                       kd.ShardedSAGEConv(F_OUT, sg, aggregator="mean", normalize=True),
                       kd.ShardedSAGEConv(F_OUT, sg, aggregator="pooling", pool_hidden_dim=10)):
             layer._ensure_built(xl)  # weights drawn per rank, then broadcast from rank 0
+            if isinstance(layer, kd.ShardedGINConv) and layer.conv.aggregator == "sum":
+                assert layer._fused(xl)  # (1+eps) x + aggr -> first Dense (+ReLU) fused into the passes
             with torch.no_grad():
                 outs.append((layer(xl).numpy(), list(layer.conv.get_weights())))
         q.put((rank, outs))

@@ -229,3 +229,46 @@ def test_fused256_tiny_tail_bit_identical(dev, red, weighted, gin):
     if gin:
         aggr = np.float32(1.25) * xs.numpy().astype(np.float64) + aggr
     assert_dot_bound(y.cpu().numpy(), aggr, W.cpu().double().numpy(), b.cpu().double().numpy(), k_eps=3e-5)
+
+
+@pytest.mark.parametrize("weighted", [False, True])
+@pytest.mark.parametrize("gin", [False, True])
+def test_fused256_two_tables_bit_identical(dev, weighted, gin):
+    """kgx_spmm_gemm_f256_ex with sources >= n_x1 read from a second table (the
+    sharded GIN layer's merged halo pass) equals the one-table launch over the
+    concatenated table bit for bit -- main kernel, degree 3..7 launch, tiny tail
+    and hub fix-up alike -- in the new-output, overwrite (accumulate=False, rows
+    outside a restricted schedule untouched) and accumulate forms."""
+    N, H, E = 12000, 5000, 30000
+    rng = np.random.default_rng(11 + 2 * weighted + gin)
+    s, d = rmat_edges(3 + gin, scale_for(N + H), N + H, 0, E)
+    d = d % N  # destinations are this shard's rows; sources own or halo
+    ei = T(np.stack([s, d]).astype(np.int32)).to(dev)
+    g = G.build_csr(ei[0].contiguous(), ei[1].contiguous(), N + H, N, n_features=F, split_len=16)
+    assert g.n_split > 0 and getattr(g, "_kgx_tiny", (None,))[0] is not None  # fix-up and tiny tail both run
+    if weighted:
+        g.w = T(rng.uniform(0.1, 1.0, g.kept).astype(np.float32)).to(dev)
+    x_all = T(rng.standard_normal((N + H, F)).astype(np.float32)).to(dev)
+    x_own, x_halo = x_all[:N].contiguous(), x_all[N:].contiguous()
+    W = T((rng.standard_normal((F, F)) * 0.06).astype(np.float32)).to(dev)
+    b = T(rng.standard_normal(F).astype(np.float32)).to(dev)
+    kw = dict(weighted=weighted, bias=b, pre_gin=gin, gin_scale=1.25)
+    with torch.no_grad():
+        one = kops.aggregate_transform(g, x_all, W, "sum", **kw)
+        two = kops.aggregate_transform(g, x_own, W, "sum", x2=x_halo, **kw)
+        assert torch.equal(one, two)
+        # overwrite the rows of a restricted schedule, leave the rest alone
+        mask = torch.zeros(N, dtype=torch.bool, device=dev)
+        mask[::3] = True
+        gr = G.restrict_rows(g, mask)
+        fill = torch.full((N, F), 7.0, device=dev)
+        o1, o2 = fill.clone(), fill.clone()
+        kops.aggregate_transform(gr, x_all, W, "sum", out=o1, accumulate=False, **kw)
+        kops.aggregate_transform(gr, x_own, W, "sum", out=o2, x2=x_halo, accumulate=False, **kw)
+        assert torch.equal(o1, o2)
+        assert torch.equal(o1[mask], one[mask]) and bool((o1[~mask] == 7.0).all())
+        # accumulate (plain sums; the later exchange groups of the sharded pass)
+        a1, a2 = one.clone(), one.clone()
+        kops.aggregate_transform(g, x_all, W, "sum", out=a1, weighted=weighted)
+        kops.aggregate_transform(g, x_own, W, "sum", out=a2, x2=x_halo, weighted=weighted)
+        assert torch.equal(a1, a2)

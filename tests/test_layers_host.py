@@ -87,7 +87,7 @@ def test_fused_shape_routing(monkeypatch):
     assert not kops.fused_transform_supported(128, 256)  # F_in <= F_out but the 128 kernel stops at 128
     assert kops.fused_transform_supported(256, 256)
     assert not kops.fused_transform_supported(256, 128)  # transform first: narrower rows to gather
-    assert not kops.fused_transform_supported(256, 256, two_table=True)
+    assert kops.fused_transform_supported(256, 256, two_table=True)  # sharded GIN at C4: kgx_spmm_gemm_f256_ex
     assert kops.fused_transform_supported(128, 128, two_table=True)
     monkeypatch.setenv("KGX_FUSED256", "0")
     assert not kops.fused_transform_supported(256, 256) and kops.fused_transform_supported(128, 128)
