@@ -830,6 +830,7 @@ template <int VEC, int NT, int RED, bool W, bool TWO = false>
 int launch_main(const SpmmArgs& a_in, hipStream_t s) {
   SpmmArgs a = a_in;
   ForkJoin* joined = nullptr;
+  int64_t a_hub_slots = 0;  // KGX_EXACT_FORK=2: spmm_kernel's grid leaves these block slots to the hub kernel
   if constexpr (NT == 1) {
     static const bool hub_off = [] {
       const char* h = getenv("KGX_HUB");
@@ -849,11 +850,21 @@ int launch_main(const SpmmArgs& a_in, hipStream_t s) {
       // Measured slower at NS: contiguous row batches of the
       // degree-descending list concentrate the heaviest rows on single groups
       // (8 / 32 / 256-row batches: 12.7 / 15.0 / 65 ms against 10.9 static).
-      static const bool fork_on = [] {
+      // KGX_EXACT_FORK=2: forked, but spmm_kernel keeps its static interleaved
+      // (grid-stride) rows, with its grid cut to the block slots the hub blocks
+      // leave, so every group is resident from the start (no atomics).
+      static const int fork_mode = [] {
         const char* h = getenv("KGX_EXACT_FORK");
-        return h && atoi(h) == 1;
+        return h ? atoi(h) : 0;
       }();
-      a.dyn_rows = fork_on ? 1 : 0;
+      static const int hub_cus = [] {
+        const char* h = getenv("KGX_EXACT_HUB_CUS");
+        return h ? atoi(h) : 0;
+      }();
+      const bool fork_on = fork_mode == 1 || fork_mode == 2;
+      a.dyn_rows = fork_mode == 1 ? 1 : 0;
+      int64_t hub_blocks = nb;
+      if (fork_mode == 2 && hub_cus > 0 && hub_cus < hub_blocks) hub_blocks = hub_cus;
       if (a.dyn && fork_on) {
         // dynamic pickup: the hub kernel runs on a forked stream BESIDE spmm_kernel
         // (which skips the hub rows and takes its rows from a counter), so the CUs
@@ -864,13 +875,14 @@ int launch_main(const SpmmArgs& a_in, hipStream_t s) {
           set_error("kgx_spmm: stream fork failed");
           return KGX_ERR_HIP;
         }
-        hipLaunchKernelGGL(kh, dim3(unsigned(nb)), dim3(kHubThreads), 0, fj.side, a);
+        hipLaunchKernelGGL(kh, dim3(unsigned(hub_blocks)), dim3(kHubThreads), 0, fj.side, a);
         KGX_CHECK_LAUNCH();
         if (hipEventRecord(fj.join, fj.side) != hipSuccess) {
           set_error("kgx_spmm: stream join failed");
           return KGX_ERR_HIP;
         }
         joined = &fj;
+        if (fork_mode == 2) a_hub_slots = hub_blocks * (kHubThreads / kBlock);  // spmm blocks a hub block displaces
       } else {
         hipLaunchKernelGGL(kh, dim3(unsigned(nb)), dim3(kHubThreads), 0, s, a);
         KGX_CHECK_LAUNCH();
@@ -904,7 +916,12 @@ int launch_main(const SpmmArgs& a_in, hipStream_t s) {
     if constexpr (RED == KGX_SUM && !TWO) {
       if (a.drop_key) k = spmm_kernel<VEC, NT, RED, W, true>;
     }
-    hipLaunchKernelGGL(k, dim3(resident_grid(k, work_long, a.G)), dim3(kBlock), 0, s, a);
+    unsigned grid = resident_grid(k, work_long, a.G);
+    if (a_hub_slots > 0) {
+      const int64_t g = int64_t(grid) - a_hub_slots;
+      grid = unsigned(g > int64_t(cu_count()) ? g : int64_t(cu_count()));
+    }
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, s, a);
     KGX_CHECK_LAUNCH();
   }
   if (joined && hipStreamWaitEvent(s, joined->join, 0) != hipSuccess) {
