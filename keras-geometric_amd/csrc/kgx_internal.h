@@ -77,6 +77,16 @@ unsigned resident_grid(Kern kernel, int64_t groups_needed, int G) {
   return unsigned(g < 1 ? 1 : g);
 }
 
+// A launch that shares the GPU with a concurrent stream (KGX_FUSED_SHARE_GPU)
+// takes (den - 1) / den of its resident grid: den = KGX_SHARE_DEN (default 8).
+inline int64_t shared_cap(int64_t full) {
+  const char* h = getenv("KGX_SHARE_DEN");  // read per launch: measurement sweeps change it in-process
+  const int v = h ? atoi(h) : 8;
+  const int den = v >= 2 ? v : 8;
+  const int64_t c = full * (den - 1) / den;
+  return c > 0 ? c : 1;
+}
+
 inline int next_pow2(int v) {
   int p = 1;
   while (p < v) p <<= 1;

@@ -1069,9 +1069,10 @@ int launch(const FusedArgs& a, hipStream_t s) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, 0) != hipSuccess || per_cu <= 0)
       per_cu = 2;
     const int64_t need = (work + kGroups - 1) / kGroups;
-    // KGX_FUSED_SHARE_GPU: leave an eighth of the block slots free so a
-    // concurrent collective's kernels (RCCL halo all-to-all) are not starved
-    const int64_t cap = a.share_gpu ? int64_t(per_cu) * cus * 7 / 8 : int64_t(per_cu) * cus;
+    // KGX_FUSED_SHARE_GPU: leave 1/den of the block slots free (share_den(),
+    // default an eighth) so a concurrent collective's kernels (RCCL halo
+    // all-to-all) and the side stream's packing are not starved
+    const int64_t cap = a.share_gpu ? shared_cap(int64_t(per_cu) * cus) : int64_t(per_cu) * cus;
     hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kThreads), 0, s, a);
     KGX_CHECK_LAUNCH();
   }
@@ -1088,7 +1089,7 @@ int launch(const FusedArgs& a, hipStream_t s) {
         cus2 = 256;
     }
     const int64_t need = (a.n_short_end - a.n_long + kShortRows - 1) / kShortRows;
-    const int64_t cap = a.share_gpu ? int64_t(per_cu) * cus2 * 7 / 8 : int64_t(per_cu) * cus2;
+    const int64_t cap = a.share_gpu ? shared_cap(int64_t(per_cu) * cus2) : int64_t(per_cu) * cus2;
     hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kThreads), 0, s, a);
     KGX_CHECK_LAUNCH();
   }
@@ -1104,7 +1105,7 @@ int launch(const FusedArgs& a, hipStream_t s) {
                     : (extra ? spmm_gemm_tiny_kernel<RED, W, true, 2, TWO> : spmm_gemm_tiny_kernel<RED, W, false, 2, TWO>);
       const int rows = part ? tiny_rows<1>() : tiny_rows<2>();
       const int64_t need = (b.n_tiny + rows - 1) / rows;
-      const int64_t cap = a.share_gpu ? int64_t(cu_count()) * 7 / 8 : int64_t(cu_count());
+      const int64_t cap = a.share_gpu ? shared_cap(int64_t(cu_count())) : int64_t(cu_count());
       hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kTinyThreads), 0, s, b);
       KGX_CHECK_LAUNCH();
     }

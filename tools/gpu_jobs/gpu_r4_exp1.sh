@@ -15,6 +15,8 @@ for r in 1 2; do
 done
 KGX_EXACT_FORK=2 timeout -k 10 300 python -u -m pytest tests/test_gpu_configs.py -q -x -p no:cacheprovider \
   -k "exact_aggregation_bitwise" --timeout 240 --timeout-method thread > gpurun_out/r4x/exact_fork_test.log 2>&1 || exit $?
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4x/sim_ns -o run \
+timeout -k 10 900 python tools/shard_sim.py --config ns --world 8 --chunks 1 --merge-unit chunk --steps 5 \
+  --share-den 8,4,2,16 > gpurun_out/r4x/sim_ns_share.jsonl 2> gpurun_out/r4x/sim_ns_share.err || exit $?
+timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4x/sim_ns -o run \
   -- python3 tools/shard_sim.py --config ns --world 8 --chunks 1 --merge-unit chunk --steps 5 \
   > gpurun_out/r4x/sim_ns.jsonl 2> gpurun_out/r4x/sim_ns.err

@@ -144,6 +144,9 @@ def main():
     ap.add_argument("--merge-unit", default="step", help="KGX_HALO_MERGE values: step, chunk")
     ap.add_argument("--a-late", default="0", help="KGX_HALO_A_LATE values (1: own-only rows after the merged pass)")
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--share-den", default="8",
+                    help="KGX_SHARE_DEN values timed on each built shard (the overlapped passes leave 1/den of "
+                         "the block slots to the side stream)")
     ap.add_argument("--nodes", type=int, default=None)
     ap.add_argument("--edges", type=int, default=None)
     ap.add_argument("--link-gbps", type=float, default=0.0,
@@ -189,41 +192,44 @@ def main():
             layer = kd.ShardedGINConv(F, sg, aggregator="sum")
         else:
             layer = kd.ShardedSAGEConv(F, sg, aggregator="mean")
-        with torch.no_grad():
-            layer(x)
-            g_own, g_chunks = sg.own_halo_parts()
-            for _ in range(2):
+        for den in args.share_den.split(","):
+            os.environ["KGX_SHARE_DEN"] = den
+            with torch.no_grad():
                 layer(x)
-            torch.cuda.synchronize()
-            kops.EVENT_SINK = []
-            t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            t0.record()
-            for _ in range(args.steps):
-                layer(x)
-            t1.record()
-            torch.cuda.synchronize()
-        ev = kops.EVENT_SINK
-        kops.EVENT_SINK = None
-        per = len(ev) // args.steps
-        launch_ms = [sum(ev[i * per + j][0].elapsed_time(ev[i * per + j][1]) for i in range(args.steps)) / args.steps
-                     for j in range(per)]
-        pp = sg._pp
-        if pp is not None:
-            g_chunks = pp.parts
-        recv_rows = (pp.n_rows * (P - 1) // P if pp.kind == "allgather" else pp.n_rows) if pp else sg.n_halo
-        print(json.dumps({
-            "config": args.config, "layer": layer_kind, "scaling": scaling, "nodes": n_glob, "edges": e_glob,
-            "features": F, "world": P, "exchange": pp.kind if pp else "pull", "chunks": K,
-            "push_pull": pp is not None and pp.kind == "halo", "merged": merged == "1", "merge_unit": unit,
-            "a_late": a_late == "1",
-            "link_gbps": args.link_gbps, "step_ms": round(t0.elapsed_time(t1) / args.steps, 3),
-            "launch_ms": [round(v, 3) for v in launch_ms],
-            "own_edges": g_own.kept, "chunk_edges": [g.kept for g in g_chunks],
-            "halo_rows_pull_only": sg.n_halo, "halo_rows": pp.n_rows if pp else sg.n_halo,
-            "received_MB": recv_rows * F * 4 / 1e6,
-            "pulled": pp.n_pull if pp else sg.n_halo, "pushed": pp.n_push if pp else 0,
-            "chunk_items": [g.n_items for g in g_chunks], "n_local": sg.n_local,
-        }), flush=True)
+                g_own, g_chunks = sg.own_halo_parts()
+                for _ in range(2):
+                    layer(x)
+                torch.cuda.synchronize()
+                kops.EVENT_SINK = []
+                t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                t0.record()
+                for _ in range(args.steps):
+                    layer(x)
+                t1.record()
+                torch.cuda.synchronize()
+            ev = kops.EVENT_SINK
+            kops.EVENT_SINK = None
+            per = len(ev) // args.steps
+            launch_ms = [sum(ev[i * per + j][0].elapsed_time(ev[i * per + j][1]) for i in range(args.steps))
+                         / args.steps for j in range(per)]
+            pp = sg._pp
+            if pp is not None:
+                g_chunks = pp.parts
+            recv_rows = (pp.n_rows * (P - 1) // P if pp.kind == "allgather" else pp.n_rows) if pp else sg.n_halo
+            print(json.dumps({
+                "config": args.config, "layer": layer_kind, "scaling": scaling, "nodes": n_glob, "edges": e_glob,
+                "features": F, "world": P, "exchange": pp.kind if pp else "pull", "chunks": K,
+                "push_pull": pp is not None and pp.kind == "halo", "merged": merged == "1", "merge_unit": unit,
+                "a_late": a_late == "1", "share_den": int(den),
+                "link_gbps": args.link_gbps, "step_ms": round(t0.elapsed_time(t1) / args.steps, 3),
+                "launch_ms": [round(v, 3) for v in launch_ms],
+                "own_edges": g_own.kept, "chunk_edges": [g.kept for g in g_chunks],
+                "halo_rows_pull_only": sg.n_halo, "halo_rows": pp.n_rows if pp else sg.n_halo,
+                "received_MB": recv_rows * F * 4 / 1e6,
+                "pulled": pp.n_pull if pp else sg.n_halo, "pushed": pp.n_push if pp else 0,
+                "chunk_items": [g.n_items for g in g_chunks], "n_local": sg.n_local,
+            }), flush=True)
+        os.environ.pop("KGX_SHARE_DEN", None)
         del sg, layer, x, g_own, g_chunks
         torch.cuda.empty_cache()
 
