@@ -28,11 +28,15 @@ def add_self_loops(edge_index: torch.Tensor, num_nodes: int) -> torch.Tensor:
     return torch.cat([edge_index, torch.stack([loops, loops], dim=0)], dim=1)
 
 
-def compute_gcn_normalization(edge_index: torch.Tensor, num_nodes: int) -> torch.Tensor:
-    """utils/main.py:20-33."""
+def compute_gcn_normalization(edge_index: torch.Tensor, num_nodes: int, degrees=None) -> torch.Tensor:
+    """utils/main.py:20-33.  degrees (test instrument, default None = the
+    reference): the fp32 in-degree vector to use instead of the one this edge
+    set gives -- the whole graph's, when edge_index holds only the in-edges of
+    sampled rows (tests/oracle_sample.py)."""
     source, target = edge_index[0], edge_index[1]
     ones = torch.ones_like(source, dtype=K.FLOATX)
-    degrees = K.segment_sum(ones, target, num_nodes)
+    if degrees is None:
+        degrees = K.segment_sum(ones, target, num_nodes)
     dinv = K.power(K.add(degrees, 1e-12), -0.5)
     dinv = K.where(K.isinf(dinv), torch.zeros_like(dinv), dinv)
     return K.multiply(K.take(dinv, target, axis=0), K.take(dinv, source, axis=0))
@@ -129,8 +133,10 @@ def _as_2xE(ei: torch.Tensor) -> torch.Tensor:
     return ei
 
 
-def gcn_forward(x, edge_index, kernel, bias=None, add_self_loops_: bool = True, normalize: bool = True):
-    """GCNConv.call (gcn_conv.py:275-364) incl. message (:233-248) and update (:266-272)."""
+def gcn_forward(x, edge_index, kernel, bias=None, add_self_loops_: bool = True, normalize: bool = True,
+                degrees=None):
+    """GCNConv.call (gcn_conv.py:275-364) incl. message (:233-248) and update (:266-272).
+    degrees: see compute_gcn_normalization (sampled-row checks only)."""
     x = K.cast(x, torch.float32)
     ei = _as_2xE(edge_index)
     kernel = K.convert(kernel)
@@ -144,7 +150,7 @@ def gcn_forward(x, edge_index, kernel, bias=None, add_self_loops_: bool = True, 
     if e == 0:
         y = torch.matmul(x, kernel)
         return y + bias if bias is not None else y
-    w = compute_gcn_normalization(ei, n) if normalize else torch.ones((e,), dtype=torch.float32)
+    w = compute_gcn_normalization(ei, n, degrees) if normalize else torch.ones((e,), dtype=torch.float32)
     src, dst = ei[0], ei[1]
     x_j = K.take(x, src, axis=0)
     _x_i = K.take(x, dst, axis=0)  # gathered by the reference (message_passing.py:196), unused by GCN

@@ -34,6 +34,7 @@ from keras_geometric_amd import _native as nat
 from keras_geometric_amd import graph as G
 from keras_geometric_amd import ops as kops
 from keras_geometric_amd import synthetic
+import oracle_sample as OS
 from oracle import reference as R
 
 pytestmark = [pytest.mark.gpu, pytest.mark.slow, pytest.mark.timeout(900)]
@@ -269,3 +270,46 @@ def test_c5_sage_mean_properties(dev):
     a = torch.cat([x[rows], sp[rows]], 1)
     Wcat = torch.cat([layer.lin_self.kernel.detach(), layer.lin_neigh.kernel.detach()], 0)
     _dense_bound_check(y[rows], a, Wcat, layer.bias.detach(), relu=True)
+
+
+# ------------------------------------------------ full-size layers vs the oracle on sampled rows
+def _oracle_sampled(got, ref, scale, what):
+    err = OS.scaled_err(got, ref, scale)
+    print(f"{what}: layer vs oracle on {got.shape[0]} sampled rows, max scaled err {err:.3e}")
+    assert err <= 1e-5, err
+
+
+def test_c4_gin_layer_vs_oracle_sampled(c4):
+    """The C4 GIN layer on the fused 256-wide kernels vs the oracle's op-for-op
+    forward on ~1500 sampled rows incl. the largest hubs (tests/oracle_sample.py);
+    bar: 1e-5 of the same forward on |x|, |W|, |b| (re-associated sums)."""
+    ei, x = c4
+    n, e, f = C4
+    layer = kgx.GINConv(f, aggregator="sum", eps_init=0.25)
+    with torch.no_grad():
+        layer([x, ei])
+        dense = layer.mlp.layers[-1]
+        dense.bias.copy_(torch.randn(f, generator=torch.Generator().manual_seed(21)).to(x.device))
+        y = layer([x, ei])
+    W, b = dense.kernel.detach().cpu(), dense.bias.detach().cpu()
+    rows = OS.sample_rows(ei, n)
+    ref = OS.gin_rows(ei, x, rows, [(W, b, None)], 0.25)
+    scale = OS.gin_rows(ei, x.abs(), rows, [(W.abs(), b.abs(), None)], 0.25)
+    _oracle_sampled(y[rows], ref, scale, "C4 GINConv")
+
+
+def test_c5_sage_layer_vs_oracle_sampled(dev):
+    n, e, f = C5
+    ei = synthetic.rmat_edge_index(n, e, seed=0, device=dev)
+    x = torch.randn(n, f, device=dev, generator=torch.Generator(device=dev).manual_seed(8))
+    layer = kgx.SAGEConv(f, aggregator="mean")
+    with torch.no_grad():
+        layer([x, ei])
+        layer.bias.copy_(torch.randn(f, generator=torch.Generator().manual_seed(9)).to(dev))
+        y = layer([x, ei])
+    wn, ws, b = (t.detach().cpu() for t in (layer.lin_neigh.kernel, layer.lin_self.kernel, layer.bias))
+    rows = OS.sample_rows(ei, n)
+    ref = OS.sage_rows(ei, x, rows, wn, ws, b)
+    scale = OS.sage_rows(ei, x.abs(), rows, wn.abs(), ws.abs(), b.abs())
+    _oracle_sampled(y[rows], ref, scale, "C5 SAGEConv")
+    G.clear_cache()

@@ -138,3 +138,26 @@ def test_tiny_tail_bit_identical_fullsize(big):
             g._kgx_tiny = saved
         assert torch.equal(y_tiny, y_short), red
         del y_tiny, y_short
+
+
+def test_ns_gcn_layer_vs_oracle_sampled(big):
+    """The north-star GCNConv layer (fused kernels, split hub rows) vs the
+    oracle's op-for-op forward on ~1500 sampled rows incl. the largest hubs,
+    with the whole graph's degrees (tests/oracle_sample.py); bar: 1e-5 of the
+    same forward on |x|, |W|, |b| (re-associated sums)."""
+    import keras_geometric_amd as kgx
+    import oracle_sample as OS
+
+    ei, _, x = big
+    layer = kgx.GCNConv(F)
+    with torch.no_grad():
+        layer([x, ei])
+        layer.bias.copy_(torch.randn(F, generator=torch.Generator().manual_seed(3)).to(x.device))
+        y = layer([x, ei])
+    W, b = layer.kernel.detach().cpu(), layer.bias.detach().cpu()
+    rows = OS.sample_rows(ei, N)
+    ref = OS.gcn_rows(ei, x, rows, W, b)
+    scale = OS.gcn_rows(ei, x.abs(), rows, W.abs(), b.abs())
+    err = OS.scaled_err(y[rows], ref, scale)
+    print(f"NS GCNConv vs oracle on {rows.numel()} sampled rows: max scaled err {err:.3e}")
+    assert err <= 1e-5, err

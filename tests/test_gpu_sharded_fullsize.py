@@ -33,6 +33,7 @@ import keras_geometric_amd as kgx
 from keras_geometric_amd import distributed as kd
 from keras_geometric_amd import graph as G
 from keras_geometric_amd import synthetic
+import oracle_sample as OS
 from test_gpu_distributed import AsyncThreadComm, ThreadHub
 
 pytestmark = [pytest.mark.gpu, pytest.mark.slow, pytest.mark.timeout(900)]
@@ -78,7 +79,10 @@ def _run(world, make_layer, n, e, f, x, seed, chunks, exchange="halo"):
     return torch.cat([res[r][1] for r in range(world)]), res[0][2]
 
 
-def _check(got, single, abs_single, x, ei, weights):
+def _check(got, single, abs_single, x, ei, weights, oracle_rows=None):
+    """The sharded rows vs the single-GPU layer on every row, and (oracle_rows:
+    weights, x -> the oracle on sampled rows, tests/oracle_sample.py) vs the
+    CPU oracle on ~1500 sampled rows incl. the largest hubs."""
     with torch.no_grad():
         single([x, ei])
         single.set_weights([w.cpu().numpy() for w in weights])
@@ -90,6 +94,12 @@ def _check(got, single, abs_single, x, ei, weights):
     print(f"sharded vs single-GPU: max scaled err {err:.3e}")
     assert err <= 1e-5, err
     assert got.abs().max().item() > 0
+    if oracle_rows is not None:
+        rows = OS.sample_rows(ei, x.shape[0])
+        ref_o = oracle_rows([w.detach().cpu() for w in weights], x, rows)
+        err_o = OS.scaled_err(got[rows], ref_o, scale[rows])
+        print(f"sharded vs oracle on {rows.numel()} sampled rows: max scaled err {err_o:.3e}")
+        assert err_o <= 1e-5, err_o
     return err
 
 
@@ -107,7 +117,7 @@ def test_c4_sharded_gin_sum_world8_fullsize(dev):
                         n, e, f, x, seed=0, chunks=2)
     ei = synthetic.rmat_edge_index(n, e, seed=0, device=dev)
     _check(got, kgx.GINConv(f, aggregator="sum", eps_init=0.25), kgx.GINConv(f, aggregator="sum", eps_init=0.25),
-           x, ei, weights)
+           x, ei, weights, lambda w, x_, rows: OS.gin_rows(ei, x_, rows, [(w[0], w[1], None)], 0.25))
 
 
 @pytest.mark.parametrize("exchange", ["halo", "allgather"])
@@ -117,4 +127,6 @@ def test_c5_sharded_sage_mean_world4_fullsize(dev, exchange):
     got, weights = _run(world, lambda sg: kd.ShardedSAGEConv(f, sg, aggregator="mean"), n, e, f, x, seed=0,
                         chunks=2, exchange=exchange)
     ei = synthetic.rmat_edge_index(n, e, seed=0, device=dev)
-    _check(got, kgx.SAGEConv(f, aggregator="mean"), kgx.SAGEConv(f, aggregator="mean"), x, ei, weights)
+    # SAGEConv.weights: bias, lin_neigh, lin_self (sage_conv.py:405-439)
+    _check(got, kgx.SAGEConv(f, aggregator="mean"), kgx.SAGEConv(f, aggregator="mean"), x, ei, weights,
+           lambda w, x_, rows: OS.sage_rows(ei, x_, rows, w[1], w[2], w[0]))
