@@ -394,8 +394,10 @@ def main() -> None:
     launches = len(events) // args.steps
 
     fused = kind == "gcn" and not args.exact and kops.fused_transform_supported(f_in, f_out)
-    # GINConv's (1+eps) x_i + aggr -> Dense in one launch (1 GPU; the sharded passes stay unfused)
-    fused_gin = kind == "gin" and world == 1 and not args.exact and kops.fused_transform_supported(f_in, f_out)
+    # GINConv's (1+eps) x_i + aggr -> Dense in one launch (1 GPU), or in each of the sharded layer's
+    # merged halo passes (N > 1: two-table gathers, kgx_spmm_gemm_f256_ex)
+    fused_gin = kind == "gin" and not args.exact and kops.fused_transform_supported(f_in, f_out,
+                                                                                     two_table=world > 1)
     if kind == "gcn":
         # SURVEY.md §8d per rank; at N>1 the accumulating halo-chunk passes' re-reads
         # of the rows they add to are implementation overhead, not algorithmic bytes

@@ -75,8 +75,8 @@ def test_cache_key_tracks_version():
 
 def test_fused_shape_routing(monkeypatch):
     """Which shapes take a fused aggregate -> transform kernel: F_in 128 ->
-    128 (kgx_spmm_gemm), 256 -> 256 (kgx_spmm_gemm_f256, one table only:
-    the sharded passes' two-table gathers stay on F_in 128); KGX_FUSED256=0 /
+    128 (kgx_spmm_gemm), 256 -> 256 (kgx_spmm_gemm_f256; the sharded passes'
+    two-table gathers through kgx_spmm_gemm_f256_ex); KGX_FUSED256=0 /
     KGX_FUSED=0 turn them off."""
     from keras_geometric_amd import ops as kops
 
