@@ -398,6 +398,8 @@ def main() -> None:
     # merged halo passes (N > 1: two-table gathers, kgx_spmm_gemm_f256_ex)
     fused_gin = kind == "gin" and not args.exact and kops.fused_transform_supported(f_in, f_out,
                                                                                      two_table=world > 1)
+    # SAGEConv's neighbour map in the aggregation's store (1 GPU; the sharded layer keeps kgx_dense)
+    fused_sage = kind == "sage" and world == 1 and not args.exact and kops.fused_sage_supported(f_in, f_out)
     if kind == "gcn":
         # SURVEY.md §8d per rank; at N>1 the accumulating halo-chunk passes' re-reads
         # of the rows they add to are implementation overhead, not algorithmic bytes
@@ -414,6 +416,12 @@ def main() -> None:
         balg = b_alg_spmm(n_rows, e_agg, f_in, weighted=False, f_out=f_out) + 4 * n_rows * f_in
         kernel = ("spmm_gemm256_kernel", "spmm_gemm256_tiny2_kernel", "spmm_gemm256_tiny_kernel",
                   "spmm_gemm256_fixup_kernel")
+    elif fused_sage:
+        # SAGE mean with W_neigh fused into the aggregation's store (kgx_spmm_gemm, F_in 100):
+        # gathered rows F_in wide, output rows F_out wide (the accumulate's re-read of the
+        # kgx_dense x W_self + b rows is implementation overhead, not counted)
+        balg = b_alg_spmm(n_rows, e_agg, f_in, weighted=False, f_out=f_out)
+        kernel = ("spmm_gemm_kernel", "spmm_gemm_short_kernel", "spmm_gemm_tiny_kernel", "spmm_gemm_fixup_kernel")
     else:  # GIN: + the x_i root row of the (1+eps) x_i + aggr epilogue; SAGE mean: plain gather-sum
         balg = b_alg_spmm(n_rows, e_agg, f_in, weighted=False) + (4 * n_rows * f_in if kind == "gin" else 0)
         kernel = ("spmm_kernel", "spmm_short_kernel", "spmm_fixup_kernel")
@@ -481,7 +489,8 @@ def main() -> None:
             "features": [f_in, f_out],
             "mode": ("exact" if args.exact else "split-hub")
                     + (", fused aggregate->transform (W on bf16x3-split MFMA, f32-accurate)" if fused or fused_gin
-                       else ""),
+                       else ", W_neigh fused into the aggregation's store (bf16x3-split MFMA), x W_self + b by kgx_dense"
+                       if fused_sage else ""),
             "parallelism": f"dst-shard{world}" if world > 1 else "single",
         },
         "edges_per_s_aggregation_kernel": e_total / (kern_ms * 1e-3) if kern_ms > 0 else None,

@@ -205,13 +205,14 @@ int kgx_dropout_mask(uint64_t seed, float p, const int32_t* keys, int64_t n, int
  *   out[i,:] (+)= bias + PRE( REDUCE_{e in row i} x[idx[e],:] * (w ? w[e] : 1) ) @ W
  *   PRE = identity, or gin_scale * x[i,:] + aggr with KGX_FUSED_PRE_GIN;
  *   "+=" (read-add-write of out) with KGX_FUSED_ACCUMULATE, used to add the
- *   halo-source part of a sharded row after its local part (distributed.py).
+ *   halo-source part of a sharded row after its local part (distributed.py),
+ *   and SAGEConv's neighbour map onto out = b + x W_self (sage_conv.py:404-433).
  * Replaces GCNConv's per-edge x_j @ W + segment_sum + bias (gcn_conv.py:233-272)
  * and GINConv's (1+eps)x + aggr -> single-Dense MLP (gin_conv.py:216-225) by the
  * algebraically equal aggregate-then-transform order (W applied once per row
  * on MFMA as the six significant products of a three-way bf16 split of both
  * operands: f32-accurate); tolerance-equal to the reference, not bit-equal.
- * Shapes: F_in == 128, F_out a multiple of 16 <= 128, W [F_in, F_out] row-major.
+ * Shapes: F_in and F_out multiples of 4 <= 128, W [F_in, F_out] row-major.
  * reduce in {SUM, MEAN, MAX, MIN}; partials: n_slots * 128 floats.
  * agg_out (optional, [n, ld_agg >= F_in]): also store PRE(REDUCE(...)), the
  * rows before the transform — what the backward's dW = agg^T dOut needs.
@@ -219,7 +220,9 @@ int kgx_dropout_mask(uint64_t seed, float p, const int32_t* keys, int64_t n, int
 /* KGX_FUSED_SHARE_GPU: launch 7/8 of the resident grid, leaving block slots
  * for kernels of a concurrent stream (the sharded layer's RCCL exchange).
  * KGX_FUSED_RELU: out = max(bias + ..., 0), the activation of a GIN MLP's
- * first Dense (gin_conv.py:129-162); not combinable with ACCUMULATE. */
+ * first Dense (gin_conv.py:129-162) or SAGEConv's activation; with ACCUMULATE
+ * it applies to the sum (out = max(out + ..., 0)).  kgx_spmm_gemm_f256 rejects
+ * RELU | ACCUMULATE. */
 enum { KGX_FUSED_PRE_GIN = 1, KGX_FUSED_ACCUMULATE = 2, KGX_FUSED_SHARE_GPU = 4, KGX_FUSED_RELU = 8 };
 int kgx_spmm_gemm(int reduce, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
                   const int32_t* items, int64_t n_items, const int32_t* split, int64_t n_split,

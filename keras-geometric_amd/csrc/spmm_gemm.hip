@@ -10,7 +10,8 @@
 // re-association only (tolerance-checked, not bit-checked).
 //
 // Block = 512 threads = 16 row-groups of 32 lanes (F_in = 128: float4 per
-// lane).  Per iteration the block takes 16 consecutive schedule items; each
+// lane; F_in < 128, a multiple of 4: the lanes past it re-load column 0 and
+// put zeros in the planes, W's rows past F_in load as zero).  Per iteration the block takes 16 consecutive schedule items; each
 // group reduces its item's edges exactly like spmm_kernel (4 gathers in
 // flight, sequential RN adds) and writes the row, split three ways into bf16
 // hi/mid/lo planes, to an LDS tile; then wave w (of 8) computes output columns
@@ -62,7 +63,8 @@ struct FusedArgs {
   const float* w;
   const float* x;  // [*, 128] gathered rows
   int64_t ld_x;
-  const float* W;  // [128, F_out] row-major
+  const float* W;  // [F_in, F_out] row-major
+  int F_in;   // <= 128: lanes past it gather nothing new and carry zeros
   int F_out;
   const float* bias;  // [F_out] or null
   float* out;
@@ -73,7 +75,7 @@ struct FusedArgs {
   int pre_gin;      // apply gin_scale * x[row] + aggr before the transform
   int accumulate;   // out += result
   int share_gpu;    // launch 7/8 of the resident grid
-  int relu;         // out = max(result, 0) (not with accumulate)
+  int relu;         // out = max(result, 0), after the accumulate
   float gin_scale;
   int debug;        // experiment builds only (-DKGX_EXPERIMENTS, env KGX_FUSED_DEBUG): 1 skip MFMA, 2 skip stores (main / short kernels); 4 / 8 / 16 tiny kernel: skip MFMA, skip stores, gathers all from row 0
   int64_t n_short_end;  // items [n_long, n_short_end): spmm_gemm_short_kernel
@@ -181,11 +183,14 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
   const int g = tid >> 5;     // row-group 0..15
   const int lane = tid & 31;  // lane in the group
   const int f = lane * 4;
+  const bool f_ok = f < a.F_in;  // lanes past F_in (F_in < 128) load column 0 again and carry zeros
+  const int fg = f_ok ? f : 0;
   const int wave = tid >> 6;  // 0..7 -> output columns [16 wave, 16 wave + 16)
   const int wl = tid & 63;    // lane in the wave
   const int n_col = wave * 16 + (wl & 15);
   const int q = wl >> 4;
   const bool mfma_wave = wave * 16 < a.F_out;
+  const bool w_ok = mfma_wave && n_col < a.F_out;  // W rows k >= F_in and columns >= F_out load as 0
 
   // W fragment for this wave's 16 columns, K permuted: k = 32 q + s.
 #if KGX_FUSED_BF16X3
@@ -198,8 +203,8 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
     u32x4_t ph, pm, pl;
 #pragma unroll
     for (int j = 0; j < 8; j += 2) {
-      const float v0 = mfma_wave ? a.W[int64_t(32 * q + 8 * s + j) * a.F_out + n_col] : 0.0f;
-      const float v1 = mfma_wave ? a.W[int64_t(32 * q + 8 * s + j + 1) * a.F_out + n_col] : 0.0f;
+      const float v0 = w_ok && 32 * q + 8 * s + j < a.F_in ? a.W[int64_t(32 * q + 8 * s + j) * a.F_out + n_col] : 0.0f;
+      const float v1 = w_ok && 32 * q + 8 * s + j + 1 < a.F_in ? a.W[int64_t(32 * q + 8 * s + j + 1) * a.F_out + n_col] : 0.0f;
       uint32_t h, m_, l;
       split3_pair(v0, v1, h, m_, l);
       ph[j / 2] = h;
@@ -213,7 +218,7 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
 #else
   float wb[32];
 #pragma unroll
-  for (int s = 0; s < 32; ++s) wb[s] = mfma_wave ? a.W[int64_t(32 * q + s) * a.F_out + n_col] : 0.0f;
+  for (int s = 0; s < 32; ++s) wb[s] = w_ok && 32 * q + s < a.F_in ? a.W[int64_t(32 * q + s) * a.F_out + n_col] : 0.0f;
 #endif
 #if KGX_FUSED_TSTORE && KGX_FUSED_BF16X3
   const int c4 = wave * 16 + 4 * q;
@@ -262,7 +267,7 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
       if (u < pn)  // exec-masked: rows of degree < PF issue no redundant loads
-        vload<4>(pv[u], gsrc<TWO>(a, c[u]) + f);
+        vload<4>(pv[u], gsrc<TWO>(a, c[u]) + fg);
     }
   };
 
@@ -309,7 +314,7 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
 #endif
       float v[B][4];
 #pragma unroll
-      for (int u = 0; u < B; ++u) vload<4>(v[u], gsrc<TWO>(a, c[u]) + f);
+      for (int u = 0; u < B; ++u) vload<4>(v[u], gsrc<TWO>(a, c[u]) + fg);
 #pragma unroll
       for (int u = 0; u < B; ++u)
 #pragma unroll
@@ -329,11 +334,15 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
     for (int k = 0; k < 4; ++k) r[k] = full_row ? R::finish(acc[k], end - beg) : 0.0f;
     if (full_row && a.pre_gin) {
       float xv[4];
-      vload<4>(xv, a.x + int64_t(row) * a.ld_x + f);
+      vload<4>(xv, a.x + int64_t(row) * a.ld_x + fg);
 #pragma unroll
       for (int k = 0; k < 4; ++k) r[k] = __fadd_rn(__fmul_rn(a.gin_scale, xv[k]), r[k]);
     }
-    if (full_row && a.agg_out) vstore<4>(a.agg_out + int64_t(row) * a.ld_agg + f, r);
+    if (full_row && a.agg_out && f_ok) vstore<4>(a.agg_out + int64_t(row) * a.ld_agg + f, r);
+    if (a.F_in < kFin) {  // wave-uniform: lanes past F_in put zeros in the planes
+#pragma unroll
+      for (int k = 0; k < 4; ++k) r[k] = f_ok ? r[k] : 0.0f;
+    }
 #if KGX_FUSED_BF16X3
     {
       bf16x4_t ph, pm, pl;
@@ -411,7 +420,7 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
 #if KGX_FUSED_TSTORE && KGX_FUSED_BF16X3
       // straight from the accumulators: lane (m, q) writes columns 16 wave + 4 q .. + 3 of tile row m
       const int rr = tile_row[m];
-      if (rr >= 0 && !(a.debug & 2)) {
+      if (rr >= 0 && c4 < a.F_out && !(a.debug & 2)) {
         float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + c4);
         const float4 b4 = *reinterpret_cast<const float4*>(&sbias[c4]);
         float4 v = make_float4((d0[0] + d1[0]) + b4.x, (d0[1] + d1[1]) + b4.y, (d0[2] + d1[2]) + b4.z,
@@ -491,11 +500,14 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
   const int g = tid >> 5;
   const int lane = tid & 31;
   const int f = lane * 4;
+  const bool f_ok = f < a.F_in;  // lanes past F_in (F_in < 128) load column 0 again and carry zeros
+  const int fg = f_ok ? f : 0;
   const int wave = tid >> 6;
   const int wl = tid & 63;
   const int n_col = wave * 16 + (wl & 15);
   const int q = wl >> 4;
   const bool mfma_wave = wave * 16 < a.F_out;
+  const bool w_ok = mfma_wave && n_col < a.F_out;  // W rows k >= F_in and columns >= F_out load as 0
 
   bf16x8_t wfh[4], wfm[4], wfl[4];
 #pragma unroll
@@ -504,8 +516,8 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
     u32x4_t ph, pm, pl;
 #pragma unroll
     for (int j = 0; j < 8; j += 2) {
-      const float v0 = mfma_wave ? a.W[int64_t(32 * q + 8 * s + j) * a.F_out + n_col] : 0.0f;
-      const float v1 = mfma_wave ? a.W[int64_t(32 * q + 8 * s + j + 1) * a.F_out + n_col] : 0.0f;
+      const float v0 = w_ok && 32 * q + 8 * s + j < a.F_in ? a.W[int64_t(32 * q + 8 * s + j) * a.F_out + n_col] : 0.0f;
+      const float v1 = w_ok && 32 * q + 8 * s + j + 1 < a.F_in ? a.W[int64_t(32 * q + 8 * s + j + 1) * a.F_out + n_col] : 0.0f;
       uint32_t h, m_, l;
       split3_pair(v0, v1, h, m_, l);
       ph[j / 2] = h;
@@ -559,7 +571,7 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
       for (int r = 0; r < kRPG; ++r)
 #pragma unroll
         for (int u = 0; u < kSPF; ++u)
-          if (u < deg[r]) vload<4>(v[r][u], gsrc<TWO>(a, c[r][u]) + f);
+          if (u < deg[r]) vload<4>(v[r][u], gsrc<TWO>(a, c[r][u]) + fg);
 #pragma unroll
       for (int r = 0; r < kRPG; ++r)
 #pragma unroll
@@ -587,7 +599,7 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
           if constexpr (WEIGHTED) wt[u] = a.w[ee];
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) vload<4>(v[u], gsrc<TWO>(a, c[u]) + f);
+        for (int u = 0; u < 2; ++u) vload<4>(v[u], gsrc<TWO>(a, c[u]) + fg);
 #pragma unroll
         for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -606,11 +618,15 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
       for (int k = 0; k < 4; ++k) v[k] = ok ? R::finish(acc[r][k], deg[r]) : 0.0f;
       if (ok && a.pre_gin) {
         float xv[4];
-        vload<4>(xv, a.x + int64_t(row[r]) * a.ld_x + f);
+        vload<4>(xv, a.x + int64_t(row[r]) * a.ld_x + fg);
 #pragma unroll
         for (int k = 0; k < 4; ++k) v[k] = __fadd_rn(__fmul_rn(a.gin_scale, xv[k]), v[k]);
       }
-      if (ok && a.agg_out) vstore<4>(a.agg_out + int64_t(row[r]) * a.ld_agg + f, v);
+      if (ok && a.agg_out && f_ok) vstore<4>(a.agg_out + int64_t(row[r]) * a.ld_agg + f, v);
+      if (a.F_in < kFin) {  // wave-uniform: lanes past F_in put zeros in the planes
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = f_ok ? v[k] : 0.0f;
+      }
       bf16x4_t ph, pm, pl;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -676,7 +692,7 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
 #pragma unroll
       for (int rb = 0; rb < kRPG; ++rb) {
         const int rr = tile_row[16 * rb + m];
-        if (rr >= 0) {
+        if (rr >= 0 && c4 < a.F_out) {
           float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + c4);
           const float4 b4 = *reinterpret_cast<const float4*>(&sbias[c4]);
           float4 v = make_float4(d[rb][0] + b4.x, d[rb][1] + b4.y, d[rb][2] + b4.z, d[rb][3] + b4.w);
@@ -776,6 +792,7 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
     const int q = wl >> 4, m = wl & 15;
     const int n_col = wave * 16 + m;
     const bool mfma_wave = wave * 16 < a.F_out;
+    const bool w_ok = mfma_wave && n_col < a.F_out;
     bf16x8_t wfh[4], wfm[4], wfl[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -783,8 +800,8 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
       u32x4_t ph, pm, pl;
 #pragma unroll
       for (int j = 0; j < 8; j += 2) {
-        const float v0 = mfma_wave ? a.W[int64_t(32 * q + 8 * s + j) * a.F_out + n_col] : 0.0f;
-        const float v1 = mfma_wave ? a.W[int64_t(32 * q + 8 * s + j + 1) * a.F_out + n_col] : 0.0f;
+        const float v0 = w_ok && 32 * q + 8 * s + j < a.F_in ? a.W[int64_t(32 * q + 8 * s + j) * a.F_out + n_col] : 0.0f;
+        const float v1 = w_ok && 32 * q + 8 * s + j + 1 < a.F_in ? a.W[int64_t(32 * q + 8 * s + j + 1) * a.F_out + n_col] : 0.0f;
         uint32_t h, m_, l;
         split3_pair(v0, v1, h, m_, l);
         ph[j / 2] = h;
@@ -846,7 +863,7 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
 #pragma unroll
         for (int rb = 0; rb < kTinyRPG; ++rb) {
           const int rr = trow[b][16 * rb + m];
-          if (rr >= 0) {
+          if (rr >= 0 && c4 < a.F_out) {
             float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + c4);
             const float4 b4 = *reinterpret_cast<const float4*>(&sbias[c4]);
             float4 v = make_float4(d[rb][0] + b4.x, d[rb][1] + b4.y, d[rb][2] + b4.z, d[rb][3] + b4.w);
@@ -864,7 +881,7 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int rr = trow[b][16 * rb + 4 * q + j];
-            if (rr >= 0) {
+            if (rr >= 0 && n_col < a.F_out) {
               float* dst = a.out + int64_t(rr) * a.ld_o + n_col;
               float v = d[rb][j] + bcol;
               if (a.accumulate) v = __fadd_rn(*dst, v);
@@ -882,6 +899,8 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
   // ---- producers: tile i at iteration i
   const int pt = tid - 512;
   const int g = pt >> 5, lane = pt & 31, f = lane * 4;
+  const bool f_ok = f < a.F_in;  // lanes past F_in (F_in < 128) load column 0 again and carry zeros
+  const int fg = f_ok ? f : 0;
   struct Rec {
     int4 p[kTinyRPG];
     float2 w[kTinyRPG];
@@ -903,11 +922,11 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
     for (int j = 0; j < kTinyRPG; ++j) {
 #ifdef KGX_EXPERIMENTS
       const bool hit = a.debug & 16;
-      v[j][0] = *reinterpret_cast<const f4*>(gsrc<TWO>(a, hit ? 0 : r.p[j].z) + f);
-      if constexpr (NG == 2) v[j][1] = *reinterpret_cast<const f4*>(gsrc<TWO>(a, hit ? 0 : r.p[j].w) + f);
+      v[j][0] = *reinterpret_cast<const f4*>(gsrc<TWO>(a, hit ? 0 : r.p[j].z) + fg);
+      if constexpr (NG == 2) v[j][1] = *reinterpret_cast<const f4*>(gsrc<TWO>(a, hit ? 0 : r.p[j].w) + fg);
 #else
-      v[j][0] = *reinterpret_cast<const f4*>(gsrc<TWO>(a, r.p[j].z) + f);
-      if constexpr (NG == 2) v[j][1] = *reinterpret_cast<const f4*>(gsrc<TWO>(a, r.p[j].w) + f);
+      v[j][0] = *reinterpret_cast<const f4*>(gsrc<TWO>(a, r.p[j].z) + fg);
+      if constexpr (NG == 2) v[j][1] = *reinterpret_cast<const f4*>(gsrc<TWO>(a, r.p[j].w) + fg);
 #endif
     }
   };
@@ -931,11 +950,15 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
       if constexpr (EXTRA) {
         if (row >= 0 && a.pre_gin) {
           float xv[4];
-          vload<4>(xv, a.x + int64_t(row) * a.ld_x + f);
+          vload<4>(xv, a.x + int64_t(row) * a.ld_x + fg);
 #pragma unroll
           for (int k = 0; k < 4; ++k) o[k] = __fadd_rn(__fmul_rn(a.gin_scale, xv[k]), o[k]);
         }
-        if (row >= 0 && a.agg_out) vstore<4>(a.agg_out + int64_t(row) * a.ld_agg + f, o);
+        if (row >= 0 && a.agg_out && f_ok) vstore<4>(a.agg_out + int64_t(row) * a.ld_agg + f, o);
+      }
+      if (a.F_in < kFin) {  // wave-uniform: lanes past F_in put zeros in the planes
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = f_ok ? o[k] : 0.0f;
       }
       bf16x4_t ph, pm, pl;
 #pragma unroll
@@ -1030,19 +1053,19 @@ __global__ __launch_bounds__(256) void spmm_gemm_fixup_kernel(FusedArgs a) {
       for (int k = 0; k < 4; ++k) acc[k] = R::finish(acc[k], s.w);
       if (a.pre_gin) {
         float xv[4];
-        vload<4>(xv, a.x + int64_t(row) * a.ld_x + lane * 4);
+        vload<4>(xv, a.x + int64_t(row) * a.ld_x + (lane * 4 < a.F_in ? lane * 4 : 0));
 #pragma unroll
         for (int k = 0; k < 4; ++k) acc[k] = __fadd_rn(__fmul_rn(a.gin_scale, xv[k]), acc[k]);
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) vrow[g][lane * 4 + k] = acc[k];
-      if (a.agg_out) vstore<4>(a.agg_out + int64_t(row) * a.ld_agg + lane * 4, acc);
+      if (a.agg_out && lane * 4 < a.F_in) vstore<4>(a.agg_out + int64_t(row) * a.ld_agg + lane * 4, acc);
     }
     __syncthreads();
     if (row >= 0) {
       for (int c = lane; c < a.F_out; c += 32) {
         float s = 0.0f;
-        for (int k = 0; k < kFin; ++k) s = fmaf(vrow[g][k], a.W[int64_t(k) * a.F_out + c], s);
+        for (int k = 0; k < a.F_in; ++k) s = fmaf(vrow[g][k], a.W[int64_t(k) * a.F_out + c], s);
         float v = s + (a.bias ? a.bias[c] : 0.0f);
         if (a.accumulate) v = __fadd_rn(a.out[int64_t(row) * a.ld_o + c], v);
         if (a.relu) v = fmaxf(v, 0.0f);
@@ -1180,20 +1203,19 @@ extern "C" int kgx_spmm_gemm_ex3(int reduce, const int32_t* rowptr, const int32_
   KGX_REQUIRE(!tiny_pack || (n_tiny_deg2 >= 0 && n_tiny_deg2 <= n_items - n_short_end), KGX_ERR_ARG,
               "kgx_spmm_gemm: n_tiny_deg2 must lie in [0, n_items - n_short_end]");
   KGX_REQUIRE(reduce >= KGX_SUM && reduce <= KGX_MIN, KGX_ERR_ARG, "kgx_spmm_gemm: reduce %d unsupported", reduce);
-  KGX_REQUIRE(F_in == kFin, KGX_ERR_UNSUPPORTED, "kgx_spmm_gemm: F_in must be %d (got %lld)", kFin,
-              (long long)F_in);
-  KGX_REQUIRE(F_out > 0 && F_out <= 128 && F_out % 16 == 0, KGX_ERR_UNSUPPORTED,
-              "kgx_spmm_gemm: F_out must be a multiple of 16 <= 128 (got %lld)", (long long)F_out);
+  KGX_REQUIRE(F_in > 0 && F_in <= kFin && F_in % 4 == 0, KGX_ERR_UNSUPPORTED,
+              "kgx_spmm_gemm: F_in must be a multiple of 4 <= %d (got %lld)", kFin, (long long)F_in);
+  KGX_REQUIRE(F_out > 0 && F_out <= 128 && F_out % 4 == 0, KGX_ERR_UNSUPPORTED,
+              "kgx_spmm_gemm: F_out must be a multiple of 4 <= 128 (got %lld)", (long long)F_out);
   KGX_REQUIRE(n_rows >= 0 && n_items >= 0 && n_split >= 0, KGX_ERR_ARG, "kgx_spmm_gemm: negative size");
   KGX_REQUIRE((flags & ~(KGX_FUSED_PRE_GIN | KGX_FUSED_ACCUMULATE | KGX_FUSED_SHARE_GPU | KGX_FUSED_RELU)) == 0,
               KGX_ERR_ARG, "kgx_spmm_gemm: unknown flags 0x%x", flags);
-  KGX_REQUIRE(!((flags & KGX_FUSED_RELU) && (flags & KGX_FUSED_ACCUMULATE)), KGX_ERR_ARG,
-              "kgx_spmm_gemm: KGX_FUSED_RELU cannot be combined with KGX_FUSED_ACCUMULATE");
   KGX_REQUIRE(!agg_out || (ld_agg >= F_in && reinterpret_cast<uintptr_t>(agg_out) % 16 == 0 && ld_agg % 4 == 0),
               KGX_ERR_ARG, "kgx_spmm_gemm: agg_out must be 16-byte aligned with ld >= F_in, ld %% 4 == 0");
   if (n_rows == 0) return KGX_OK;
   KGX_REQUIRE(rowptr && rows && idx && x && W && out, KGX_ERR_ARG, "kgx_spmm_gemm: null pointer");
-  KGX_REQUIRE(ld_x < (int64_t(1) << 31), KGX_ERR_ARG, "kgx_spmm_gemm: x leading dimension >= 2^31");
+  KGX_REQUIRE(ld_x >= F_in && ld_x < (int64_t(1) << 31), KGX_ERR_ARG,
+              "kgx_spmm_gemm: x leading dimension must lie in [F_in, 2^31)");
   KGX_REQUIRE(ld_x % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0 && ld_out >= F_out, KGX_ERR_ARG,
               "kgx_spmm_gemm: x must be 16-byte aligned with ld %% 4 == 0");
   KGX_REQUIRE(ld_out % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0, KGX_ERR_ARG,
@@ -1224,6 +1246,7 @@ extern "C" int kgx_spmm_gemm_ex3(int reduce, const int32_t* rowptr, const int32_
                                                uintptr_t(n_x1) * uintptr_t(ld_x) * sizeof(float))
              : x;
   a.W = W;
+  a.F_in = int(F_in);
   a.F_out = int(F_out);
   a.bias = bias;
   a.out = out;

@@ -147,8 +147,40 @@ class SAGEConv(MessagePassing):
         edge_index = inputs[1]
         ei = edge_index_tensor(edge_index, x.device, allow_transpose=True)
         num_nodes = x.shape[0]
+        out = self._call_fused(x, ei, edge_index, training)
+        if out is not None:
+            return out
         aggregated = self.aggregate_neighbors(x, ei, num_nodes, training=training, edge_index_obj=edge_index)
         return self.update_nodes(x, aggregated)
+
+    def _call_fused(self, x, ei, edge_index_obj, training):
+        """Inference with root_weight and a mean / sum / max aggregator: the
+        neighbour map fused into the aggregation (sage_conv.py:404-433 in two
+        launches): out = b + x W_self (kgx_dense), then kgx_spmm_gemm gathers,
+        reduces, multiplies by W_neigh and adds into out in its store (relu
+        there too), so the [N, F_in] aggregate is never written or re-read.
+        Same terms as the reference, summed as (b + x W_self) + aggr W_neigh
+        instead of (x W_self + aggr W_neigh) + b (tolerance-checked).  None
+        when the shapes or the mode need the two-step path."""
+        use_b = self.use_bias and self.bias is not None
+        if (not self.root_weight or self.lin_self is None or self.exact or not x.is_cuda
+                or self.actual_aggregator not in ("mean", "sum", "max") or ei.shape[1] == 0
+                or (training and self.dropout_rate > 0)
+                or not kops.fused_sage_supported(x.shape[1], self.output_dim)):
+            return None
+        W_self, W_neigh = self.lin_self.kernel, self.lin_neigh.kernel
+        b = self.bias if use_b else None
+        if kops._needs_grad(x, W_self, W_neigh, b):
+            return None
+        g = graph_for(edge_index_obj, ei, x.shape[0], x.shape[0], n_features=x.shape[1])
+        relu = self.activation is torch.relu
+        out = kops.dense(x, W_self, b)
+        kops.aggregate_transform(g, x.contiguous(), W_neigh, self.actual_aggregator, out=out, relu=relu)
+        if self.activation is not None and not relu:
+            out = self.activation(out)
+        if self.normalize:
+            out = l2_normalize(out)
+        return out
 
     def update_nodes(self, x, aggregated):
         """lin_neigh(aggr) + lin_self(x) + bias, activation, L2 norm (sage_conv.py:409-439);

@@ -230,6 +230,11 @@ def _f256_call(reduce, rowptr, rows, n_dst, items, n_items, split, n_split, idx,
     )
 
 
+def _partial_width(x: torch.Tensor) -> int:
+    """Floats per hub-chunk partial: the 256-wide kernels 256, kgx_spmm_gemm 128 (any F_in <= 128)."""
+    return F256 if x.shape[1] == F256 else 128
+
+
 def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, bias, pre_gin, gin_scale, save_agg,
                     relu=False, n_long=-1, tpack=None, tw=None, n_short_end=-1, n_tiny2=0, x2=None):
     x, w, W, bias, x2 = _f32c(x), _f32c(w), _f32c(W), _f32c(bias), _f32c(x2)
@@ -244,7 +249,7 @@ def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, b
     n_split = 0 if split is None else split.shape[0]
     partials = None
     if items is not None and n_split > 0:
-        partials = torch.empty((n_slots, x.shape[1]), dtype=torch.float32, device=dev)
+        partials = torch.empty((n_slots, _partial_width(x)), dtype=torch.float32, device=dev)
     flags = int(pre_gin) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0) | (nat.FUSED_RELU if relu else 0)
     if x.shape[1] == F256:
         _f256_call(reduce, rowptr, rows, n_dst, items, n_items, split, n_split, idx, w, x, x2, W, bias, flags,
@@ -375,7 +380,7 @@ def spmm_gemm_acc_(
     n_split = 0 if split is None else split.shape[0]
     partials = None
     if items is not None and n_split > 0:
-        partials = torch.empty((n_slots, x.shape[1]), dtype=torch.float32, device=dev)
+        partials = torch.empty((n_slots, _partial_width(x)), dtype=torch.float32, device=dev)
     if x.shape[1] == F256:
         _f256_call(reduce, rowptr, rows, n_dst, items, n_items, split, n_split, idx, w, x, x2, W, bias,
                    (nat.FUSED_ACCUMULATE if accumulate else 0) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0) | flags,
@@ -415,6 +420,20 @@ def fused_transform_supported(f_in: int, f_out: int, two_table: bool = False) ->
     if f_in == F256:
         return f_out == F256 and os.environ.get("KGX_FUSED256", _F256_DEFAULT) not in ("0", "false", "False")
     return f_in == 128 and f_out % 16 == 0 and 0 < f_out <= 128 and f_in <= f_out
+
+
+def fused_sage_supported(f_in: int, f_out: int) -> bool:
+    """SAGEConv's update through kgx_spmm_gemm (any F_in, F_out <= 128, multiples
+    of 4): out = x W_self + b by kgx_dense, then out = relu?(out + REDUCE(x) W_neigh)
+    in the fused aggregation's store, so the [N, F_in] aggregate is never
+    written (C5: 2.45M x 100).  KGX_FUSED_SAGE=0 / KGX_FUSED=0 turn it off."""
+    import os
+
+    if os.environ.get("KGX_FUSED", "1") in ("0", "false", "False"):
+        return False
+    if os.environ.get("KGX_FUSED_SAGE", "1") in ("0", "false", "False"):
+        return False
+    return 0 < f_in <= 128 and f_in % 4 == 0 and 0 < f_out <= 128 and f_out % 4 == 0
 
 
 def _gatv2_impl(h_src, h_dst, rowptr, rows, items, split, col, att, heads, channels, negative_slope, bias,
@@ -834,10 +853,11 @@ def aggregate_transform(
     if x2 is not None and _needs_grad(x, x2, W, bias):
         raise NotImplementedError("aggregate_transform(x2=...) is a forward-only (no_grad) path")
     if out is not None:  # accumulate into `out` (sum only: the caller splits a row's edges)
-        if red != nat.SUM:
-            raise ValueError("aggregate_transform(out=...) accumulates plain sums only")
-        if (pre_gin or relu) and accumulate:
-            raise ValueError("aggregate_transform(out=...): pre_gin / relu only with accumulate=False (overwrite)")
+        if red != nat.SUM and (x2 is not None or x.shape[1] == F256):
+            raise ValueError("aggregate_transform(out=...): two-table and 256-wide passes accumulate plain sums only")
+        if accumulate and (pre_gin or (relu and x.shape[1] == F256)):
+            raise ValueError("aggregate_transform(out=...): pre_gin (and relu at F_in 256) only with "
+                             "accumulate=False (overwrite)")
         if _needs_grad(x, W, bias, out):
             raise NotImplementedError("aggregate_transform(out=...) is a forward-only (no_grad) path")
         items, _, split, _, n_slots = g.work(exact)
