@@ -50,10 +50,25 @@ class LoopbackComm(kd.TorchComm):
     ready, and occupies it for bytes / link_gbps (a spin of one wave, so the
     modelled transfer takes time but no HBM bandwidth) before its copy lands."""
 
-    def __init__(self, world: int, n_local: int, link_gbps: float = 0.0, cycles_per_ms: float = 0.0):
+    def __init__(self, world: int, n_local: int, link_gbps: float = 0.0, cycles_per_ms: float = 0.0,
+                 free_exchange: bool = False):
         self.w, self.n_local = world, n_local
         self.link_gbps, self.cycles_per_ms = link_gbps, cycles_per_ms
         self.link = None
+        # free_exchange: after a buffer's first landing (real values), later exchanges into it
+        # move nothing -- the step is the rank's compute alone; otherwise the loopback copy
+        # (a local read + write of every received byte) stands in for RCCL's receive writes
+        self.free_exchange, self._landed = free_exchange, set()
+
+    def _land(self, out) -> bool:
+        """True when this exchange should copy (always, unless free_exchange and out has landed once)."""
+        if not self.free_exchange:
+            return True
+        key = (out.data_ptr(), out.numel())
+        if key in self._landed:
+            return False
+        self._landed.add(key)
+        return True
 
     def rank(self):
         return 0
@@ -73,7 +88,8 @@ class LoopbackComm(kd.TorchComm):
         """Asynchronous like RCCL's: the copy is queued on the current (side)
         stream and wait() makes the then-current stream wait for it."""
         if self.link_gbps <= 0:
-            self.all_to_all_single(out, inp, out_splits, in_splits)
+            if self._land(out):
+                self.all_to_all_single(out, inp, out_splits, in_splits)
             ev = torch.cuda.Event()
             ev.record()
             return _EventWork(ev)
@@ -103,7 +119,8 @@ class LoopbackComm(kd.TorchComm):
     def all_gather_start(self, out, inp):
         """As all_to_all_start: the modelled link time covers the (world-1)/world received share."""
         if self.link_gbps <= 0:
-            self.all_gather(out, inp)
+            if self._land(out):
+                self.all_gather(out, inp)
             ev = torch.cuda.Event()
             ev.record()
             return _EventWork(ev)
@@ -150,7 +167,10 @@ def main():
     ap.add_argument("--nodes", type=int, default=None)
     ap.add_argument("--edges", type=int, default=None)
     ap.add_argument("--link-gbps", type=float, default=0.0,
-                    help="model the exchange: per-GPU receive rate in GB/s (0: the exchange is free)")
+                    help="model the exchange: per-GPU receive rate in GB/s (0: no link time)")
+    ap.add_argument("--free-exchange", action="store_true",
+                    help="with --link-gbps 0: received buffers land once, later exchanges move nothing "
+                         "(the rank's compute alone; default: a loopback device copy per exchange)")
     args = ap.parse_args()
     layer_kind, n_cfg, e_cfg, F, scaling = CONFIGS[args.config]
     n_cfg = args.nodes or n_cfg
@@ -180,7 +200,8 @@ def main():
         os.environ["KGX_HALO_MERGE"] = unit
         os.environ["KGX_HALO_A_LATE"] = a_late
         n_local = kd.equal_bounds(n_glob, P)[1]
-        comm = LoopbackComm(P, n_local, args.link_gbps, cycles_per_ms)
+        comm = LoopbackComm(P, n_local, args.link_gbps, cycles_per_ms,
+                            free_exchange=args.free_exchange and args.link_gbps <= 0)
         gcn = layer_kind == "gcn"
         sg = kd.ShardedGraph.rmat(n_glob, e_glob, seed=0, device=dev, comm=comm, self_loops=gcn, gcn_norm=gcn,
                                   halo_chunks=K, n_features=F)
@@ -221,7 +242,9 @@ def main():
                 "features": F, "world": P, "exchange": pp.kind if pp else "pull", "chunks": K,
                 "push_pull": pp is not None and pp.kind == "halo", "merged": merged == "1", "merge_unit": unit,
                 "a_late": a_late == "1", "share_den": int(den),
-                "link_gbps": args.link_gbps, "step_ms": round(t0.elapsed_time(t1) / args.steps, 3),
+                "link_gbps": args.link_gbps,
+                "exchange_model": "free" if comm.free_exchange else "loopback-copy" if args.link_gbps <= 0
+                else "modelled-link", "step_ms": round(t0.elapsed_time(t1) / args.steps, 3),
                 "launch_ms": [round(v, 3) for v in launch_ms],
                 "own_edges": g_own.kept, "chunk_edges": [g.kept for g in g_chunks],
                 "halo_rows_pull_only": sg.n_halo, "halo_rows": pp.n_rows if pp else sg.n_halo,
