@@ -765,6 +765,10 @@ constexpr int kTinyGroups = 16;  // producer row groups
 #ifndef KGX_TINY_TSTORE
 #define KGX_TINY_TSTORE 1
 #endif
+// accumulate mode: load the output rows before the MFMAs (experiment, 0 = after)
+#ifndef KGX_TINY_ACC_EARLY
+#define KGX_TINY_ACC_EARLY 0
+#endif
 template <int NG>
 constexpr int tiny_rows() { return kTinyGroups * (NG == 1 ? KGX_TINY_RPG1 : KGX_TINY_RPG); }
 
@@ -823,6 +827,19 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
         f32x4 d[kTinyRPG];
 #pragma unroll
         for (int rb = 0; rb < kTinyRPG; ++rb) d[rb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#if KGX_TINY_TSTORE && KGX_TINY_ACC_EARLY
+        // accumulate mode: the rows added to are loaded before the MFMAs, so their
+        // latency runs under the matrix work instead of after it
+        float4 pacc[kTinyRPG];
+        if (a.accumulate) {
+#pragma unroll
+          for (int rb = 0; rb < kTinyRPG; ++rb) {
+            const int rr = trow[b][16 * rb + m];
+            pacc[rb] = rr >= 0 && c4 < a.F_out ? *reinterpret_cast<const float4*>(a.out + int64_t(rr) * a.ld_o + c4)
+                                               : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+          }
+        }
+#endif
 #ifdef KGX_EXPERIMENTS  // cost decomposition (KGX_FUSED_DEBUG 4: no MFMAs, 8: no stores, 16: gathers all hit row 0)
         if (!(a.debug & 4))
 #endif
@@ -868,7 +885,11 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
             const float4 b4 = *reinterpret_cast<const float4*>(&sbias[c4]);
             float4 v = make_float4(d[rb][0] + b4.x, d[rb][1] + b4.y, d[rb][2] + b4.z, d[rb][3] + b4.w);
             if (a.accumulate) {
+#if KGX_TINY_ACC_EARLY
+              const float4 p = pacc[rb];
+#else
               const float4 p = *dst;
+#endif
               v = make_float4(__fadd_rn(p.x, v.x), __fadd_rn(p.y, v.y), __fadd_rn(p.z, v.z), __fadd_rn(p.w, v.w));
             }
             if (a.relu) v = make_float4(fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f));
