@@ -405,8 +405,8 @@ def test_fused_accumulate_own_halo_split(dev, split_len):
     np.add.at(aggr, rows, x[csr.col.cpu().numpy()].astype(np.float64) * csr.w.cpu().numpy()[:, None])
     assert_dot_bound(out.cpu().numpy(), aggr, W.astype(np.float64), b.astype(np.float64), k_eps=2e-5)
     assert_dot_bound(one, aggr, W.astype(np.float64), b.astype(np.float64), k_eps=2e-5)
-    with pytest.raises(ValueError):
-        kops.aggregate_transform(g_oth, xd[n_own:].contiguous(), Wd, "max", out=out)
+    with pytest.raises(ValueError):  # two-table passes accumulate plain sums only
+        kops.aggregate_transform(g_oth, xd[n_own:].contiguous(), Wd, "max", out=out, x2=xd)
 
 
 def test_split_by_source_ranges_accumulate_parts(dev):
