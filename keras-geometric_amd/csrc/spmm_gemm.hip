@@ -164,9 +164,16 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
 #ifdef KGX_FUSED_U
   constexpr int U = KGX_FUSED_U;
 #else
-  constexpr int U = 4;  // gathers in flight per group (measured: 4 beats 6 and 8 here)
+  // gathers in flight per group: weighted (GCN, NS) 4 beat 6 and 8 (each cost
+  // occupancy); unweighted rows (SAGE at C5: 50 edges per row on average) take
+  // 6 in the same 124 VGPRs, the W fragments' registers staying put
+  constexpr int U = WEIGHTED ? 4 : 6;
 #endif
-  constexpr int PF = U;  // rows prefetched per group for the next tile
+#ifdef KGX_FUSED_PF
+  constexpr int PF = KGX_FUSED_PF;
+#else
+  constexpr int PF = 4;  // rows prefetched per group for the next tile (live across the MFMA phase)
+#endif
 #if KGX_FUSED_BF16X3
   __shared__ short tile3[3][kGroups][kFin + 8];  // hi / mid / lo planes of the aggregated rows
 #else

@@ -42,7 +42,7 @@ def main():
     busy, gaps, end = 0, [], None
     per = defaultdict(float)
     for s, e, name in rows:
-        per[name.split("(")[0][-60:]] += (e - s) / 1e6
+        per[name.replace("(anonymous namespace)::", "").split("(")[0][-60:]] += (e - s) / 1e6
         if end is None or s >= end:
             if end is not None:
                 gaps.append((s - end) / 1e6)
