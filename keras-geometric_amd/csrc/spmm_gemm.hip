@@ -158,16 +158,17 @@ struct Red {
   }
 };
 
-template <int RED, bool WEIGHTED, bool TWO>
+// NARROW: F_in < 128 or F_out not a multiple of 16 (masks compiled in only there)
+template <int RED, bool WEIGHTED, bool TWO, bool NARROW>
 __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedArgs a) {  // TWO: hold 4 waves per SIMD
   using R = Red<RED>;
 #ifdef KGX_FUSED_U
   constexpr int U = KGX_FUSED_U;
 #else
-  // gathers in flight per group: weighted (GCN, NS) 4 beat 6 and 8 (each cost
-  // occupancy); unweighted rows (SAGE at C5: 50 edges per row on average) take
-  // 6 in the same 124 VGPRs, the W fragments' registers staying put
-  constexpr int U = WEIGHTED ? 4 : 6;
+  // gathers in flight per group: at F_in 128 (GCN, NS) 4 beat 6 and 8 (each cost
+  // occupancy); the narrow unweighted form (SAGE at C5: 50 edges per row on
+  // average) takes 6 in 124 VGPRs, occupancy kept (C5 main kernel 7.70 -> 7.37 ms)
+  constexpr int U = (NARROW && !WEIGHTED) ? 6 : 4;
 #endif
 #ifdef KGX_FUSED_PF
   constexpr int PF = KGX_FUSED_PF;
@@ -190,14 +191,14 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
   const int g = tid >> 5;     // row-group 0..15
   const int lane = tid & 31;  // lane in the group
   const int f = lane * 4;
-  const bool f_ok = f < a.F_in;  // lanes past F_in (F_in < 128) load column 0 again and carry zeros
+  const bool f_ok = !NARROW || f < a.F_in;  // lanes past F_in (F_in < 128) load column 0 again and carry zeros
   const int fg = f_ok ? f : 0;
   const int wave = tid >> 6;  // 0..7 -> output columns [16 wave, 16 wave + 16)
   const int wl = tid & 63;    // lane in the wave
   const int n_col = wave * 16 + (wl & 15);
   const int q = wl >> 4;
   const bool mfma_wave = wave * 16 < a.F_out;
-  const bool w_ok = mfma_wave && n_col < a.F_out;  // W rows k >= F_in and columns >= F_out load as 0
+  const bool w_ok = mfma_wave && (!NARROW || n_col < a.F_out);  // W rows k >= F_in and columns >= F_out load as 0
 
   // W fragment for this wave's 16 columns, K permuted: k = 32 q + s.
 #if KGX_FUSED_BF16X3
@@ -210,8 +211,8 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
     u32x4_t ph, pm, pl;
 #pragma unroll
     for (int j = 0; j < 8; j += 2) {
-      const float v0 = w_ok && 32 * q + 8 * s + j < a.F_in ? a.W[int64_t(32 * q + 8 * s + j) * a.F_out + n_col] : 0.0f;
-      const float v1 = w_ok && 32 * q + 8 * s + j + 1 < a.F_in ? a.W[int64_t(32 * q + 8 * s + j + 1) * a.F_out + n_col] : 0.0f;
+      const float v0 = w_ok && (!NARROW || 32 * q + 8 * s + j < a.F_in) ? a.W[int64_t(32 * q + 8 * s + j) * a.F_out + n_col] : 0.0f;
+      const float v1 = w_ok && (!NARROW || 32 * q + 8 * s + j + 1 < a.F_in) ? a.W[int64_t(32 * q + 8 * s + j + 1) * a.F_out + n_col] : 0.0f;
       uint32_t h, m_, l;
       split3_pair(v0, v1, h, m_, l);
       ph[j / 2] = h;
@@ -225,7 +226,7 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
 #else
   float wb[32];
 #pragma unroll
-  for (int s = 0; s < 32; ++s) wb[s] = w_ok && 32 * q + s < a.F_in ? a.W[int64_t(32 * q + s) * a.F_out + n_col] : 0.0f;
+  for (int s = 0; s < 32; ++s) wb[s] = w_ok && (!NARROW || 32 * q + s < a.F_in) ? a.W[int64_t(32 * q + s) * a.F_out + n_col] : 0.0f;
 #endif
 #if KGX_FUSED_TSTORE && KGX_FUSED_BF16X3
   const int c4 = wave * 16 + 4 * q;
@@ -346,7 +347,7 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
       for (int k = 0; k < 4; ++k) r[k] = __fadd_rn(__fmul_rn(a.gin_scale, xv[k]), r[k]);
     }
     if (full_row && a.agg_out && f_ok) vstore<4>(a.agg_out + int64_t(row) * a.ld_agg + f, r);
-    if (a.F_in < kFin) {  // wave-uniform: lanes past F_in put zeros in the planes
+    if (NARROW && a.F_in < kFin) {  // wave-uniform: lanes past F_in put zeros in the planes
 #pragma unroll
       for (int k = 0; k < 4; ++k) r[k] = f_ok ? r[k] : 0.0f;
     }
@@ -427,7 +428,7 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
 #if KGX_FUSED_TSTORE && KGX_FUSED_BF16X3
       // straight from the accumulators: lane (m, q) writes columns 16 wave + 4 q .. + 3 of tile row m
       const int rr = tile_row[m];
-      if (rr >= 0 && c4 < a.F_out && !(a.debug & 2)) {
+      if (rr >= 0 && (!NARROW || c4 < a.F_out) && !(a.debug & 2)) {
         float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + c4);
         const float4 b4 = *reinterpret_cast<const float4*>(&sbias[c4]);
         float4 v = make_float4((d0[0] + d1[0]) + b4.x, (d0[1] + d1[1]) + b4.y, (d0[2] + d1[2]) + b4.z,
@@ -490,7 +491,7 @@ constexpr int kRPG = KGX_SHORT_RPG;        // rows per group per tile
 constexpr int kSPF = KGX_SHORT_PF;         // edges per row gathered up front (all rows together)
 constexpr int kShortRows = kGroups * kRPG;
 
-template <int RED, bool WEIGHTED, bool TWO>
+template <int RED, bool WEIGHTED, bool TWO, bool NARROW>
 __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs a) {  // 4 waves per SIMD: two blocks per CU
   using R = Red<RED>;
   // split planes of the 64 aggregated rows; after the MFMAs the same bytes hold the f32 results
@@ -507,14 +508,14 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
   const int g = tid >> 5;
   const int lane = tid & 31;
   const int f = lane * 4;
-  const bool f_ok = f < a.F_in;  // lanes past F_in (F_in < 128) load column 0 again and carry zeros
+  const bool f_ok = !NARROW || f < a.F_in;  // lanes past F_in (F_in < 128) load column 0 again and carry zeros
   const int fg = f_ok ? f : 0;
   const int wave = tid >> 6;
   const int wl = tid & 63;
   const int n_col = wave * 16 + (wl & 15);
   const int q = wl >> 4;
   const bool mfma_wave = wave * 16 < a.F_out;
-  const bool w_ok = mfma_wave && n_col < a.F_out;  // W rows k >= F_in and columns >= F_out load as 0
+  const bool w_ok = mfma_wave && (!NARROW || n_col < a.F_out);  // W rows k >= F_in and columns >= F_out load as 0
 
   bf16x8_t wfh[4], wfm[4], wfl[4];
 #pragma unroll
@@ -523,8 +524,8 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
     u32x4_t ph, pm, pl;
 #pragma unroll
     for (int j = 0; j < 8; j += 2) {
-      const float v0 = w_ok && 32 * q + 8 * s + j < a.F_in ? a.W[int64_t(32 * q + 8 * s + j) * a.F_out + n_col] : 0.0f;
-      const float v1 = w_ok && 32 * q + 8 * s + j + 1 < a.F_in ? a.W[int64_t(32 * q + 8 * s + j + 1) * a.F_out + n_col] : 0.0f;
+      const float v0 = w_ok && (!NARROW || 32 * q + 8 * s + j < a.F_in) ? a.W[int64_t(32 * q + 8 * s + j) * a.F_out + n_col] : 0.0f;
+      const float v1 = w_ok && (!NARROW || 32 * q + 8 * s + j + 1 < a.F_in) ? a.W[int64_t(32 * q + 8 * s + j + 1) * a.F_out + n_col] : 0.0f;
       uint32_t h, m_, l;
       split3_pair(v0, v1, h, m_, l);
       ph[j / 2] = h;
@@ -630,7 +631,7 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
         for (int k = 0; k < 4; ++k) v[k] = __fadd_rn(__fmul_rn(a.gin_scale, xv[k]), v[k]);
       }
       if (ok && a.agg_out && f_ok) vstore<4>(a.agg_out + int64_t(row[r]) * a.ld_agg + f, v);
-      if (a.F_in < kFin) {  // wave-uniform: lanes past F_in put zeros in the planes
+      if (NARROW && a.F_in < kFin) {  // wave-uniform: lanes past F_in put zeros in the planes
 #pragma unroll
         for (int k = 0; k < 4; ++k) v[k] = f_ok ? v[k] : 0.0f;
       }
@@ -699,7 +700,7 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
 #pragma unroll
       for (int rb = 0; rb < kRPG; ++rb) {
         const int rr = tile_row[16 * rb + m];
-        if (rr >= 0 && c4 < a.F_out) {
+        if (rr >= 0 && (!NARROW || c4 < a.F_out)) {
           float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + c4);
           const float4 b4 = *reinterpret_cast<const float4*>(&sbias[c4]);
           float4 v = make_float4(d[rb][0] + b4.x, d[rb][1] + b4.y, d[rb][2] + b4.z, d[rb][3] + b4.w);
@@ -781,7 +782,7 @@ constexpr int tiny_rows() { return kTinyGroups * (NG == 1 ? KGX_TINY_RPG1 : KGX_
 
 // NG: edges gathered per row (2 for the degree-2 head of the tail, 1 for the
 // degree <= 1 rest: the schedule is degree-descending, so each is a range).
-template <int RED, bool WEIGHTED, bool EXTRA, int NG, bool TWO>  // EXTRA: pre_gin or agg_out (loads / stores under a row mask)
+template <int RED, bool WEIGHTED, bool EXTRA, int NG, bool TWO, bool NARROW>  // EXTRA: pre_gin or agg_out (loads / stores under a row mask)
 __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedArgs a) {
   using R = Red<RED>;
   constexpr int kTinyRPG = NG == 1 ? KGX_TINY_RPG1 : KGX_TINY_RPG;  // rows per group per tile
@@ -803,7 +804,7 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
     const int q = wl >> 4, m = wl & 15;
     const int n_col = wave * 16 + m;
     const bool mfma_wave = wave * 16 < a.F_out;
-    const bool w_ok = mfma_wave && n_col < a.F_out;
+    const bool w_ok = mfma_wave && (!NARROW || n_col < a.F_out);
     bf16x8_t wfh[4], wfm[4], wfl[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -811,8 +812,8 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
       u32x4_t ph, pm, pl;
 #pragma unroll
       for (int j = 0; j < 8; j += 2) {
-        const float v0 = w_ok && 32 * q + 8 * s + j < a.F_in ? a.W[int64_t(32 * q + 8 * s + j) * a.F_out + n_col] : 0.0f;
-        const float v1 = w_ok && 32 * q + 8 * s + j + 1 < a.F_in ? a.W[int64_t(32 * q + 8 * s + j + 1) * a.F_out + n_col] : 0.0f;
+        const float v0 = w_ok && (!NARROW || 32 * q + 8 * s + j < a.F_in) ? a.W[int64_t(32 * q + 8 * s + j) * a.F_out + n_col] : 0.0f;
+        const float v1 = w_ok && (!NARROW || 32 * q + 8 * s + j + 1 < a.F_in) ? a.W[int64_t(32 * q + 8 * s + j + 1) * a.F_out + n_col] : 0.0f;
         uint32_t h, m_, l;
         split3_pair(v0, v1, h, m_, l);
         ph[j / 2] = h;
@@ -842,7 +843,7 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
 #pragma unroll
           for (int rb = 0; rb < kTinyRPG; ++rb) {
             const int rr = trow[b][16 * rb + m];
-            pacc[rb] = rr >= 0 && c4 < a.F_out ? *reinterpret_cast<const float4*>(a.out + int64_t(rr) * a.ld_o + c4)
+            pacc[rb] = rr >= 0 && (!NARROW || c4 < a.F_out) ? *reinterpret_cast<const float4*>(a.out + int64_t(rr) * a.ld_o + c4)
                                                : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
           }
         }
@@ -887,7 +888,7 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
 #pragma unroll
         for (int rb = 0; rb < kTinyRPG; ++rb) {
           const int rr = trow[b][16 * rb + m];
-          if (rr >= 0 && c4 < a.F_out) {
+          if (rr >= 0 && (!NARROW || c4 < a.F_out)) {
             float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + c4);
             const float4 b4 = *reinterpret_cast<const float4*>(&sbias[c4]);
             float4 v = make_float4(d[rb][0] + b4.x, d[rb][1] + b4.y, d[rb][2] + b4.z, d[rb][3] + b4.w);
@@ -909,7 +910,7 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int rr = trow[b][16 * rb + 4 * q + j];
-            if (rr >= 0 && n_col < a.F_out) {
+            if (rr >= 0 && (!NARROW || n_col < a.F_out)) {
               float* dst = a.out + int64_t(rr) * a.ld_o + n_col;
               float v = d[rb][j] + bcol;
               if (a.accumulate) v = __fadd_rn(*dst, v);
@@ -927,7 +928,7 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
   // ---- producers: tile i at iteration i
   const int pt = tid - 512;
   const int g = pt >> 5, lane = pt & 31, f = lane * 4;
-  const bool f_ok = f < a.F_in;  // lanes past F_in (F_in < 128) load column 0 again and carry zeros
+  const bool f_ok = !NARROW || f < a.F_in;  // lanes past F_in (F_in < 128) load column 0 again and carry zeros
   const int fg = f_ok ? f : 0;
   struct Rec {
     int4 p[kTinyRPG];
@@ -984,7 +985,7 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
         }
         if (row >= 0 && a.agg_out && f_ok) vstore<4>(a.agg_out + int64_t(row) * a.ld_agg + f, o);
       }
-      if (a.F_in < kFin) {  // wave-uniform: lanes past F_in put zeros in the planes
+      if (NARROW && a.F_in < kFin) {  // wave-uniform: lanes past F_in put zeros in the planes
 #pragma unroll
         for (int k = 0; k < 4; ++k) o[k] = f_ok ? o[k] : 0.0f;
       }
@@ -1053,7 +1054,7 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
 }
 
 // Split rows: combine chunk partials in order, finish, then out = v @ W + b (VALU).
-template <int RED>
+template <int RED, bool NARROW>
 __global__ __launch_bounds__(256) void spmm_gemm_fixup_kernel(FusedArgs a) {
   using R = Red<RED>;
   __shared__ float vrow[8][kFin];
@@ -1081,19 +1082,19 @@ __global__ __launch_bounds__(256) void spmm_gemm_fixup_kernel(FusedArgs a) {
       for (int k = 0; k < 4; ++k) acc[k] = R::finish(acc[k], s.w);
       if (a.pre_gin) {
         float xv[4];
-        vload<4>(xv, a.x + int64_t(row) * a.ld_x + (lane * 4 < a.F_in ? lane * 4 : 0));
+        vload<4>(xv, a.x + int64_t(row) * a.ld_x + (!NARROW || lane * 4 < a.F_in ? lane * 4 : 0));
 #pragma unroll
         for (int k = 0; k < 4; ++k) acc[k] = __fadd_rn(__fmul_rn(a.gin_scale, xv[k]), acc[k]);
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) vrow[g][lane * 4 + k] = acc[k];
-      if (a.agg_out && lane * 4 < a.F_in) vstore<4>(a.agg_out + int64_t(row) * a.ld_agg + lane * 4, acc);
+      if (a.agg_out && (!NARROW || lane * 4 < a.F_in)) vstore<4>(a.agg_out + int64_t(row) * a.ld_agg + lane * 4, acc);
     }
     __syncthreads();
     if (row >= 0) {
       for (int c = lane; c < a.F_out; c += 32) {
         float s = 0.0f;
-        for (int k = 0; k < a.F_in; ++k) s = fmaf(vrow[g][k], a.W[int64_t(k) * a.F_out + c], s);
+        for (int k = 0; k < (NARROW ? a.F_in : kFin); ++k) s = fmaf(vrow[g][k], a.W[int64_t(k) * a.F_out + c], s);
         float v = s + (a.bias ? a.bias[c] : 0.0f);
         if (a.accumulate) v = __fadd_rn(a.out[int64_t(row) * a.ld_o + c], v);
         if (a.relu) v = fmaxf(v, 0.0f);
@@ -1104,7 +1105,7 @@ __global__ __launch_bounds__(256) void spmm_gemm_fixup_kernel(FusedArgs a) {
   }
 }
 
-template <int RED, bool W, bool TWO = false>
+template <int RED, bool W, bool TWO = false, bool NARROW = false>
 int launch(const FusedArgs& a, hipStream_t s) {
   const int64_t work = a.items ? a.n_long : a.n_rows;
   if (work > 0) {
@@ -1116,7 +1117,7 @@ int launch(const FusedArgs& a, hipStream_t s) {
         cus = 256;
     }
     int per_cu = 0;
-    auto k = spmm_gemm_kernel<RED, W, TWO>;
+    auto k = spmm_gemm_kernel<RED, W, TWO, NARROW>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, 0) != hipSuccess || per_cu <= 0)
       per_cu = 2;
     const int64_t need = (work + kGroups - 1) / kGroups;
@@ -1129,7 +1130,7 @@ int launch(const FusedArgs& a, hipStream_t s) {
   }
   if (a.items && a.n_long < a.n_short_end) {
     int per_cu = 0;
-    auto k = spmm_gemm_short_kernel<RED, W, TWO>;
+    auto k = spmm_gemm_short_kernel<RED, W, TWO, NARROW>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, 0) != hipSuccess || per_cu <= 0)
       per_cu = 2;
     static int cus2 = 0;
@@ -1152,8 +1153,10 @@ int launch(const FusedArgs& a, hipStream_t s) {
       b.tw = a.tw ? a.tw + (part ? a.n_tiny2 : 0) : nullptr;
       b.n_tiny = part ? a.n_tiny - a.n_tiny2 : a.n_tiny2;
       if (b.n_tiny <= 0) continue;
-      auto k = part ? (extra ? spmm_gemm_tiny_kernel<RED, W, true, 1, TWO> : spmm_gemm_tiny_kernel<RED, W, false, 1, TWO>)
-                    : (extra ? spmm_gemm_tiny_kernel<RED, W, true, 2, TWO> : spmm_gemm_tiny_kernel<RED, W, false, 2, TWO>);
+      auto k = part ? (extra ? spmm_gemm_tiny_kernel<RED, W, true, 1, TWO, NARROW>
+                             : spmm_gemm_tiny_kernel<RED, W, false, 1, TWO, NARROW>)
+                    : (extra ? spmm_gemm_tiny_kernel<RED, W, true, 2, TWO, NARROW>
+                             : spmm_gemm_tiny_kernel<RED, W, false, 2, TWO, NARROW>);
       const int rows = part ? tiny_rows<1>() : tiny_rows<2>();
       const int64_t need = (b.n_tiny + rows - 1) / rows;
       const int64_t cap = a.share_gpu ? shared_cap(int64_t(cu_count())) : int64_t(cu_count());
@@ -1163,8 +1166,8 @@ int launch(const FusedArgs& a, hipStream_t s) {
   }
   if (a.items && a.n_split > 0) {
     const int64_t blocks = (a.n_split + 7) / 8;
-    hipLaunchKernelGGL(spmm_gemm_fixup_kernel<RED>, dim3(unsigned(blocks < 4096 ? blocks : 4096)), dim3(256), 0,
-                       s, a);
+    auto fk = spmm_gemm_fixup_kernel<RED, NARROW>;
+    hipLaunchKernelGGL(fk, dim3(unsigned(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s, a);
     KGX_CHECK_LAUNCH();
   }
   return KGX_OK;
@@ -1220,8 +1223,10 @@ extern "C" int kgx_spmm_gemm_ex3(int reduce, const int32_t* rowptr, const int32_
   hipStream_t stream = as_stream(stream_);
   KGX_REQUIRE(!x2 || (n_x1 >= 0 && n_x1 < (int64_t(1) << 31) && reinterpret_cast<uintptr_t>(x2) % 16 == 0),
               KGX_ERR_ARG, "kgx_spmm_gemm: x2 must be 16-byte aligned and 0 <= n_x1 < 2^31");
-  KGX_REQUIRE(!x2 || (reduce == KGX_SUM && !(flags & KGX_FUSED_PRE_GIN)), KGX_ERR_UNSUPPORTED,
-              "kgx_spmm_gemm: two-table gathers are implemented for plain sums (the sharded GCN pass)");
+  KGX_REQUIRE(!x2 || (reduce == KGX_SUM && !(flags & KGX_FUSED_PRE_GIN) && F_in == kFin && F_out % 16 == 0),
+              KGX_ERR_UNSUPPORTED,
+              "kgx_spmm_gemm: two-table gathers are implemented for plain sums at F_in 128, F_out %% 16 == 0 "
+              "(the sharded GCN pass)");
   KGX_REQUIRE(!items || tiny_pack || n_short_end == n_items, KGX_ERR_ARG,
               "kgx_spmm_gemm: without tiny_pack, n_short_end must equal n_items");
   KGX_REQUIRE(!items || (n_long_items >= 0 && n_long_items <= n_short_end && n_short_end <= n_items), KGX_ERR_ARG,
@@ -1298,6 +1303,14 @@ extern "C" int kgx_spmm_gemm_ex3(int reduce, const int32_t* rowptr, const int32_
 #endif
   const bool wt = w != nullptr;
   if (x2) return wt ? launch<KGX_SUM, true, true>(a, stream) : launch<KGX_SUM, false, true>(a, stream);
+  if (F_in < kFin || F_out % 16 != 0) {  // the masked instantiations (SAGEConv at C5: 100 -> 100)
+    switch (reduce) {
+      case KGX_SUM: return wt ? launch<KGX_SUM, true, false, true>(a, stream) : launch<KGX_SUM, false, false, true>(a, stream);
+      case KGX_MEAN: return wt ? launch<KGX_MEAN, true, false, true>(a, stream) : launch<KGX_MEAN, false, false, true>(a, stream);
+      case KGX_MAX: return wt ? launch<KGX_MAX, true, false, true>(a, stream) : launch<KGX_MAX, false, false, true>(a, stream);
+      default: return wt ? launch<KGX_MIN, true, false, true>(a, stream) : launch<KGX_MIN, false, false, true>(a, stream);
+    }
+  }
   switch (reduce) {
     case KGX_SUM: return wt ? launch<KGX_SUM, true>(a, stream) : launch<KGX_SUM, false>(a, stream);
     case KGX_MEAN: return wt ? launch<KGX_MEAN, true>(a, stream) : launch<KGX_MEAN, false>(a, stream);
