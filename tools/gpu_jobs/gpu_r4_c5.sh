@@ -22,6 +22,6 @@ for r in 1 2; do
     > gpurun_out/r4c5/twostep_r$r.json 2>> gpurun_out/r4c5/bench.err || exit $?
 done
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4c5/prof -o run \
-  -- python3 bench.py --config c5 --steps 10 --warmup 2 $B > gpurun_out/r4c5/prof.log 2>&1
+  -- python3 bench.py --config c5 --steps 10 --warmup 2 $B > gpurun_out/r4c5/prof.log 2>&1 || exit $?
 KGX_FUSED_SAGE=0 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4c5/prof2 -o run \
   -- python3 bench.py --config c5 --steps 10 --warmup 2 $B > gpurun_out/r4c5/prof2.log 2>&1
