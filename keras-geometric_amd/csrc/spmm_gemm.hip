@@ -166,16 +166,16 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
   constexpr int U = KGX_FUSED_U;
 #else
   // gathers in flight per group: at F_in 128 (GCN, NS) 4 beat 6 and 8 with PF = U
-  // (each cost occupancy); the narrow unweighted form (SAGE at C5: 50 edges per
-  // row on average) takes 8 with a 2-row prefetch in 124 VGPRs, occupancy kept
-  // (C5 main kernel 7.70 ms at U = 4, 7.37-7.48 at U = 6 with PF = 4)
-  constexpr int U = (NARROW && !WEIGHTED) ? 8 : 4;
+  // (each cost occupancy) and U = 8 with PF = 2 (NS 8.90 -> 9.05-9.15 ms); the
+  // narrow unweighted form (SAGE at C5: 50 edges per row on average) takes 6 in
+  // 124 VGPRs, occupancy kept (C5 main kernel 7.70 ms at U = 4, 7.37-7.48 at
+  // U = 6, 7.77 at U = 8 with PF = 2)
+  constexpr int U = (NARROW && !WEIGHTED) ? 6 : 4;
 #endif
 #ifdef KGX_FUSED_PF
   constexpr int PF = KGX_FUSED_PF;
 #else
-  // rows prefetched per group for the next tile (live across the MFMA phase)
-  constexpr int PF = (NARROW && !WEIGHTED) ? 2 : 4;
+  constexpr int PF = 4;  // rows prefetched per group for the next tile (live across the MFMA phase)
 #endif
 #if KGX_FUSED_BF16X3
   __shared__ short tile3[3][kGroups][kFin + 8];  // hi / mid / lo planes of the aggregated rows

@@ -426,12 +426,15 @@ def fused_sage_supported(f_in: int, f_out: int) -> bool:
     """SAGEConv's update through kgx_spmm_gemm (any F_in, F_out <= 128, multiples
     of 4): out = x W_self + b by kgx_dense, then out = relu?(out + REDUCE(x) W_neigh)
     in the fused aggregation's store, so the [N, F_in] aggregate is never
-    written (C5: 2.45M x 100).  KGX_FUSED_SAGE=0 / KGX_FUSED=0 turn it off."""
+    written (C5: 2.45M x 100).  Opt-in (KGX_FUSED_SAGE=1): at C5 it measured
+    slower than the two-step path -- the fused main kernel's W registers hold
+    it at 4 waves per SIMD, and C5's 50-edge rows want spmm_kernel's gather
+    depth.  KGX_FUSED=0 turns it off too."""
     import os
 
     if os.environ.get("KGX_FUSED", "1") in ("0", "false", "False"):
         return False
-    if os.environ.get("KGX_FUSED_SAGE", "1") in ("0", "false", "False"):
+    if os.environ.get("KGX_FUSED_SAGE", "0") not in ("1", "true", "True"):
         return False
     return 0 < f_in <= 128 and f_in % 4 == 0 and 0 < f_out <= 128 and f_out % 4 == 0
 

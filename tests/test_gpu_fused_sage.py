@@ -3,7 +3,7 @@
 F_in < 128 (a multiple of 4): the lanes past F_in re-load column 0 and put
 zeros in the bf16x3 planes, W's rows past F_in load as zero; F_out not a
 multiple of 16: the stores stop at F_out.  SAGEConv at inference (root_weight,
-mean / sum / max) runs out = b + x W_self (kgx_dense) and then the fused
+mean / sum / max; opt-in, KGX_FUSED_SAGE=1) runs out = b + x W_self (kgx_dense) and then the fused
 aggregation adds REDUCE(x) W_neigh into out in its store (relu there too) --
 sage_conv.py:404-433 with the [N, F_in] aggregate never written.  Checked
 against the oracle within the fp32 dot-product bound, on graphs whose rows
@@ -95,7 +95,9 @@ def test_fused_narrow_overwrite(dev, F_in, F_out):
 def test_sage_layer_fused_vs_oracle(dev, monkeypatch, aggr, F_in, F_out):
     """SAGEConv inference takes the fused update (no kops.aggregate call) and
     matches the oracle's sage_forward (sage_conv.py:404-439) within 1e-5 of the
-    same forward on |x|, |W|, |b|; KGX_FUSED_SAGE=0 gives the two-step path."""
+    same forward on |x|, |W|, |b| (KGX_FUSED_SAGE=1); KGX_FUSED_SAGE=0 gives the
+    two-step path."""
+    monkeypatch.setenv("KGX_FUSED_SAGE", "1")
     N = 4000
     s, d = _graph(13, N, 50000)
     rng = np.random.default_rng(3)
@@ -123,8 +125,9 @@ def test_sage_layer_fused_vs_oracle(dev, monkeypatch, aggr, F_in, F_out):
         assert err.max() <= 1e-5, err.max()
 
 
-def test_sage_layer_fused_degree_zero_rows(dev):
+def test_sage_layer_fused_degree_zero_rows(dev, monkeypatch):
     """Rows with no in-edges: the aggregate is 0, so out = relu(b + x W_self)."""
+    monkeypatch.setenv("KGX_FUSED_SAGE", "1")
     N, F = 10, 100
     s = np.array([1, 2, 3], np.int64)
     d = np.array([0, 0, 9], np.int64)

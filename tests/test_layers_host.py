@@ -97,12 +97,14 @@ def test_fused_shape_routing(monkeypatch):
 
 def test_fused_sage_routing(monkeypatch):
     """SAGEConv's fused update (kgx_spmm_gemm accumulating into b + x W_self):
-    any F_in, F_out <= 128 that are multiples of 4 (C5: 100 -> 100);
-    KGX_FUSED_SAGE=0 / KGX_FUSED=0 turn it off."""
+    opt-in with KGX_FUSED_SAGE=1; any F_in, F_out <= 128 that are multiples of 4
+    (C5: 100 -> 100); KGX_FUSED=0 turns it off too."""
     from keras_geometric_amd import ops as kops
 
     monkeypatch.delenv("KGX_FUSED", raising=False)
     monkeypatch.delenv("KGX_FUSED_SAGE", raising=False)
+    assert not kops.fused_sage_supported(100, 100)  # opt-in: slower than the two-step path at C5
+    monkeypatch.setenv("KGX_FUSED_SAGE", "1")
     assert kops.fused_sage_supported(100, 100) and kops.fused_sage_supported(128, 4)
     assert not kops.fused_sage_supported(102, 100)  # rows must be whole float4s
     assert not kops.fused_sage_supported(256, 256) and not kops.fused_sage_supported(100, 132)
