@@ -161,7 +161,11 @@ int kgx_spmm(int reduce, int epilogue,
 /* kgx_spmm with the schedule's short-row suffix named: items [n_long_items,
  * n_items) are unsplit rows of degree <= KGX_SHORT_ROW_MAX (defined below),
  * taken several per lane group by a second kernel (not with message dropout
- * or column slices wider than 64 lanes).  n_long_items = n_items is kgx_spmm. */
+ * or column slices wider than 64 lanes).  n_long_items = n_items is kgx_spmm.
+ * EXACT mode (items = NULL): 0 < n_long_items < n_rows names the same suffix
+ * of the degree-descending `rows` list, rows[n_long_items, n_rows), for the
+ * same kernel (each row still one chain of adds in CSR order: bit-identical);
+ * any other value leaves every row to the main kernel. */
 int kgx_spmm_ex(int reduce, int epilogue, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
                 const int32_t* items, int64_t n_items, int64_t n_long_items, const int32_t* split,
                 int64_t n_split, const int32_t* idx, const float* w, const float* table, int64_t ld_table,

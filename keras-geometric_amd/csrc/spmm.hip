@@ -61,6 +61,9 @@ struct SpmmArgs {
   int f_base;  // first column of this launch (column slicing of wide F)
   int long_rows;  // EXACT mode: rows of degree >= kLongRow are reduced by spmm_long_kernel
   int64_t n_long;  // items [n_long, n_items): short rows (degree <= KGX_SHORT_ROW_MAX) for spmm_short_kernel
+  // EXACT mode (no items): rows[n_rows_long, n_rows) of the degree-ordered list have degree <=
+  // KGX_SHORT_ROW_MAX and go to spmm_short_kernel (each row still one chain in CSR order)
+  int64_t n_rows_long;
   // two-table gathers (kgx_spmm_ex2): sources c >= n_t1 are rows c - n_t1 of a second
   // table (same ld_t); t2b = table2 - n_t1 * ld_t as an address.  n_t1 = INT32_MAX: one table.
   const float* t2b;
@@ -202,7 +205,7 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
   const int G = a.G;
   const int lane = threadIdx.x & (G - 1);
   const int64_t ngroups = (int64_t(gridDim.x) * kBlock) >> a.lgG;
-  const int64_t n_work = a.items ? a.n_long : a.n_rows;
+  const int64_t n_work = a.items ? a.n_long : a.n_rows_long;
 
   // Every global load below is unconditional (clamped to a valid address) and
   // masked work is folded in as the reduction's identity: a load under a
@@ -632,20 +635,29 @@ __global__ __launch_bounds__(kBlock) void spmm_short_kernel(SpmmArgs a) {
   const int fo = lane * VEC;
   const bool fv = fo < a.F;
   const int fl = fv ? fo : a.F - VEC;
-  const int64_t n_short = a.n_items - a.n_long;
+  // the schedule's items [n_long, n_items), or in EXACT mode rows [n_rows_long, n_rows)
+  const int64_t s0 = a.items ? a.n_long : a.n_rows_long;
+  const int64_t s1 = a.items ? a.n_items : a.n_rows;
+  const int64_t n_short = s1 - s0;
   for (int64_t q = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> a.lgG; q * kSR < n_short; q += ngroups) {
     int32_t row[kSR], beg[kSR], deg[kSR];
 #pragma unroll
     for (int r = 0; r < kSR; ++r) {
-      const int64_t it = a.n_long + q * kSR + r;
+      const int64_t it = s0 + q * kSR + r;
       row[r] = -1;
       beg[r] = 0;
       deg[r] = 0;
-      if (it < a.n_items) {
-        const int4 v = a.items[it];
-        row[r] = v.x;
-        beg[r] = v.y;
-        deg[r] = v.z - v.y;
+      if (it < s1) {
+        if (a.items) {
+          const int4 v = a.items[it];
+          row[r] = v.x;
+          beg[r] = v.y;
+          deg[r] = v.z - v.y;
+        } else {
+          row[r] = a.rows[it];
+          beg[r] = a.rowptr[row[r]];
+          deg[r] = a.rowptr[row[r] + 1] - beg[r];
+        }
       }
     }
     float acc[kSR][VEC];
@@ -899,18 +911,20 @@ int launch_main(const SpmmArgs& a_in, hipStream_t s) {
     }
   }
   if constexpr (NT == 1) {
-    if (a.items && a.n_long < a.n_items && !a.drop_key) {
+    const int64_t n_short = a.items ? a.n_items - a.n_long : a.n_rows - a.n_rows_long;
+    if (n_short > 0 && !a.drop_key) {
       auto ks = spmm_short_kernel<VEC, RED, W, TWO>;
-      hipLaunchKernelGGL(ks, dim3(resident_grid(ks, (a.n_items - a.n_long + kSR - 1) / kSR, a.G)), dim3(kBlock), 0, s,
-                         a);
+      hipLaunchKernelGGL(ks, dim3(resident_grid(ks, (n_short + kSR - 1) / kSR, a.G)), dim3(kBlock), 0, s, a);
       KGX_CHECK_LAUNCH();
     } else {
       a.n_long = a.n_items;
+      a.n_rows_long = a.n_rows;
     }
   } else {
     a.n_long = a.n_items;
+    a.n_rows_long = a.n_rows;
   }
-  const int64_t work_long = a.items ? a.n_long : a.n_rows;
+  const int64_t work_long = a.items ? a.n_long : a.n_rows_long;
   if (work_long > 0) {
     auto k = spmm_kernel<VEC, NT, RED, W, false, TWO>;
     if constexpr (RED == KGX_SUM && !TWO) {
@@ -1045,6 +1059,8 @@ extern "C" int kgx_spmm_ex2(int reduce, int epilogue, const int32_t* rowptr, con
   a.split = reinterpret_cast<const int4*>(split);
   a.n_split = use_items ? n_split : 0;
   a.n_long = use_items ? n_long_items : 0;
+  // EXACT mode: 0 < n_long_items < n_rows names the short-row suffix of the degree-ordered rows
+  a.n_rows_long = (!use_items && reduce != KGX_STD && n_long_items > 0 && n_long_items < n_rows) ? n_long_items : n_rows;
   a.idx = idx;
   a.w = w;
   a.epi = epilogue;

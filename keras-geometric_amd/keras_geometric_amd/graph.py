@@ -202,6 +202,23 @@ def short_suffix_start(items: torch.Tensor) -> int:
     return int(not_short[-1]) + 1 if not_short.numel() else 0
 
 
+def exact_short_start(g: CSRGraph) -> int:
+    """EXACT mode (no schedule): the index in g.rows (degree-descending) where the
+    suffix of rows of degree <= SHORT_ROW_MAX starts; kgx_spmm reduces that
+    suffix with its short-row kernel (each row still one chain in CSR order).
+    -1 when there is no such suffix or KGX_SHORT_ROWS=0 (cached per graph)."""
+    hit = g.extras.get("exact_short")
+    if hit is not None:
+        return hit
+    n = -1
+    if g.rows is not None and g.n_dst > 0 and os.environ.get("KGX_SHORT_ROWS", "1") not in ("0", "false", "False"):
+        smax = int(os.environ.get("KGX_SHORT_MAX", SHORT_ROW_MAX))
+        k = int((g.deg[g.rows.long()] > smax).sum())  # rows come in descending degree
+        n = k if 0 < k < g.n_dst else -1
+    g.extras["exact_short"] = n
+    return n
+
+
 def row_of_slot(g: CSRGraph) -> torch.Tensor:
     """int32 [kept]: the destination row of every CSR slot (cached)."""
     r = g.extras.get("row_of_slot")

@@ -595,6 +595,13 @@ def _needs_grad(*ts) -> bool:
     return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts)
 
 
+def _exact_short(g, red) -> int:
+    """EXACT mode's short-row suffix for kgx_spmm's n_long_items (graph.exact_short_start)."""
+    from . import graph as G
+
+    return -1 if red == nat.STD else G.exact_short_start(g)
+
+
 def _aggregate_raw(g, table, red, weighted, by_edge, epilogue, bias, xroot, gin_scale, exact, drop_p=0.0,
                    drop_seed=0):
     items, _, split, _, n_slots = g.work(exact or red == nat.STD)
@@ -606,7 +613,8 @@ def _aggregate_raw(g, table, red, weighted, by_edge, epilogue, bias, xroot, gin_
         raise ValueError("message dropout is implemented for sum aggregation (GCNConv) only")
     return _timed(lambda: torch.ops.kgx.spmm(
         table, g.rowptr, g.rows, items, split, idx, w, n_slots, red, epilogue, bias, xroot, float(gin_scale),
-        g.eid if drop_p > 0 else None, float(drop_p), int(drop_seed), g.n_long if items is not None else -1,
+        g.eid if drop_p > 0 else None, float(drop_p), int(drop_seed),
+        g.n_long if items is not None else _exact_short(g, red),
     ))
 
 
