@@ -63,7 +63,8 @@ def spmm(
     partials = None
     if items is not None and n_split > 0 and reduce != nat.STD:
         partials = torch.empty((n_slots, F), dtype=torch.float32, device=dev)
-    n_long = n_items if n_long < 0 or n_long > n_items else n_long
+    if items is not None:  # EXACT mode (no items): n_long names the short suffix of the row list (or -1)
+        n_long = n_items if n_long < 0 or n_long > n_items else n_long
     # EXACT mode: the hub-row kernel hands its items out dynamically (KGX_EXACT_DYN=0: static, A/B only)
     counters = (torch.zeros(2, dtype=torch.int32, device=dev)
                 if items is None and reduce != nat.STD and _EXACT_DYN else None)
