@@ -102,7 +102,8 @@ class LoopbackComm(kd.TorchComm):
             ms = out.numel() * out.element_size() / (self.link_gbps * 1e6)
             if ms > 0:
                 torch.cuda._sleep(int(ms * self.cycles_per_ms))
-            self.all_to_all_single(out, inp, out_splits, in_splits)
+            if self._land(out):
+                self.all_to_all_single(out, inp, out_splits, in_splits)
             inp.record_stream(self.link)
             out.record_stream(self.link)
             ev = torch.cuda.Event()
@@ -133,7 +134,8 @@ class LoopbackComm(kd.TorchComm):
             ms = out.numel() * out.element_size() * (self.w - 1) / self.w / (self.link_gbps * 1e6)
             if ms > 0:
                 torch.cuda._sleep(int(ms * self.cycles_per_ms))
-            self.all_gather(out, inp)
+            if self._land(out):
+                self.all_gather(out, inp)
             inp.record_stream(self.link)
             out.record_stream(self.link)
             ev = torch.cuda.Event()
@@ -169,8 +171,10 @@ def main():
     ap.add_argument("--link-gbps", type=float, default=0.0,
                     help="model the exchange: per-GPU receive rate in GB/s (0: no link time)")
     ap.add_argument("--free-exchange", action="store_true",
-                    help="with --link-gbps 0: received buffers land once, later exchanges move nothing "
-                         "(the rank's compute alone; default: a loopback device copy per exchange)")
+                    help="received buffers land once (a loopback device copy), later exchanges copy nothing: "
+                         "with --link-gbps 0 the step is the rank's compute alone; with a link rate the "
+                         "modelled transfer time stands for RCCL's receive (default: a loopback device copy "
+                         "per exchange, after the modelled link time)")
     args = ap.parse_args()
     layer_kind, n_cfg, e_cfg, F, scaling = CONFIGS[args.config]
     n_cfg = args.nodes or n_cfg
@@ -200,8 +204,7 @@ def main():
         os.environ["KGX_HALO_MERGE"] = unit
         os.environ["KGX_HALO_A_LATE"] = a_late
         n_local = kd.equal_bounds(n_glob, P)[1]
-        comm = LoopbackComm(P, n_local, args.link_gbps, cycles_per_ms,
-                            free_exchange=args.free_exchange and args.link_gbps <= 0)
+        comm = LoopbackComm(P, n_local, args.link_gbps, cycles_per_ms, free_exchange=args.free_exchange)
         gcn = layer_kind == "gcn"
         sg = kd.ShardedGraph.rmat(n_glob, e_glob, seed=0, device=dev, comm=comm, self_loops=gcn, gcn_norm=gcn,
                                   halo_chunks=K, n_features=F)
@@ -243,8 +246,9 @@ def main():
                 "push_pull": pp is not None and pp.kind == "halo", "merged": merged == "1", "merge_unit": unit,
                 "a_late": a_late == "1", "share_den": int(den),
                 "link_gbps": args.link_gbps,
-                "exchange_model": "free" if comm.free_exchange else "loopback-copy" if args.link_gbps <= 0
-                else "modelled-link", "step_ms": round(t0.elapsed_time(t1) / args.steps, 3),
+                "exchange_model": ("modelled-link" if args.link_gbps > 0 else "free" if comm.free_exchange
+                                   else "loopback-copy") + ("" if args.link_gbps <= 0 or not comm.free_exchange
+                                                            else ", no local copy"), "step_ms": round(t0.elapsed_time(t1) / args.steps, 3),
                 "launch_ms": [round(v, 3) for v in launch_ms],
                 "own_edges": g_own.kept, "chunk_edges": [g.kept for g in g_chunks],
                 "halo_rows_pull_only": sg.n_halo, "halo_rows": pp.n_rows if pp else sg.n_halo,
