@@ -1075,7 +1075,14 @@ class ShardedGCNConv(Layer):
         sg = self.sg
         g_a, g_b, later, first_wait = sg.merged_passes(pp)
         steps = [st for c in pp.chunks for st in c.steps]
-        a_late = os.environ.get("KGX_HALO_A_LATE", "0") == "1"  # measurement A/B: own-only rows after the merged pass
+        # the own-only rows' pass (g_a) after the merged pass when two or more exchange
+        # groups follow the first: then the first pack runs alone and the first transfer
+        # starts earlier (tools/shard_sim.py at modelled 400 GB/s, NS weak P=8: K=2 step
+        # groups 13.91 -> 12.98 ms, K=4 chunks 14.08 -> 13.81; with one group or none
+        # after the first it measured slower: K=1 14.22 -> 15.82, K=2 chunks 13.91 ->
+        # 14.47).  KGX_HALO_A_LATE=0 / 1 forces either order (measurement A/B).
+        forced = os.environ.get("KGX_HALO_A_LATE")
+        a_late = forced == "1" if forced in ("0", "1") else len(later) >= 2
         with torch.no_grad():
             works = sg.start_halo_exchange(x_local, halo, pp.chunks)
             handles = []

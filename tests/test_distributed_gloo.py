@@ -210,6 +210,16 @@ def _worker(rank, world, chunks, port, q):
         finally:
             del os.environ["KGX_HALO_MERGE"]
         assert pp.merged["chunk"][1] is not None
+        # the own-only rows' pass before / after the merged pass (the default picks by the
+        # number of later exchange groups): disjoint rows, so the same bits either way
+        for order in ("0", "1"):
+            os.environ["KGX_HALO_A_LATE"] = order
+            try:
+                with torch.no_grad():
+                    y_order = layer(torch.from_numpy(x[lo:hi]))
+            finally:
+                del os.environ["KGX_HALO_A_LATE"]
+            assert torch.equal(y_order, y), order
         os.environ["KGX_HALO_MERGED"] = "0"
         try:
             with torch.no_grad():

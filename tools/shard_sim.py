@@ -161,7 +161,8 @@ def main():
     ap.add_argument("--push", default="1", help="KGX_HALO_PUSH values to run (0: pull-only halo)")
     ap.add_argument("--merged", default="1", help="KGX_HALO_MERGED values to run (0: round-2 own pass + chunk passes)")
     ap.add_argument("--merge-unit", default="step", help="KGX_HALO_MERGE values: step, chunk")
-    ap.add_argument("--a-late", default="0", help="KGX_HALO_A_LATE values (1: own-only rows after the merged pass)")
+    ap.add_argument("--a-late", default="auto",
+                    help="KGX_HALO_A_LATE values (1: own-only rows after the merged pass; auto: the layer's rule)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--share-den", default="8",
                     help="KGX_SHARE_DEN values timed on each built shard (the overlapped passes leave 1/den of "
@@ -197,12 +198,15 @@ def main():
     for exchange, merged, push, K, unit, a_late in runs:
         if exchange == "allgather" and (push == "0" or merged == "0"):
             continue  # the all-gather has neither pulls nor pushes, and always runs merged
-        if merged == "0" and (unit != "step" or a_late != "0"):
+        if merged == "0" and (unit != "step" or a_late == "1"):
             continue
         os.environ["KGX_HALO_PUSH"] = push
         os.environ["KGX_HALO_MERGED"] = merged
         os.environ["KGX_HALO_MERGE"] = unit
-        os.environ["KGX_HALO_A_LATE"] = a_late
+        if a_late in ("0", "1"):
+            os.environ["KGX_HALO_A_LATE"] = a_late
+        else:
+            os.environ.pop("KGX_HALO_A_LATE", None)
         n_local = kd.equal_bounds(n_glob, P)[1]
         comm = LoopbackComm(P, n_local, args.link_gbps, cycles_per_ms, free_exchange=args.free_exchange)
         gcn = layer_kind == "gcn"
@@ -244,7 +248,7 @@ def main():
                 "config": args.config, "layer": layer_kind, "scaling": scaling, "nodes": n_glob, "edges": e_glob,
                 "features": F, "world": P, "exchange": pp.kind if pp else "pull", "chunks": K,
                 "push_pull": pp is not None and pp.kind == "halo", "merged": merged == "1", "merge_unit": unit,
-                "a_late": a_late == "1", "share_den": int(den),
+                "a_late": a_late, "share_den": int(den),
                 "link_gbps": args.link_gbps,
                 "exchange_model": ("modelled-link" if args.link_gbps > 0 else "free" if comm.free_exchange
                                    else "loopback-copy") + ("" if args.link_gbps <= 0 or not comm.free_exchange
