@@ -231,23 +231,46 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
 #endif
   constexpr int kDynRows = KGX_DYN_ROWS;
   const int64_t gid = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> a.lgG;
+  // dyn_rows == 2 (KGX_EXACT_FORK=3): batch b, one atomic, is rows b, b + NB,
+  // b + 2 NB, ... -- one row from each kDynRows-th of the degree-descending
+  // list, so every batch carries about the same work, heaviest batches first
+  const bool dyn_il = dyn && a.dyn_rows == 2;
+  const int64_t NB = (n_work + kDynRows - 1) / kDynRows;
   int64_t it = gid, batch_end = 0;
+  int jj = kDynRows;
   if (dyn) it = batch_end = 0;
   for (;;) {
-    if (dyn) {
-      if (it >= batch_end) {
+    int64_t cur;
+    if (dyn_il) {
+      if (jj >= kDynRows) {
         int64_t b = 0;
-        if (lane == 0) b = int64_t(atomicAdd(a.dyn + 1, kDynRows));
-        b = __shfl(b, 0, G);  // the group's lane 0 (groups are aligned G-lane slices of the wave)
-        it = b;
-        batch_end = b + kDynRows < n_work ? b + kDynRows : n_work;
+        if (lane == 0) b = int64_t(atomicAdd(a.dyn + 1, 1));
+        it = __shfl(b, 0, G);
+        jj = 0;
       }
-      if (it >= n_work) break;
-    } else if (it >= n_work) {
-      break;
+      if (it >= NB) break;
+      cur = it + int64_t(jj) * NB;
+      ++jj;
+      if (cur >= n_work) {  // the later rows of this batch are past the end too
+        jj = kDynRows;
+        continue;
+      }
+    } else {
+      if (dyn) {
+        if (it >= batch_end) {
+          int64_t b = 0;
+          if (lane == 0) b = int64_t(atomicAdd(a.dyn + 1, kDynRows));
+          b = __shfl(b, 0, G);  // the group's lane 0 (groups are aligned G-lane slices of the wave)
+          it = b;
+          batch_end = b + kDynRows < n_work ? b + kDynRows : n_work;
+        }
+        if (it >= n_work) break;
+      } else if (it >= n_work) {
+        break;
+      }
+      cur = it;
+      it = dyn ? it + 1 : it + ngroups;
     }
-    const int64_t cur = it;
-    it = dyn ? it + 1 : it + ngroups;
     int32_t row, beg, end, slot;
     if (a.items) {
       const int4 v = a.items[cur];
@@ -873,8 +896,11 @@ int launch_main(const SpmmArgs& a_in, hipStream_t s) {
         const char* h = getenv("KGX_EXACT_HUB_CUS");
         return h ? atoi(h) : 0;
       }();
-      const bool fork_on = fork_mode == 1 || fork_mode == 2;
-      a.dyn_rows = fork_mode == 1 ? 1 : 0;
+      // KGX_EXACT_FORK=3: forked, spmm_kernel on its full grid taking interleaved
+      // row batches from a counter (one atomic per kDynRows rows), and the
+      // short-row kernel after it, once the hub kernel's tail is over
+      const bool fork_on = fork_mode == 1 || fork_mode == 2 || fork_mode == 3;
+      a.dyn_rows = fork_mode == 1 ? 1 : (fork_mode == 3 ? 2 : 0);
       int64_t hub_blocks = nb;
       if (fork_mode == 2 && hub_cus > 0 && hub_cus < hub_blocks) hub_blocks = hub_cus;
       if (a.dyn && fork_on) {
@@ -910,20 +936,30 @@ int launch_main(const SpmmArgs& a_in, hipStream_t s) {
       KGX_CHECK_LAUNCH();
     }
   }
+  bool short_on = false;
+  int64_t n_short = 0;
   if constexpr (NT == 1) {
-    const int64_t n_short = a.items ? a.n_items - a.n_long : a.n_rows - a.n_rows_long;
-    if (n_short > 0 && !a.drop_key) {
-      auto ks = spmm_short_kernel<VEC, RED, W, TWO>;
-      hipLaunchKernelGGL(ks, dim3(resident_grid(ks, (n_short + kSR - 1) / kSR, a.G)), dim3(kBlock), 0, s, a);
-      KGX_CHECK_LAUNCH();
-    } else {
-      a.n_long = a.n_items;
-      a.n_rows_long = a.n_rows;
-    }
-  } else {
+    n_short = a.items ? a.n_items - a.n_long : a.n_rows - a.n_rows_long;
+    short_on = n_short > 0 && !a.drop_key;
+  }
+  if (!short_on) {
     a.n_long = a.n_items;
     a.n_rows_long = a.n_rows;
   }
+  auto launch_short = [&]() -> int {
+    if constexpr (NT == 1) {
+      if (short_on) {
+        auto ks = spmm_short_kernel<VEC, RED, W, TWO>;
+        hipLaunchKernelGGL(ks, dim3(resident_grid(ks, (n_short + kSR - 1) / kSR, a.G)), dim3(kBlock), 0, s, a);
+        KGX_CHECK_LAUNCH();
+      }
+    }
+    return KGX_OK;
+  };
+  // the short-row kernel first, except beside a forked hub kernel whose rows
+  // spmm_kernel's dynamic batches work around (KGX_EXACT_FORK=3)
+  const bool short_last = a.dyn_rows == 2 && joined;
+  if (!short_last && launch_short() != KGX_OK) return KGX_ERR_HIP;
   const int64_t work_long = a.items ? a.n_long : a.n_rows_long;
   if (work_long > 0) {
     auto k = spmm_kernel<VEC, NT, RED, W, false, TWO>;
@@ -938,6 +974,7 @@ int launch_main(const SpmmArgs& a_in, hipStream_t s) {
     hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, s, a);
     KGX_CHECK_LAUNCH();
   }
+  if (short_last && launch_short() != KGX_OK) return KGX_ERR_HIP;
   if (joined && hipStreamWaitEvent(s, joined->join, 0) != hipSuccess) {
     set_error("kgx_spmm: stream join failed");
     return KGX_ERR_HIP;
