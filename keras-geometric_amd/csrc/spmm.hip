@@ -880,25 +880,28 @@ int launch_main(const SpmmArgs& a_in, hipStream_t s) {
       else if (gh == 8) kh = spmm_hub_kernel<8, RED, W>;
       const int64_t work = a.n_rows * ((a.F + 4 * gh - 1) / (4 * gh));
       const int64_t nb = work < cu_count() ? work : cu_count();  // one resident block per CU
-      // Experiment (KGX_EXACT_FORK=1, off by default): the hub kernel forked
-      // beside spmm_kernel, whose rows are then handed out dynamically.
-      // Measured slower at NS: contiguous row batches of the
-      // degree-descending list concentrate the heaviest rows on single groups
-      // (8 / 32 / 256-row batches: 12.7 / 15.0 / 65 ms against 10.9 static).
-      // KGX_EXACT_FORK=2: forked, but spmm_kernel keeps its static interleaved
-      // (grid-stride) rows, with its grid cut to the block slots the hub blocks
-      // leave, so every group is resident from the start (no atomics).
+      // Experiments: KGX_EXACT_FORK=1, the hub kernel forked beside spmm_kernel,
+      // whose rows are then handed out dynamically in contiguous batches of the
+      // degree-descending list -- which concentrate the heaviest rows on single
+      // groups (8 / 32 / 256-row batches: 12.7 / 15.0 / 65 ms against 10.9
+      // static); KGX_EXACT_FORK=2, forked, spmm_kernel keeping its static
+      // grid-stride rows with its grid cut to the block slots the hub blocks
+      // leave (10.29-10.32 against 9.92-10.01 ms: the cut grid runs short of
+      // gathers in flight for the whole launch).
       static const int fork_mode = [] {
         const char* h = getenv("KGX_EXACT_FORK");
-        return h ? atoi(h) : 0;
+        return h ? atoi(h) : 3;  // 3: measured 9.69-9.73 -> 8.96-8.98 ms at NS (0: sequential)
       }();
       static const int hub_cus = [] {
         const char* h = getenv("KGX_EXACT_HUB_CUS");
         return h ? atoi(h) : 0;
       }();
-      // KGX_EXACT_FORK=3: forked, spmm_kernel on its full grid taking interleaved
-      // row batches from a counter (one atomic per kDynRows rows), and the
-      // short-row kernel after it, once the hub kernel's tail is over
+      // KGX_EXACT_FORK=3 (default): forked, spmm_kernel on its full grid taking
+      // interleaved row batches from a counter (one atomic per kDynRows rows),
+      // and the short-row kernel after it, once the hub kernel's tail is over.
+      // The hub kernel's mass of rows ends in ~0.3 ms; its largest row then
+      // holds two CUs for ~1 ms, which spmm_kernel's batches fill: NS EXACT
+      // aggregation 9.69-9.73 -> 8.96-8.98 ms (profiles/r04/exact_fork3_ab.jsonl)
       const bool fork_on = fork_mode == 1 || fork_mode == 2 || fork_mode == 3;
       a.dyn_rows = fork_mode == 1 ? 1 : (fork_mode == 3 ? 2 : 0);
       int64_t hub_blocks = nb;
