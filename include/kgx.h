@@ -183,9 +183,12 @@ int kgx_spmm_ex(int reduce, int epilogue, const int32_t* rowptr, const int32_t* 
  * (row, column group) items dynamically, so its blocks balance instead of
  * waiting behind the largest row (bit-identical results: every row is still
  * reduced by one lane chain in CSR order, aggregators.py:126-137).  NULL: the
- * static schedule.  (KGX_EXACT_FORK=1, an experiment: the hub kernel also
- * forks onto a library-owned stream beside the main kernel, whose rows are
- * then handed out from counters[1]; joined back into `stream`.) */
+ * static schedule.  With counters the hub kernel also forks onto a
+ * library-owned stream beside the main kernel (joined back into `stream`
+ * before the call returns), and the main kernel takes interleaved batches of
+ * rows from counters[1] (batch b = rows b, b + NB, ..., one atomic per 8 rows),
+ * so the GPU is not idle behind the largest hub row (KGX_EXACT_FORK=0: the
+ * sequential form). */
 int kgx_spmm_ex2(int reduce, int epilogue, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
                  const int32_t* items, int64_t n_items, int64_t n_long_items, const int32_t* split, int64_t n_split,
                  const int32_t* idx, const float* w, const float* table, int64_t ld_table, const float* table2,
