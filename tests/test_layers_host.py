@@ -113,3 +113,30 @@ def test_fused_sage_routing(monkeypatch):
     monkeypatch.setenv("KGX_FUSED_SAGE", "1")
     monkeypatch.setenv("KGX_FUSED", "0")
     assert not kops.fused_sage_supported(100, 100)
+
+
+def _cpu_graph(deg):
+    """A CSRGraph shell on the host: rows in descending degree, as build_csr orders them."""
+    deg = torch.tensor(deg, dtype=torch.int32)
+    rowptr = torch.zeros(len(deg) + 1, dtype=torch.int32)
+    rowptr[1:] = torch.cumsum(deg, 0)
+    kept = int(rowptr[-1])
+    rows = torch.argsort(-deg.long(), stable=True).to(torch.int32)
+    z = torch.zeros(max(kept, 1), dtype=torch.int32)
+    return G.CSRGraph(n_src=len(deg), n_dst=len(deg), n_input_edges=kept, kept=kept, max_degree=int(deg.max()),
+                      flags=0, rowptr=rowptr, col=z, eid=z, deg=deg, rows=rows)
+
+
+def test_exact_short_start(monkeypatch):
+    """EXACT mode's short-row suffix (kgx_spmm_ex n_long_items with items = NULL):
+    the index in the degree-descending row list where degree <= 7 starts; -1 when
+    every row is short or none is, or with KGX_SHORT_ROWS=0."""
+    monkeypatch.delenv("KGX_SHORT_ROWS", raising=False)
+    monkeypatch.delenv("KGX_SHORT_MAX", raising=False)
+    g = _cpu_graph([3, 9, 0, 2048, 7, 8, 1])
+    assert G.exact_short_start(g) == 3  # rows of degree 2048, 9, 8 come first
+    assert g.extras["exact_short"] == 3
+    assert G.exact_short_start(_cpu_graph([1, 2, 3])) == -1  # all short: the main kernel keeps them
+    assert G.exact_short_start(_cpu_graph([8, 9, 100])) == -1  # none short
+    monkeypatch.setenv("KGX_SHORT_ROWS", "0")
+    assert G.exact_short_start(_cpu_graph([3, 9, 0])) == -1
