@@ -5,6 +5,8 @@
 # mean: fused update (narrow main kernel U = 8, PF = 2) vs KGX_TINY_ACC_EARLY=1
 # (libkgx_accearly.so) vs the two-step path (KGX_FUSED_SAGE=0); kernel stats of
 # the fused C5 layer.
+# Build first (here): make -C keras-geometric_amd/csrc variant NAME=accearly DEFS=-DKGX_TINY_ACC_EARLY=1 and
+#   variant NAME=u8pf2 DEFS="-DKGX_FUSED_U=8 -DKGX_FUSED_PF=2"
 set -o pipefail
 mkdir -p gpurun_out/r4ab2
 export TMPDIR=/tmp

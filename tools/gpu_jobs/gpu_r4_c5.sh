@@ -3,6 +3,7 @@
 # NS GCN layer; C5 SAGEConv mean with the fused update (narrow kernels, main
 # kernel U = 6) against KGX_TINY_ACC_EARLY=1 (libkgx_accearly.so) and the
 # two-step path (KGX_FUSED_SAGE=0); rocprofv3 kernel stats of the fused C5 layer.
+# Build first (here): make -C keras-geometric_amd/csrc variant NAME=accearly DEFS=-DKGX_TINY_ACC_EARLY=1
 set -o pipefail
 mkdir -p gpurun_out/r4c5
 export TMPDIR=/tmp

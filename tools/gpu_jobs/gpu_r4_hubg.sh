@@ -2,6 +2,7 @@
 # Round 4: EXACT hub rows in 4 column groups of 32 features (KGX_HUB_G=8,
 # lib/variants/libkgx_hubg8.so) against 2 groups of 64 (shipped), NS --exact,
 # interleaved; the bit-identity tests under the variant.
+# Build first (here): make -C keras-geometric_amd/csrc variant NAME=hubg8 DEFS=-DKGX_HUB_G=8
 set -o pipefail
 mkdir -p gpurun_out/r4h
 export TMPDIR=/tmp
