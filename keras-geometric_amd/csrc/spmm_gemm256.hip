@@ -213,6 +213,13 @@ __device__ __forceinline__ void transform_tile(const F256Args& a, const short (*
 #ifndef KGX_F256_MID_PF
 #define KGX_F256_MID_PF 6
 #endif
+// pre_gin: load the rows' own x rows with the next tile's prefetch instead of
+// after the fold, where their latency was exposed once per tile (C4 layer
+// 21.51-21.53 -> 21.20-21.21 ms interleaved; 8 more VGPRs spilled in a kernel
+// already at 256, which costs less than the wait)
+#ifndef KGX_F256_ROOT_PF
+#define KGX_F256_ROOT_PF 1
+#endif
 template <int RED, bool WEIGHTED, int PF, bool TWO>
 __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_kernel(F256Args a) {
   using R = RowRed<RED>;
@@ -240,6 +247,9 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_kernel(F256Args a) {
   int32_t row[2], beg[2], end[2], slot[2];
   int pn[2];
   float pv[2][PF][4], pw[2][PF];
+#if KGX_F256_ROOT_PF
+  float px[2][4];  // pre_gin: the rows' own x rows, loaded with the prefetch
+#endif
   // descriptors of items it, it + 1 and their first PF gathers
   auto fetch = [&](int64_t it) {
     int32_t c[2][PF];
@@ -275,6 +285,12 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_kernel(F256Args a) {
 #pragma unroll
       for (int u = 0; u < PF; ++u)
         if (u < pn[r]) vload<4>(pv[r][u], gsrc256<TWO>(a, c[r][u]) + f);
+#if KGX_F256_ROOT_PF
+    if (a.pre_gin) {  // wave-uniform; clamped rows, unconditional per lane
+#pragma unroll
+      for (int r = 0; r < 2; ++r) vload<4>(px[r], a.x + int64_t(row[r] >= 0 ? row[r] : 0) * a.ld_x + f);
+    }
+#endif
   };
 
   fetch(int64_t(blockIdx.x) * kRows + 2 * wave);
@@ -361,7 +377,12 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_kernel(F256Args a) {
       for (int k = 0; k < 4; ++k) v[k] = full_row ? R::finish(acc[r][k], end[r] - beg[r]) : 0.0f;
       if (full_row && a.pre_gin) {
         float xv[4];
+#if KGX_F256_ROOT_PF
+#pragma unroll
+        for (int k = 0; k < 4; ++k) xv[k] = px[r][k];
+#else
         vload<4>(xv, a.x + int64_t(row[r]) * a.ld_x + f);
+#endif
 #pragma unroll
         for (int k = 0; k < 4; ++k) v[k] = __fadd_rn(__fmul_rn(a.gin_scale, xv[k]), v[k]);
       }
