@@ -864,7 +864,8 @@ def aggregate_transform(
     red = _reduce_id(reduce)
     if x2 is not None and _needs_grad(x, x2, W, bias):
         raise NotImplementedError("aggregate_transform(x2=...) is a forward-only (no_grad) path")
-    if out is not None:  # accumulate into `out` (sum only: the caller splits a row's edges)
+    if out is not None:  # into `out`: a sum may be split over launches (the caller splits a row's edges);
+        # a mean / max / min launch must cover each row's whole edge list
         if red != nat.SUM and (x2 is not None or x.shape[1] == F256):
             raise ValueError("aggregate_transform(out=...): two-table and 256-wide passes accumulate plain sums only")
         if accumulate and (pre_gin or (relu and x.shape[1] == F256)):
