@@ -857,6 +857,10 @@ class ShardedGraph:
         self._side.wait_stream(cur)
         with torch.cuda.stream(self._side):
             works = run()
+            # the side stream after its last packing kernel (the transfers run on the
+            # comm's own stream): a pass may wait for the packs without the transfers
+            self.packs_done = torch.cuda.Event()
+            self.packs_done.record()
         if any(w is None for w in works):  # synchronous comm: order the halo rows before later work
             cur.wait_stream(self._side)
         return works
@@ -1081,8 +1085,11 @@ class ShardedGCNConv(Layer):
         # groups 13.91 -> 12.98 ms, K=4 chunks 14.08 -> 13.81; with one group or none
         # after the first it measured slower: K=1 14.22 -> 15.82, K=2 chunks 13.91 ->
         # 14.47).  KGX_HALO_A_LATE=0 / 1 forces either order (measurement A/B).
+        # KGX_HALO_A_LATE=2 (experiment): pass A where it is, but after the packs
+        # (the side stream's packing alone on the GPU, then pass A beside the transfers)
         forced = os.environ.get("KGX_HALO_A_LATE")
-        a_late = forced == "1" if forced in ("0", "1") else len(later) >= 2
+        a_late = forced == "1" if forced in ("0", "1", "2") else len(later) >= 2
+        a_after_pack = forced == "2"
         with torch.no_grad():
             works = sg.start_halo_exchange(x_local, halo, pp.chunks)
             handles = []
@@ -1101,6 +1108,8 @@ class ShardedGCNConv(Layer):
                 out = torch.empty((x_local.shape[0], self.kernel.shape[1]), dtype=torch.float32,
                                   device=x_local.device)
             else:
+                if a_after_pack and getattr(sg, "packs_done", None) is not None and x_local.is_cuda:
+                    torch.cuda.current_stream(x_local.device).wait_event(sg.packs_done)
                 with kops.sharing_gpu():  # the exchange's packing and RCCL kernels run beside this pass
                     out = sg.backend.aggregate_transform(g_a, x_local, self.kernel, bias=bias)
             if g_b is not None:
