@@ -43,6 +43,18 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   return max(max(a, b), max(c, d));
 }
 
+// maximum of v over each 32-lane half of the wave (lanes 0-31, 32-63: the
+// 128-wide kernels' row groups), every lane active; each lane gets its half's
+__device__ __forceinline__ uint32_t half_max_u32(uint32_t v) {
+  v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0xB1, 0xF, 0xF, false)));
+  v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x4E, 0xF, 0xF, false)));
+  v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x141, 0xF, 0xF, false)));
+  v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x140, 0xF, 0xF, false)));
+  const uint32_t lo = max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16));
+  const uint32_t hi = max(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48));
+  return (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) & 32) ? hi : lo;
+}
+
 // |x| as bits (monotone in |x| for finite x; inf / NaN above 0x7f7fffff)
 __device__ __forceinline__ uint32_t abs_bits(float x) { return __builtin_bit_cast(uint32_t, x) & 0x7fffffffu; }
 
@@ -72,6 +84,28 @@ __device__ __forceinline__ void split2h_pair_nf(float a, float b, int sh, uint32
     hi &= 0x0000ffffu;
     lo = (lo & 0x0000ffffu) | (uint32_t(__builtin_bit_cast(uint16_t, static_cast<_Float16>(b))) << 16);
   }
+}
+
+// A 128-wide row held by a 32-lane group (four values per lane; both groups of
+// the wave call this together) -> this lane's packed hi / lo planes; returns
+// the row's unscale exponent.  A row with an inf / NaN gives non-finite
+// outputs in every column (inf * w, or inf * 0 = NaN, as in f32), so its scale
+// is taken with those magnitudes clamped to FLT_MAX (one reduction) and only
+// the non-finite values' own placement (the lo plane) matters.
+__device__ __forceinline__ int split_row_h2_half(const float (&v)[4], uint2& ph, uint2& pl) {
+  const uint32_t raw = max(max(abs_bits(v[0]), abs_bits(v[1])), max(abs_bits(v[2]), abs_bits(v[3])));
+  const int sh = h2_shift(half_max_u32(min(raw, 0x7f7fffffu)));
+  uint32_t h0, l0, h1, l1;
+  if (raw < 0x7f800000u) {
+    split2h_pair(v[0], v[1], sh, h0, l0);
+    split2h_pair(v[2], v[3], sh, h1, l1);
+  } else {
+    split2h_pair_nf(v[0], v[1], sh, h0, l0);
+    split2h_pair_nf(v[2], v[3], sh, h1, l1);
+  }
+  ph = make_uint2(h0, h1);
+  pl = make_uint2(l0, l1);
+  return -sh;
 }
 
 }  // namespace kgx

@@ -29,6 +29,7 @@
 #include <type_traits>
 
 #include "kgx_bf16x3.h"
+#include "kgx_f16x2.h"
 #include "kgx_internal.h"
 #include "kgx_vec.h"
 
@@ -49,6 +50,18 @@ constexpr int kThreads = kGroups * 32;
 #endif
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// The transform's operand split (main, short-row and tiny-row kernels alike,
+// so their outputs stay bit-identical to each other): 2 = f16x2 (two fp16
+// planes with power-of-two row / column scales, three MFMAs per k-step, W's
+// fragments in 32 VGPRs; kgx_f16x2.h), 3 = bf16x3 (three bf16 planes, six
+// MFMAs, 48 VGPRs; kgx_bf16x3.h).
+#ifndef KGX_FUSED_SPLIT
+#define KGX_FUSED_SPLIT 3
+#endif
+constexpr bool kFH2 = KGX_FUSED_SPLIT == 2;
+constexpr int kFPlanes = kFH2 ? 2 : 3;
+static_assert(!kFH2 || (KGX_FUSED_BF16X3 && KGX_FUSED_TSTORE), "the f16x2 split replaces the bf16x3 transform");
 
 struct FusedArgs {
   const int32_t* rowptr;
@@ -117,6 +130,124 @@ __device__ __forceinline__ void lds_barrier() {
 typedef short bf16x8_t __attribute__((ext_vector_type(8)));
 typedef short bf16x4_t __attribute__((ext_vector_type(4)));
 
+// W's split B-fragments for this lane's output column n_col: k-step s (0..3)
+// of lane group q covers k = 32 q + 8 s + j (j = 0..7), so each A fragment is
+// 8 contiguous elements of a tile row (one ds_read_b128).  bf16x3: hi / mid /
+// lo planes; f16x2: hi in wfh, lo in wfl (wfm unused), the column scaled by
+// its own power of two (the max over its four lane groups); returns the
+// column's unscale exponent (0 for bf16x3).
+template <bool NARROW, typename Args>
+__device__ __forceinline__ int load_w128(const Args& a, bool w_ok, int n_col, int q, bf16x8_t (&wfh)[4],
+                                         bf16x8_t (&wfm)[4], bf16x8_t (&wfl)[4]) {
+  auto wv = [&](int k) { return w_ok && (!NARROW || k < a.F_in) ? a.W[int64_t(k) * a.F_out + n_col] : 0.0f; };
+  int sh = 0;
+  if constexpr (kFH2) {
+    uint32_t m = 0;
+    for (int k = 32 * q; k < 32 * q + 32; ++k) {
+      const uint32_t b = abs_bits(wv(k));
+      m = max(m, b < 0x7f800000u ? b : 0u);
+    }
+    m = max(m, uint32_t(__shfl_xor(int(m), 16)));
+    m = max(m, uint32_t(__shfl_xor(int(m), 32)));
+    sh = h2_shift(m);
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+    u32x4_t ph, pm, pl;
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const float v0 = wv(32 * q + 8 * s + j), v1 = wv(32 * q + 8 * s + j + 1);
+      uint32_t h, m_ = 0, l;
+      if constexpr (kFH2)
+        split2h_pair(v0, v1, sh, h, l);
+      else
+        split3_pair(v0, v1, h, m_, l);
+      ph[j / 2] = h;
+      pm[j / 2] = m_;
+      pl[j / 2] = l;
+    }
+    wfh[s] = __builtin_bit_cast(bf16x8_t, ph);
+    wfm[s] = __builtin_bit_cast(bf16x8_t, pm);
+    wfl[s] = __builtin_bit_cast(bf16x8_t, pl);
+  }
+  return -sh;
+}
+
+// One k-step of a 16-row block on one accumulator: D^T += W^T x^T with the
+// split's products, small terms first (the tile's planes: bf16x3 hi / mid / lo,
+// f16x2 hi / lo in ah / am)
+__device__ __forceinline__ f32x4 kstep_t(const bf16x8_t& wh, const bf16x8_t& wm, const bf16x8_t& wl,
+                                         const bf16x8_t& ah, const bf16x8_t& am, const bf16x8_t& al, f32x4 d) {
+  if constexpr (kFH2) {
+    const kgx_h8_t Wh = __builtin_bit_cast(kgx_h8_t, wh), Wl = __builtin_bit_cast(kgx_h8_t, wl);
+    const kgx_h8_t Xh = __builtin_bit_cast(kgx_h8_t, ah), Xl = __builtin_bit_cast(kgx_h8_t, am);
+    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(Wh, Xl, d, 0, 0, 0);
+    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(Wl, Xh, d, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(Wh, Xh, d, 0, 0, 0);
+  }
+  d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, al, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, ah, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, am, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, am, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, ah, d, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, ah, d, 0, 0, 0);
+}
+
+// f16x2, D = x W (the out-tile epilogues): kstep_t's products with the
+// operands swapped, same order -- the same bits, transposed
+__device__ __forceinline__ f32x4 kstep_n(const bf16x8_t& wh, const bf16x8_t& wl, const bf16x8_t& ah,
+                                         const bf16x8_t& al, f32x4 d) {
+  const kgx_h8_t Wh = __builtin_bit_cast(kgx_h8_t, wh), Wl = __builtin_bit_cast(kgx_h8_t, wl);
+  const kgx_h8_t Xh = __builtin_bit_cast(kgx_h8_t, ah), Xl = __builtin_bit_cast(kgx_h8_t, al);
+  d = __builtin_amdgcn_mfma_f32_16x16x32_f16(Xl, Wh, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x32_f16(Xh, Wl, d, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(Xh, Wh, d, 0, 0, 0);
+}
+
+// A tile row's split planes from this lane's four values (every lane of the
+// wave calls this together: the f16x2 scale is its 32-lane group's maximum);
+// returns the row's unscale exponent (0 for bf16x3).  bf16x3: the fast split,
+// or split3_a_lo (non-finite values to the lo plane) when the lane holds one.
+__device__ __forceinline__ int split_row128(const float (&v)[4], bf16x4_t& ph, bf16x4_t& pm, bf16x4_t& pl) {
+  if constexpr (kFH2) {
+    uint2 h, l;
+    const int ue = split_row_h2_half(v, h, l);
+    ph = __builtin_bit_cast(bf16x4_t, h);
+    pm = __builtin_bit_cast(bf16x4_t, l);
+    return ue;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    short h, m_, l;
+    split3_a(v[k], h, m_, l);
+    ph[k] = h;
+    pm[k] = m_;
+    pl[k] = l;
+  }
+  // inf / NaN in this lane's values (their sum is then non-finite): move them
+  // to the lo plane (split3_a_lo) -- a rare branch instead of two selects per
+  // value on every row
+  if (!split_fast_ok(v[0], v[1], v[2], v[3])) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      short h, m_, l;
+      split3_a_lo(v[k], h, m_, l);
+      ph[k] = h;
+      pm[k] = m_;
+      pl[k] = l;
+    }
+  }
+  return 0;
+}
+
+// accumulator value -> output value before the bias: f16x2 undoes the row's
+// and the column's scales (exact power-of-two ldexp)
+__device__ __forceinline__ float unscale(float d, int e) {
+  if constexpr (kFH2) return __builtin_ldexpf(d, e);
+  return d;
+}
+
 #ifndef KGX_FUSED_QUAD_IDX
 #define KGX_FUSED_QUAD_IDX 0
 #endif
@@ -178,7 +309,9 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
   constexpr int PF = 4;  // rows prefetched per group for the next tile (live across the MFMA phase)
 #endif
 #if KGX_FUSED_BF16X3
-  __shared__ short tile3[3][kGroups][kFin + 8];  // hi / mid / lo planes of the aggregated rows
+  __shared__ __attribute__((aligned(16))) short tile3[kFPlanes][kGroups][kFin + 8];  // split planes of the aggregated rows
+  __shared__ int32_t tile_ue[kGroups];                        // f16x2: the rows' unscale exponents
+  __shared__ __attribute__((aligned(16))) int ucol[kFin];     // f16x2: W columns' unscale exponents
 #else
   __shared__ float tile[kGroups][kTileLd];
 #endif
@@ -204,26 +337,10 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
 
   // W fragment for this wave's 16 columns, K permuted: k = 32 q + s.
 #if KGX_FUSED_BF16X3
-  // B fragments: k-step s (0..3) of lane group q covers k = 32 q + 8 s + j (j = 0..7),
-  // so each A fragment is 8 contiguous bf16 of a tile row (one ds_read_b128).
   bf16x8_t wfh[4], wfm[4], wfl[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-    u32x4_t ph, pm, pl;
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-      const float v0 = w_ok && (!NARROW || 32 * q + 8 * s + j < a.F_in) ? a.W[int64_t(32 * q + 8 * s + j) * a.F_out + n_col] : 0.0f;
-      const float v1 = w_ok && (!NARROW || 32 * q + 8 * s + j + 1 < a.F_in) ? a.W[int64_t(32 * q + 8 * s + j + 1) * a.F_out + n_col] : 0.0f;
-      uint32_t h, m_, l;
-      split3_pair(v0, v1, h, m_, l);
-      ph[j / 2] = h;
-      pm[j / 2] = m_;
-      pl[j / 2] = l;
-    }
-    wfh[s] = __builtin_bit_cast(bf16x8_t, ph);
-    wfm[s] = __builtin_bit_cast(bf16x8_t, pm);
-    wfl[s] = __builtin_bit_cast(bf16x8_t, pl);
+  {
+    const int uc = load_w128<NARROW>(a, w_ok, n_col, q, wfh, wfm, wfl);
+    if (kFH2 && q == 0) ucol[n_col] = uc;  // first read after the tile barrier
   }
 #else
   float wb[32];
@@ -356,30 +473,11 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
 #if KGX_FUSED_BF16X3
     {
       bf16x4_t ph, pm, pl;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        short h, m_, l;
-        split3_a(r[k], h, m_, l);
-        ph[k] = h;
-        pm[k] = m_;
-        pl[k] = l;
-      }
-      // inf / NaN in this lane's values (their sum is then non-finite): move
-      // them to the lo plane (split3_a_lo) -- a rare branch instead of two
-      // selects per value on every row
-      if (!split_fast_ok(r[0], r[1], r[2], r[3])) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          short h, m_, l;
-          split3_a_lo(r[k], h, m_, l);
-          ph[k] = h;
-          pm[k] = m_;
-          pl[k] = l;
-        }
-      }
+      const int ue = split_row128(r, ph, pm, pl);
       *reinterpret_cast<bf16x4_t*>(&tile3[0][g][f]) = ph;
       *reinterpret_cast<bf16x4_t*>(&tile3[1][g][f]) = pm;
-      *reinterpret_cast<bf16x4_t*>(&tile3[2][g][f]) = pl;
+      if constexpr (!kFH2) *reinterpret_cast<bf16x4_t*>(&tile3[kFPlanes - 1][g][f]) = pl;
+      if (kFH2 && lane == 0) tile_ue[g] = ue;
     }
 #else
     *reinterpret_cast<float4*>(&tile[g][f]) = make_float4(r[0], r[1], r[2], r[3]);
@@ -398,7 +496,14 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
       for (int s4 = 0; s4 < 4; ++s4) {
         const bf16x8_t ah = *reinterpret_cast<const bf16x8_t*>(&tile3[0][m][32 * q + 8 * s4]);
         const bf16x8_t am = *reinterpret_cast<const bf16x8_t*>(&tile3[1][m][32 * q + 8 * s4]);
-        const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(&tile3[2][m][32 * q + 8 * s4]);
+        if constexpr (kFH2) {  // three products, alternating between the two chains by k-step
+          if (s4 & 1)
+            d1 = kstep_t(wfh[s4], wfm[s4], wfl[s4], ah, am, am, d1);
+          else
+            d0 = kstep_t(wfh[s4], wfm[s4], wfl[s4], ah, am, am, d0);
+          continue;
+        }
+        const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(&tile3[kFPlanes - 1][m][32 * q + 8 * s4]);
         // small terms first
 #if KGX_FUSED_TSTORE  // D^T = W^T x^T (same products and k order)
         d1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[s4], al, d1, 0, 0, 0);
@@ -433,8 +538,10 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
       if (rr >= 0 && (!NARROW || c4 < a.F_out) && !(a.debug & 2)) {
         float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + c4);
         const float4 b4 = *reinterpret_cast<const float4*>(&sbias[c4]);
-        float4 v = make_float4((d0[0] + d1[0]) + b4.x, (d0[1] + d1[1]) + b4.y, (d0[2] + d1[2]) + b4.z,
-                               (d0[3] + d1[3]) + b4.w);
+        const int ue = kFH2 ? tile_ue[m] : 0;
+        const int4 uc = kFH2 ? *reinterpret_cast<const int4*>(&ucol[c4]) : make_int4(0, 0, 0, 0);
+        float4 v = make_float4(unscale(d0[0] + d1[0], ue + uc.x) + b4.x, unscale(d0[1] + d1[1], ue + uc.y) + b4.y,
+                               unscale(d0[2] + d1[2], ue + uc.z) + b4.z, unscale(d0[3] + d1[3], ue + uc.w) + b4.w);
         if (a.accumulate) {
           const float4 p = *dst;
           v = make_float4(__fadd_rn(p.x, v.x), __fadd_rn(p.y, v.y), __fadd_rn(p.z, v.z), __fadd_rn(p.w, v.w));
@@ -497,8 +604,10 @@ template <int RED, bool WEIGHTED, bool TWO, bool NARROW>
 __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs a) {  // 4 waves per SIMD: two blocks per CU
   using R = Red<RED>;
   // split planes of the 64 aggregated rows; after the MFMAs the same bytes hold the f32 results
-  __shared__ __attribute__((aligned(16))) short tile3[3][kShortRows][kFin + 8];
+  __shared__ __attribute__((aligned(16))) short tile3[kFPlanes][kShortRows][kFin + 8];
   __shared__ int32_t tile_row[kShortRows];
+  __shared__ __attribute__((aligned(16))) int32_t tile_ue[kShortRows];  // f16x2: the rows' unscale exponents
+  __shared__ __attribute__((aligned(16))) int ucol[kFin];               // f16x2: W columns' unscale exponents
 #if KGX_SHORT_TSTORE
   __shared__ __attribute__((aligned(16))) float sbias[kFin];  // read at the stores
 #else
@@ -520,24 +629,8 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
   const bool w_ok = mfma_wave && (!NARROW || n_col < a.F_out);  // W rows k >= F_in and columns >= F_out load as 0
 
   bf16x8_t wfh[4], wfm[4], wfl[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-    u32x4_t ph, pm, pl;
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-      const float v0 = w_ok && (!NARROW || 32 * q + 8 * s + j < a.F_in) ? a.W[int64_t(32 * q + 8 * s + j) * a.F_out + n_col] : 0.0f;
-      const float v1 = w_ok && (!NARROW || 32 * q + 8 * s + j + 1 < a.F_in) ? a.W[int64_t(32 * q + 8 * s + j + 1) * a.F_out + n_col] : 0.0f;
-      uint32_t h, m_, l;
-      split3_pair(v0, v1, h, m_, l);
-      ph[j / 2] = h;
-      pm[j / 2] = m_;
-      pl[j / 2] = l;
-    }
-    wfh[s] = __builtin_bit_cast(bf16x8_t, ph);
-    wfm[s] = __builtin_bit_cast(bf16x8_t, pm);
-    wfl[s] = __builtin_bit_cast(bf16x8_t, pl);
-  }
+  const int uc_n = load_w128<NARROW>(a, w_ok, n_col, q, wfh, wfm, wfl);  // this lane's column's unscale exponent
+  if (kFH2 && q == 0) ucol[n_col] = uc_n;  // first read after two barriers
 #if KGX_SHORT_TSTORE
   const int c4 = wave * 16 + 4 * q;
   if (tid < kFin) sbias[tid] = (a.bias && tid < a.F_out) ? a.bias[tid] : 0.0f;  // first read after two barriers
@@ -638,29 +731,15 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
         for (int k = 0; k < 4; ++k) v[k] = f_ok ? v[k] : 0.0f;
       }
       bf16x4_t ph, pm, pl;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        short h, m_, l;
-        split3_a(v[k], h, m_, l);
-        ph[k] = h;
-        pm[k] = m_;
-        pl[k] = l;
-      }
-      if (!split_fast_ok(v[0], v[1], v[2], v[3])) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          short h, m_, l;
-          split3_a_lo(v[k], h, m_, l);
-          ph[k] = h;
-          pm[k] = m_;
-          pl[k] = l;
-        }
-      }
+      const int ue = split_row128(v, ph, pm, pl);
       const int tr = g + kGroups * r;
       *reinterpret_cast<bf16x4_t*>(&tile3[0][tr][f]) = ph;
       *reinterpret_cast<bf16x4_t*>(&tile3[1][tr][f]) = pm;
-      *reinterpret_cast<bf16x4_t*>(&tile3[2][tr][f]) = pl;
-      if (lane == 0) tile_row[tr] = row[r];
+      if constexpr (!kFH2) *reinterpret_cast<bf16x4_t*>(&tile3[kFPlanes - 1][tr][f]) = pl;
+      if (lane == 0) {
+        tile_row[tr] = row[r];
+        if constexpr (kFH2) tile_ue[tr] = ue;
+      }
     }
     lds_barrier();
     f32x4 d[kRPG];
@@ -675,7 +754,12 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
           const int tr = 16 * rb + m;
           const bf16x8_t ah = *reinterpret_cast<const bf16x8_t*>(&tile3[0][tr][32 * q + 8 * s4]);
           const bf16x8_t am = *reinterpret_cast<const bf16x8_t*>(&tile3[1][tr][32 * q + 8 * s4]);
-          const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(&tile3[2][tr][32 * q + 8 * s4]);
+          if constexpr (kFH2) {  // the tiny kernel's products in its order (bit-identical rows)
+            d[rb] = KGX_SHORT_TSTORE ? kstep_t(wfh[s4], wfm[s4], wfl[s4], ah, am, am, d[rb])
+                                     : kstep_n(wfh[s4], wfl[s4], ah, am, d[rb]);
+            continue;
+          }
+          const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(&tile3[kFPlanes - 1][tr][32 * q + 8 * s4]);
 #if KGX_SHORT_TSTORE  // D^T = W^T x^T (same products and k order): lane (m, q) gets 4 adjacent columns of row m
           d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[s4], al, d[rb], 0, 0, 0);
           d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfl[s4], ah, d[rb], 0, 0, 0);
@@ -705,7 +789,10 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
         if (rr >= 0 && (!NARROW || c4 < a.F_out)) {
           float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + c4);
           const float4 b4 = *reinterpret_cast<const float4*>(&sbias[c4]);
-          float4 v = make_float4(d[rb][0] + b4.x, d[rb][1] + b4.y, d[rb][2] + b4.z, d[rb][3] + b4.w);
+          const int ue = kFH2 ? tile_ue[16 * rb + m] : 0;
+          const int4 uc = kFH2 ? *reinterpret_cast<const int4*>(&ucol[c4]) : make_int4(0, 0, 0, 0);
+          float4 v = make_float4(unscale(d[rb][0], ue + uc.x) + b4.x, unscale(d[rb][1], ue + uc.y) + b4.y,
+                                 unscale(d[rb][2], ue + uc.z) + b4.z, unscale(d[rb][3], ue + uc.w) + b4.w);
           if (a.accumulate) {
             const float4 p = *dst;
             v = make_float4(__fadd_rn(p.x, v.x), __fadd_rn(p.y, v.y), __fadd_rn(p.z, v.z), __fadd_rn(p.w, v.w));
@@ -719,9 +806,12 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
     lds_barrier();  // every wave has read the planes: their bytes now take the f32 results
     if (mfma_wave) {
 #pragma unroll
-      for (int rb = 0; rb < kRPG; ++rb)
+      for (int rb = 0; rb < kRPG; ++rb) {
+        const int4 ue = kFH2 ? *reinterpret_cast<const int4*>(&tile_ue[16 * rb + 4 * q]) : make_int4(0, 0, 0, 0);
+        const int uej[4] = {ue.x, ue.y, ue.z, ue.w};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) otile[16 * rb + 4 * q + j][n_col] = d[rb][j] + bcol;
+        for (int j = 0; j < 4; ++j) otile[16 * rb + 4 * q + j][n_col] = unscale(d[rb][j], uej[j] + uc_n) + bcol;
+      }
     }
     lds_barrier();
     if (!(a.debug & 2)) {
@@ -789,8 +879,10 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
   using R = Red<RED>;
   constexpr int kTinyRPG = NG == 1 ? KGX_TINY_RPG1 : KGX_TINY_RPG;  // rows per group per tile
   constexpr int kTinyRows = kTinyGroups * kTinyRPG;
-  __shared__ __attribute__((aligned(16))) short planes[2][3][kTinyRows][kFin + 8];
+  __shared__ __attribute__((aligned(16))) short planes[2][kFPlanes][kTinyRows][kFin + 8];
   __shared__ int32_t trow[2][kTinyRows];
+  __shared__ int32_t tue[2][kTinyRows];                   // f16x2: the rows' unscale exponents
+  __shared__ __attribute__((aligned(16))) int ucol[kFin];  // f16x2: W columns' unscale exponents
 #if KGX_TINY_TSTORE
   __shared__ __attribute__((aligned(16))) float sbias[kFin];  // read at the stores
   if (threadIdx.x < kFin)  // first read after a hand-off barrier
@@ -808,23 +900,9 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
     const bool mfma_wave = wave * 16 < a.F_out;
     const bool w_ok = mfma_wave && (!NARROW || n_col < a.F_out);
     bf16x8_t wfh[4], wfm[4], wfl[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-      u32x4_t ph, pm, pl;
-#pragma unroll
-      for (int j = 0; j < 8; j += 2) {
-        const float v0 = w_ok && (!NARROW || 32 * q + 8 * s + j < a.F_in) ? a.W[int64_t(32 * q + 8 * s + j) * a.F_out + n_col] : 0.0f;
-        const float v1 = w_ok && (!NARROW || 32 * q + 8 * s + j + 1 < a.F_in) ? a.W[int64_t(32 * q + 8 * s + j + 1) * a.F_out + n_col] : 0.0f;
-        uint32_t h, m_, l;
-        split3_pair(v0, v1, h, m_, l);
-        ph[j / 2] = h;
-        pm[j / 2] = m_;
-        pl[j / 2] = l;
-      }
-      wfh[s] = __builtin_bit_cast(bf16x8_t, ph);
-      wfm[s] = __builtin_bit_cast(bf16x8_t, pm);
-      wfl[s] = __builtin_bit_cast(bf16x8_t, pl);
+    {
+      const int uc = load_w128<NARROW>(a, w_ok, n_col, q, wfh, wfm, wfl);
+      if (kFH2 && q == 0) ucol[n_col] = uc;  // first read after a hand-off barrier
     }
 #if KGX_TINY_TSTORE
     const int c4 = wave * 16 + 4 * q;
@@ -860,7 +938,11 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
             const int tr = 16 * rb + m;
             const bf16x8_t ah = *reinterpret_cast<const bf16x8_t*>(&planes[b][0][tr][32 * q + 8 * s4]);
             const bf16x8_t am = *reinterpret_cast<const bf16x8_t*>(&planes[b][1][tr][32 * q + 8 * s4]);
-            const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(&planes[b][2][tr][32 * q + 8 * s4]);
+            if constexpr (kFH2) {
+              d[rb] = kstep_t(wfh[s4], wfm[s4], wfl[s4], ah, am, am, d[rb]);
+              continue;
+            }
+            const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(&planes[b][kFPlanes - 1][tr][32 * q + 8 * s4]);
 #if KGX_TINY_TSTORE  // D^T = W^T x^T: same products, same k order, lane (m, q) gets 4 adjacent columns of row m
             d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[s4], al, d[rb], 0, 0, 0);
             d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfl[s4], ah, d[rb], 0, 0, 0);
@@ -893,7 +975,10 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
           if (rr >= 0 && (!NARROW || c4 < a.F_out)) {
             float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + c4);
             const float4 b4 = *reinterpret_cast<const float4*>(&sbias[c4]);
-            float4 v = make_float4(d[rb][0] + b4.x, d[rb][1] + b4.y, d[rb][2] + b4.z, d[rb][3] + b4.w);
+            const int ue = kFH2 ? tue[b][16 * rb + m] : 0;
+            const int4 uc = kFH2 ? *reinterpret_cast<const int4*>(&ucol[c4]) : make_int4(0, 0, 0, 0);
+            float4 v = make_float4(unscale(d[rb][0], ue + uc.x) + b4.x, unscale(d[rb][1], ue + uc.y) + b4.y,
+                                   unscale(d[rb][2], ue + uc.z) + b4.z, unscale(d[rb][3], ue + uc.w) + b4.w);
             if (a.accumulate) {
 #if KGX_TINY_ACC_EARLY
               const float4 p = pacc[rb];
@@ -992,29 +1077,15 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
         for (int k = 0; k < 4; ++k) o[k] = f_ok ? o[k] : 0.0f;
       }
       bf16x4_t ph, pm, pl;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        short h, m_, l;
-        split3_a(o[k], h, m_, l);
-        ph[k] = h;
-        pm[k] = m_;
-        pl[k] = l;
-      }
-      if (!split_fast_ok(o[0], o[1], o[2], o[3])) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          short h, m_, l;
-          split3_a_lo(o[k], h, m_, l);
-          ph[k] = h;
-          pm[k] = m_;
-          pl[k] = l;
-        }
-      }
+      const int ue = split_row128(o, ph, pm, pl);
       const int tr = g + kTinyGroups * j;
       *reinterpret_cast<bf16x4_t*>(&planes[b][0][tr][f]) = ph;
       *reinterpret_cast<bf16x4_t*>(&planes[b][1][tr][f]) = pm;
-      *reinterpret_cast<bf16x4_t*>(&planes[b][2][tr][f]) = pl;
-      if (lane == 0) trow[b][tr] = row;
+      if constexpr (!kFH2) *reinterpret_cast<bf16x4_t*>(&planes[b][kFPlanes - 1][tr][f]) = pl;
+      if (lane == 0) {
+        trow[b][tr] = row;
+        if constexpr (kFH2) tue[b][tr] = ue;
+      }
     }
   };
   // Pipeline, at iteration i: issue tile i+2's records, issue tile i+1's row

@@ -50,7 +50,7 @@ constexpr int kSteps = kF / 32;    // k-steps of 32 per MFMA chain
 // registers; kgx_f16x2.h), 3 = bf16x3 (three bf16 planes, six MFMAs per k-step,
 // W's lo plane in LDS; kgx_bf16x3.h).
 #ifndef KGX_F256_SPLIT
-#define KGX_F256_SPLIT 2
+#define KGX_F256_SPLIT 3
 #endif
 constexpr bool kH2 = KGX_F256_SPLIT == 2;
 constexpr int kPlanes = kH2 ? 2 : 3;  // activation planes per tile row
