@@ -313,6 +313,7 @@ def main() -> None:
     dev = torch.device("cuda", gpu)
     comm = None
     if world > 1:
+        os.environ.setdefault("KGX_LOG", "1")  # the sharded layers' progress (exchange tuner) on stderr
         if rehearsal:
             dist.init_process_group("gloo")
             from keras_geometric_amd.distributed import HostStagedComm
@@ -359,6 +360,7 @@ def main() -> None:
         log(f"world={world}: generating shards of R-MAT N={n_global} E={e_global}")
         t0 = time.perf_counter()
         sg, x, layer = _build_sharded(kind, n_global, e_global, f_in, f_out, args.seed, args.exact, dev, comm)
+        log(f"shard graph built in {time.perf_counter() - t0:.1f} s; first forward (plans, exchange tuner)")
         with torch.no_grad():
             layer(x)  # build, plans, and (GCN) the halo chunk count measured at the first forward
         torch.cuda.synchronize()

@@ -181,6 +181,15 @@ def _inference_only(layer: Layer, weights) -> None:
             "training runs on the single-GPU layers")
 
 
+def _progress(sg, msg: str) -> None:
+    """One progress line on stderr from rank 0 when KGX_LOG is set (bench.py
+    sets it for N > 1: long first forwards -- the exchange tuner -- stay visible)."""
+    if os.environ.get("KGX_LOG") and sg.rank == 0:
+        import sys
+
+        print(f"[kgx] {msg}", file=sys.stderr, flush=True)
+
+
 def equal_bounds(n_global: int, world: int) -> list[int]:
     base, rem = divmod(n_global, world)
     b = [0]
@@ -714,6 +723,8 @@ class ShardedGraph:
             mx = every.view(self.world, 2).max(0).values.cpu()
             worst.append(float(mx[0]))
             spent += float(mx[1])
+            _progress(self, f"tune {kind}:{K}:{unit} {1e3 * worst[-1]:.2f} ms (agreed; {spent:.1f} s spent, "
+                            f"{len(worst)}/{len(candidates)})")
         i = min(range(len(worst)), key=worst.__getitem__)
         self.exchange, self.halo_k, self.merge_unit = candidates[i]
         self.tuning = {f"{kind}:{K}:{unit}": v for (kind, K, unit), v in zip(candidates, worst)}

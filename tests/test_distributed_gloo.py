@@ -298,7 +298,7 @@ def _worker(rank, world, chunks, port, q):
 
 
 @pytest.mark.timeout(180)
-@pytest.mark.parametrize("world,chunks", [(2, 1), (2, 4), (3, 3)])
+@pytest.mark.parametrize("world,chunks", [(2, 1), (2, 4), (3, 3), (8, 2)])
 def test_sharded_equals_unsharded_bitwise(world, chunks):
     """EXACT table path bit-identical to the unsharded graph for any halo
     chunking (the chunk-major halo table only renames source rows), and the
