@@ -48,7 +48,7 @@ METRIC = "aggregated edges/sec + achieved HBM GB/s, GCNConv fwd, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 
 # name: (layer, nodes, edges, F_in, F_out, scaling); weak: nodes/edges per GPU, strong: the whole graph
-CONFIGS = {
+CONFIGS = {  # name: (layer, nodes, edges, F_in, F_out, scaling); "tiny" is a control-flow size, not a BASELINE config
     "ns": ("gcn", 10_000_000, 100_000_000, 128, 128, "weak"),
     "c2": ("gcn", 1_000_000, 10_000_000, 128, 128, "weak"),
     "tiny": ("gcn", 100_000, 1_000_000, 128, 128, "weak"),
@@ -251,6 +251,7 @@ def shard_summary(sg, kind: str, f_in: int, f_out: int, exact: bool) -> dict:
     group as torch.distributed reports it (backend, world size), the exchange
     the tuner chose (kind, K, merge unit) with every candidate's agreed time and
     the tuner's own wall time, and the halo sizes."""
+    from keras_geometric_amd import distributed as kd
     from keras_geometric_amd import ops as kops
 
     world = sg.world
@@ -271,7 +272,9 @@ def shard_summary(sg, kind: str, f_in: int, f_out: int, exact: bool) -> dict:
             "halo_rows_pushed_partials": pp.n_push if pp is not None else 0,
             "halo_MB_per_layer": n_moved * f_x * 4 / 1e6,
             "halo_chunks": sg.halo_k if sg.halo_k is not None else (len(pp.chunks) if pp else len(sg.chunks)),
-            "merge_unit": sg.merge_unit,
+            # the tuner's unit, or (tuning skipped: K fixed) the one the merged passes use
+            "merge_unit": sg.merge_unit or (os.environ.get("KGX_HALO_MERGE", "step")
+                                            if pp is not None and kd.use_merged_halo() else None),
             "exchange_tuning_s": sg.tuning,
             "exchange_tuning_total_s": sg.tuning_s,
             "exchange_tuning_skipped": sg.tuning_skipped}
@@ -373,6 +376,8 @@ def main() -> None:
 
         shard_info = shard_summary(sg, kind, f_in, f_out, args.exact)
 
+    if world > 1:
+        log(f"first forward done ({first_call_ms / 1e3:.1f} s since the shard build began); warmup")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()

@@ -476,6 +476,7 @@ class ShardedGraph:
         if ("halo", K, weighted) in self._pp_by_k:
             self._pp = self._pp_by_k[("halo", K, weighted)]
             return self._pp
+        _progress(self, f"push-pull plan: K {K}, weighted {weighted}")
         g, comm, world, lo, n_local = self.graph, self.comm, self.world, self.lo, self.n_local
         dev = g.col.device
         rows = torch.repeat_interleave(torch.arange(g.n_dst, device=dev), g.deg.long())
@@ -699,6 +700,7 @@ class ShardedGraph:
         dev = self.graph.col.device
         budget = float(os.environ.get("KGX_TUNE_BUDGET_S", "60"))
         worst, spent, t_start = [], 0.0, time.perf_counter()
+        _progress(self, f"tune: {len(candidates)} exchange candidates, budget {budget:.0f} s")
         for kind, K, unit in candidates:
             if spent > budget:  # every rank sees the same agreed times, so all stop at the same candidate
                 worst.append(float("inf"))
@@ -707,6 +709,7 @@ class ShardedGraph:
             t_plan = time.perf_counter()
             self.exchange_plan(K)
             best, total = float("inf"), time.perf_counter() - t_plan
+            _progress(self, f"tune {kind}:{K}:{unit}: plan {total:.1f} s")
             for _ in range(2):
                 if dev.type == "cuda":
                     torch.cuda.synchronize(dev)
