@@ -22,7 +22,13 @@ Provenance / pinning
   tests/test_graphsage_conv.py:465-514) — see tests/test_oracle_pins.py — and
   by cross-checks against plain sequential numpy loops (oracle/sequential.py).
 * PyTorch-Geometric comparisons in the reference tests need torch_geometric,
-  which is not installed; they pin nothing here.
+  which is not installed.  The algorithms they compare against (PyG >= 2.6.1,
+  reference pyproject.toml:51: gcn_norm + GCNConv, GATv2Conv, GINConv) are
+  restated in float64 numpy in oracle/pyg_restated.py, and
+  tests/test_oracle_pyg_pins.py holds the oracle to them at those tests'
+  tolerances -- this pins the GCN normalisation (utils/main.py:20-33) and the
+  GATv2 segment softmax (gatv2_conv.py:268-311), which no reference-held
+  vector covers.
 """
 
 ORACLE_IS_TEST_INFRASTRUCTURE = True
