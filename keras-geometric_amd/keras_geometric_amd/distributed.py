@@ -255,7 +255,7 @@ class PushPullPlan:
     recv_graph: object = None  # receiver CSR over all halo rows (sources = halo buffer rows)
     step_parts: list | None = None  # receiver CSR per exchange step, in issue order (accumulate-only)
     weighted: bool = True  # receiver edges carry the GCN norms (else weight 1, plain partial sums)
-    kind: str = "halo"  # "halo" (push-pull all-to-all) or "allgather" (every rank's rows, chunked)
+    kind: str = "halo"  # "halo" (push-pull all-to-all), "pull" (the same all-to-all, pulled rows only) or "allgather" (every rank's rows, chunked)
     merged: dict | None = None  # unit -> (own pass, first-group pass, later groups, first wait): merged_passes
 
 
@@ -334,7 +334,7 @@ class ShardedGraph:
     chunks_fixed: bool = False  # K given (halo_chunks= or KGX_HALO_CHUNKS): no tuning
     halo_k: int | None = None  # exchange chunk count chosen by tune_exchange (or fixed)
     tuning: dict | None = None  # K (or "exchange:K") -> slowest rank's forward seconds
-    exchange: str | None = None  # "halo" / "allgather"; None: not chosen yet (push-pull halo until tuned)
+    exchange: str | None = None  # "halo" / "pull" / "allgather"; None: not chosen yet (push-pull halo until tuned)
     merge_unit: str | None = None  # merged_passes' unit ("step" / "chunk" / "none"); None: KGX_HALO_MERGE or "step"
     tuning_s: float | None = None  # wall time tune_exchange took on this rank
     tuning_skipped: int = 0  # candidates left untimed once KGX_TUNE_BUDGET_S was spent
@@ -443,7 +443,8 @@ class ShardedGraph:
             return self.backend.gather_rows(x_local, c.send_rows)
         return x_local.new_empty((0, x_local.shape[1]))
 
-    def push_pull_plan(self, n_chunks: int | None = None, weighted: bool | None = None) -> PushPullPlan:
+    def push_pull_plan(self, n_chunks: int | None = None, weighted: bool | None = None,
+                       pull_only: bool = False) -> PushPullPlan:
         """A smaller halo for the weighted-sum (GCN) path.  Collective: every
         rank calls it once (ShardedGCNConv does, on its first forward).
 
@@ -465,7 +466,12 @@ class ShardedGraph:
         weighted (default: the graph carries edge weights) says whether the
         receiver's pass multiplies by them: an unweighted plan (GIN / SAGE sums
         on a graph that also has GCN norms) pushes plain partial sums and gives
-        every receiver edge weight 1, so the plans are kept per (K, weighted)."""
+        every receiver edge weight 1, so the plans are kept per (K, weighted).
+
+        pull_only (exchange kind "pull"): every halo edge is served by pulling
+        its source -- more rows on the links, but no partial sums for the
+        owner to compute and write and the receiver to read back; which wins
+        depends on the link rate, so the tuner times both."""
         K = n_chunks or self.halo_k or len(self.chunks)
         if weighted is None:
             weighted = self.graph.w is not None
@@ -473,10 +479,11 @@ class ShardedGraph:
             raise ValueError("push_pull_plan(weighted=True): the shard graph has no edge weights")
         if self._pp_by_k is None:
             self._pp_by_k = {}
-        if ("halo", K, weighted) in self._pp_by_k:
-            self._pp = self._pp_by_k[("halo", K, weighted)]
+        key = ("pull" if pull_only else "halo", K, weighted)
+        if key in self._pp_by_k:
+            self._pp = self._pp_by_k[key]
             return self._pp
-        _progress(self, f"push-pull plan: K {K}, weighted {weighted}")
+        _progress(self, f"{key[0]} plan: K {K}, weighted {weighted}")
         g, comm, world, lo, n_local = self.graph, self.comm, self.world, self.lo, self.n_local
         dev = g.col.device
         rows = torch.repeat_interleave(torch.arange(g.n_dst, device=dev), g.deg.long())
@@ -491,6 +498,8 @@ class ShardedGraph:
         ud, inv_d, cd = torch.unique(torch.bucketize(hs, bt, right=True) * stride + hd, return_inverse=True,
                                      return_counts=True)
         push = cd[inv_d] > cs[inv_s]  # the edge is served from its busier endpoint
+        if pull_only:
+            push = torch.zeros_like(push)
         pulled = torch.zeros(us.numel(), dtype=torch.bool, device=dev)
         pulled[inv_s[~push]] = True
         via_pull = pulled[inv_s]
@@ -593,8 +602,8 @@ class ShardedGraph:
             parts = list(self.backend.split_by_source(rg, [0, 0] + [c.hi for c in chunks])[1:])
             step_parts = list(self.backend.split_by_source(rg, [0, 0] + [st.hi for c in chunks for st in c.steps])[1:])
         self._pp = PushPullPlan(chunks=chunks, parts=parts, n_rows=off, n_pull=rp[-1], n_push=ru[-1], recv_graph=rg,
-                                step_parts=step_parts, weighted=weighted)
-        self._pp_by_k[("halo", K, weighted)] = self._pp
+                                step_parts=step_parts, weighted=weighted, kind=key[0])
+        self._pp_by_k[key] = self._pp
         return self._pp
 
     def allgather_plan(self, n_chunks: int = 1, weighted: bool | None = None) -> PushPullPlan:
@@ -652,9 +661,10 @@ class ShardedGraph:
     def exchange_plan(self, n_chunks: int | None = None, weighted: bool | None = None) -> PushPullPlan:
         """The plan of the chosen exchange ("halo": push-pull all-to-all; "allgather";
         not chosen yet: KGX_EXCHANGE, else the halo)."""
-        if (self.exchange or os.environ.get("KGX_EXCHANGE", "halo")) == "allgather":
+        kind = self.exchange or os.environ.get("KGX_EXCHANGE", "halo")
+        if kind == "allgather":
             return self.allgather_plan(n_chunks or self.halo_k or len(self.chunks), weighted)
-        return self.push_pull_plan(n_chunks, weighted)
+        return self.push_pull_plan(n_chunks, weighted, pull_only=kind == "pull")
 
     def exchange_candidates(self, halo_ks=(1, 2, 4), gather_ks=(1, 2, 4), units=("step", "chunk", "none")) -> list:
         """(exchange, K, merge unit) triples worth timing: the push-pull halo at
@@ -664,12 +674,15 @@ class ShardedGraph:
         graph, skip it without a run).  Collective: the halo size is agreed by
         one all-to-all (its max over ranks), so every rank lists the same
         candidates -- tune_exchange runs their collectives in lock step.
-        KGX_EXCHANGE / KGX_HALO_MERGE restrict the set."""
+        KGX_EXCHANGE (halo / pull / allgather) / KGX_HALO_MERGE restrict the set."""
         fixed = os.environ.get("KGX_EXCHANGE")
         fixed_unit = os.environ.get("KGX_HALO_MERGE")
         units = (fixed_unit,) if fixed_unit else tuple(units)
         # without merged passes the halo path ignores the unit: time each K once
         halo_units = units if use_merged_halo() else ("none",)
+        # the pull-only halo (kind "pull", KGX_EXCHANGE=pull) is not timed: one-rank
+        # simulations at NS weak P=8 put it behind push-pull both with the exchange
+        # free (11.96-12.78 vs 11.16-11.18 ms) and at 400 GB/s (22.5 vs 12.9 ms)
         cands = [("halo", k, u) for k in halo_ks for u in dict.fromkeys(halo_units)]
         n = torch.full((self.world,), self.n_halo, dtype=torch.long, device=self.graph.col.device)
         every = torch.empty_like(n)

@@ -257,6 +257,11 @@ def _worker(rank, world, chunks, port, q):
             with torch.no_grad():
                 ys_gather.append(layer2(torch.from_numpy(x[lo:hi])).numpy())
             assert sg2._pp.kind == "allgather" and len(sg2._pp.chunks) == kk
+        # the pull-only halo through the merged passes (no partial sums pushed)
+        sg2.exchange, sg2.halo_k = "pull", 2
+        with torch.no_grad():
+            y_pullplan = layer2(torch.from_numpy(x[lo:hi])).numpy()
+        assert sg2._pp.kind == "pull" and sg2._pp.n_push == 0 and len(sg2._pp.chunks) == 2
         # shapes the fused kernel does not take: X W first, then the pipelined weighted sum
         sg3 = kd.ShardedGraph.build(torch.from_numpy(s[keep]), torch.from_numpy(d[keep]), bounds,
                                     backend=UnfusedOracleBackend(), n_features=F_OUT, halo_chunks=chunks)
@@ -292,7 +297,7 @@ def _worker(rank, world, chunks, port, q):
         assert torch.equal(y_again, y)
         q.put((rank, gcn.numpy(), mx.numpy(), sg.n_halo, sum(sg.send_counts), y.numpy(), y_pull.numpy(), pp.n_push,
                y_tuned.numpy(), y_unfused.numpy(), y_wide.numpy(), y_unmerged.numpy(), ys_gather[0], ys_gather[1],
-               y_chunk.numpy()))
+               y_chunk.numpy(), y_pullplan))
     finally:
         dist.destroy_process_group()
 
@@ -334,7 +339,7 @@ def test_sharded_equals_unsharded_bitwise(world, chunks):
     # overlapped layer path, push-pull and pull-only halos: own-source part, then
     # one part per halo chunk per row (re-associated sums)
     assert sum(results[r][6] for r in range(world)) > 0  # partial sums were pushed
-    for i in (4, 5, 7, 8, 10, 11, 12, 13):
+    for i in (4, 5, 7, 8, 10, 11, 12, 13, 14):
         y_split = np.concatenate([results[r][i] for r in range(world)])
         err = np.abs(y_split - y) / np.maximum(1, np.abs(y))
         assert err.max() <= 1e-5

@@ -157,7 +157,7 @@ def main():
                          "c5: SAGE-mean 2.45M/123.7M F100 strong")
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--chunks", default="1,2,4,8")
-    ap.add_argument("--exchange", default="halo", help="halo,allgather: exchanges to run")
+    ap.add_argument("--exchange", default="halo", help="halo,pull,allgather: exchanges to run")
     ap.add_argument("--push", default="1", help="KGX_HALO_PUSH values to run (0: pull-only halo)")
     ap.add_argument("--merged", default="1", help="KGX_HALO_MERGED values to run (0: round-2 own pass + chunk passes)")
     ap.add_argument("--merge-unit", default="step", help="KGX_HALO_MERGE values: step, chunk")
