@@ -683,7 +683,8 @@ class ShardedGraph:
         # the pull-only halo (kind "pull", KGX_EXCHANGE=pull) is not timed: one-rank
         # simulations at NS weak P=8 put it behind push-pull both with the exchange
         # free (11.96-12.78 vs 11.16-11.18 ms) and at 400 GB/s (22.5 vs 12.9 ms)
-        cands = [("halo", k, u) for k in halo_ks for u in dict.fromkeys(halo_units)]
+        halo_kind = "pull" if fixed == "pull" else "halo"
+        cands = [(halo_kind, k, u) for k in halo_ks for u in dict.fromkeys(halo_units)]
         n = torch.full((self.world,), self.n_halo, dtype=torch.long, device=self.graph.col.device)
         every = torch.empty_like(n)
         self.comm.all_to_all_single(every, n)

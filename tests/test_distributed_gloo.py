@@ -522,6 +522,11 @@ def _uneven_worker(rank, world, port, q):
             fixed = sg.exchange_candidates()
         finally:
             del os.environ["KGX_EXCHANGE"], os.environ["KGX_HALO_MERGE"]
+        os.environ["KGX_EXCHANGE"] = "pull"
+        try:  # the pull-only halo is not timed by default, but a fixed choice still tunes K and unit
+            assert sg.exchange_candidates() == [("pull", k, u) for k in (1, 2, 4) for u in ("step", "chunk", "none")]
+        finally:
+            del os.environ["KGX_EXCHANGE"]
         layer = kd.ShardedGCNConv(F_OUT, sg)
         layer._build_device = torch.device("cpu")
         layer.build((hi - lo, F_IN))
