@@ -272,8 +272,9 @@ int kgx_spmm_gemm_ex2(int reduce, const int32_t* rowptr, const int32_t* rows, in
  * layers' halo pass reads a row's own-source edges from the layer input and
  * its halo edges from the exchange's receive buffer in ONE pass, so the row is
  * written once instead of written and read-modify-written (distributed.py;
- * gcn_conv.py:233-272 per shard).  x2 NULL: kgx_spmm_gemm_ex2.  Rows indexed
- * by pre_gin are rows of x. */
+ * gcn_conv.py:233-272, gin_conv.py:216-225 per shard).  With x2: sums only
+ * (weighted or not, GIN's pre-scale allowed), F_in 128, F_out % 16 == 0.
+ * x2 NULL: kgx_spmm_gemm_ex2.  Rows indexed by pre_gin are rows of x. */
 int kgx_spmm_gemm_ex3(int reduce, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,
                       const int32_t* items, int64_t n_items, int64_t n_long_items, int64_t n_short_end,
                       const int32_t* tiny_pack, const float* tiny_w, int64_t n_tiny_deg2,

@@ -67,8 +67,13 @@ struct DenseArgs {
   int accumulate;
   int cg_count;  // column groups of 16 WAVES columns (1 or 2)
   int vec_out;   // N, ld_out multiples of 4 and out 16-byte aligned: dwordx4 output stores
-  int pstore;    // experiment KGX_DENSE_PSTORE=1: the producers store the output (vec_out, no accumulate, one operand)
-  int debug;     // experiment builds only (-DKGX_EXPERIMENTS, env KGX_DENSE_DEBUG): 1 skip MFMA, 2 skip stores, 4 skip loads + split
+  // Always 0 in this build.  They are kept as kernel arguments because the
+  // producer pipeline's register allocation, hand-checked on the ISA
+  // (tools/isa_hazard_check.py), is sensitive to the branches they guard:
+  // removing them gave an allocation the checker rejects (a register set
+  // reused while its loads were still in flight).
+  int pstore;
+  int debug;
 };
 
 template <int KS>
@@ -628,7 +633,6 @@ int launch(const DenseArgs& a, hipStream_t s) {
       k = a.K1 > 0 ? dense_kernel<KS, WAVES, false, true, true> : dense_kernel<KS, WAVES, false, false, true>;
   }
 #endif
-  if (a.pstore && a.K1 == 0) k = dense_kernel<KS, WAVES, false, false, false, true>;
   static int cus = 0;
   if (cus == 0) {
     int dev = 0;
@@ -702,20 +706,9 @@ extern "C" int kgx_dense(int64_t M, const float* x0, int64_t ld_x0, int64_t K0, 
   const int K = int(K0 + K1);
   a.cg_count = N <= 128 ? 1 : 2;
   a.vec_out = N % 4 == 0 && ld_out % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0;
-  // producer-side output stores: measured slower (C4 7.7 vs 7.1 ms, NS xW 2.4 vs 2.2):
-  // the producers, not the consumers' stores, bound the kernel; opt-in experiment
-  static const bool pstore_on = [] {
-    const char* h = getenv("KGX_DENSE_PSTORE");
-    return h && atoi(h) != 0;
-  }();
-  a.pstore = a.vec_out && !a.accumulate && pstore_on;
-#ifdef KGX_EXPERIMENTS  // cost-decomposition knob; never in a product build (it changes results)
-  static const int dbg = [] {
-    const char* h = getenv("KGX_DENSE_DEBUG");
-    return h ? atoi(h) : 0;
-  }();
-  a.debug = dbg;
-#endif
+  // a.pstore / a.debug stay 0: the producer-store form (measured slower, C4 7.7
+  // vs 7.1 ms) and the cost-decomposition builds are no longer instantiated
+  // (tools/experiments/round4_variants.patch restores their switches)
   if (N <= 64) return launch_ks<4>(K, a, stream);
   return launch_ks<8>(K, a, stream);
 }

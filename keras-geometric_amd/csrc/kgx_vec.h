@@ -11,6 +11,16 @@ namespace kgx {
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
+// 1 KB of zeros in every code object, never written.  A row gather whose edge
+// is absent (past a row's degree, or a past-the-end item) reads this row
+// instead of being skipped under an exec mask: every lane of the wave issues
+// the same loads on every path, so no gather destination is a partially
+// written register and the compiler's vmcnt accounting is path-independent.
+// The fold masks the value.  Offsets up to 256 floats (a 64-lane x float4 row).
+namespace {
+[[maybe_unused]] __device__ __attribute__((aligned(16))) float kgx_zero_row[256];
+}
+
 // Load/store VEC consecutive floats (VEC in {1,2,4,8,16}; >=4 uses float4 pieces).
 template <int VEC>
 __device__ __forceinline__ void vload(float (&d)[VEC], const float* __restrict__ p) {

@@ -363,12 +363,6 @@ __global__ __launch_bounds__(kBlock) void spmm_long_kernel(SpmmArgs a) {
 #ifndef KGX_HUB_D
 #define KGX_HUB_D 8
 #endif
-// timing experiments: bit 0 skips the consumers' fold, bit 2 adds a barrier
-// per iteration.  (Never drop the gathers: the batch loads' completion is
-// proved by the gathers issued after them, see the vmcnt comment below.)
-#ifndef KGX_HUB_DEBUG
-#define KGX_HUB_DEBUG 0
-#endif
 #ifndef KGX_HUB_PRIO
 #define KGX_HUB_PRIO 0
 #endif
@@ -496,20 +490,12 @@ __global__ __launch_bounds__(kHubThreads, 1) void spmm_hub_kernel(SpmmArgs a) {
       for (int32_t s = 0; s < n_iter; s += 2) {
         if (s >= 1 && s - 1 < n_st) rd(va, s - 1);
         __builtin_amdgcn_sched_barrier(0);  // the reads fly while the previous stage folds
-#if !(KGX_HUB_DEBUG & 1)  // timing experiment: no fold
         if (s >= 2 && s - 2 < n_st) fold(vb, s - 2);
-#endif
         hub_barrier_reader();
         if (s < n_st) rd(vb, s);
         __builtin_amdgcn_sched_barrier(0);
-#if !(KGX_HUB_DEBUG & 1)
         if (s >= 1 && s - 1 < n_st) fold(va, s - 1);
-#endif
         hub_barrier_reader();
-#if KGX_HUB_DEBUG & 4
-        hub_barrier_reader();
-        hub_barrier_reader();
-#endif
       }
       if (f < fw) {
         float r[1] = {a.epi == KGX_EPI_RAW ? R::finish_raw(acc, end - beg) : R::finish(acc, end - beg)};
@@ -601,9 +587,6 @@ __global__ __launch_bounds__(kHubThreads, 1) void spmm_hub_kernel(SpmmArgs a) {
         if (j == 0) batch(fill, k + 2);
         gather(j, s + D, ci[use][j]);
         hub_barrier();
-#if KGX_HUB_DEBUG & 4  // timing experiment: a second barrier per iteration
-        hub_barrier();
-#endif
       }
       // the batch issued at j = 0 has landed (only this chunk's loads are
       // newer): the compiler may copy its registers at the loop's back edge
@@ -638,8 +621,9 @@ __global__ __launch_bounds__(kHubThreads, 1) void spmm_hub_kernel(SpmmArgs a) {
 // each row pays a chain of dependent loads (item, index, row) for 0.5-4 KB:
 // NS rows of degree <= 7 ran at 5.1 TB/s against 7.7 TB/s for the rest
 // (tools/exp_lowdeg.py spmm).  Here a group takes kSR consecutive items and
-// gathers the first kSPF edges of all of them together (exec-masked by
-// degree), the rest in pairs, each row still reduced in its CSR order.
+// gathers the first kSPF edges of all of them together (never exec-masked:
+// absent edges read kgx_zero_row and are masked at the fold), the rest in
+// pairs, each row still reduced in its CSR order.
 #ifndef KGX_SPMM_SHORT_R
 #define KGX_SPMM_SHORT_R 4
 #endif
@@ -700,7 +684,7 @@ __global__ __launch_bounds__(kBlock) void spmm_short_kernel(SpmmArgs a) {
       for (int r = 0; r < kSR; ++r)
 #pragma unroll
         for (int u = 0; u < kSPF; ++u)
-          if (u < deg[r]) vload<VEC>(v[r][u], tsrc<TWO>(a, c[r][u]) + fl);
+          vload<VEC>(v[r][u], u < deg[r] ? tsrc<TWO>(a, c[r][u]) + fl : kgx_zero_row + fl);
 #pragma unroll
       for (int r = 0; r < kSR; ++r)
 #pragma unroll
@@ -861,10 +845,23 @@ ForkJoin& fork_join() {
   return fj;
 }
 
+// Joins a forked side stream back into the caller's stream on every return
+// after the fork, so no error path leaves the caller's stream unordered
+// against the forked kernel (whose outputs the caching allocator could
+// otherwise hand out again while it still writes them).
+struct JoinGuard {
+  ForkJoin* fj = nullptr;
+  hipStream_t s = nullptr;
+  ~JoinGuard() {
+    if (fj) (void)hipStreamWaitEvent(s, fj->join, 0);
+  }
+};
+
 template <int VEC, int NT, int RED, bool W, bool TWO = false>
 int launch_main(const SpmmArgs& a_in, hipStream_t s) {
   SpmmArgs a = a_in;
   ForkJoin* joined = nullptr;
+  JoinGuard guard;
   int64_t a_hub_slots = 0;  // KGX_EXACT_FORK=2: spmm_kernel's grid leaves these block slots to the hub kernel
   if constexpr (NT == 1) {
     static const bool hub_off = [] {
@@ -923,6 +920,8 @@ int launch_main(const SpmmArgs& a_in, hipStream_t s) {
           return KGX_ERR_HIP;
         }
         joined = &fj;
+        guard.fj = &fj;
+        guard.s = s;
         if (fork_mode == 2) a_hub_slots = hub_blocks * (kHubThreads / kBlock);  // spmm blocks a hub block displaces
       } else {
         hipLaunchKernelGGL(kh, dim3(unsigned(nb)), dim3(kHubThreads), 0, s, a);
@@ -978,9 +977,12 @@ int launch_main(const SpmmArgs& a_in, hipStream_t s) {
     KGX_CHECK_LAUNCH();
   }
   if (short_last && launch_short() != KGX_OK) return KGX_ERR_HIP;
-  if (joined && hipStreamWaitEvent(s, joined->join, 0) != hipSuccess) {
-    set_error("kgx_spmm: stream join failed");
-    return KGX_ERR_HIP;
+  if (joined) {
+    guard.fj = nullptr;  // joined here, with the status checked
+    if (hipStreamWaitEvent(s, joined->join, 0) != hipSuccess) {
+      set_error("kgx_spmm: stream join failed");
+      return KGX_ERR_HIP;
+    }
   }
   if (a.items && a.n_split > 0) {
     auto k = spmm_fixup_kernel<VEC, NT, RED>;

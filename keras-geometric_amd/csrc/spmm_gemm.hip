@@ -29,7 +29,6 @@
 #include <type_traits>
 
 #include "kgx_bf16x3.h"
-#include "kgx_f16x2.h"
 #include "kgx_internal.h"
 #include "kgx_vec.h"
 
@@ -39,29 +38,17 @@ namespace {
 constexpr int kFin = 128;
 constexpr int kGroups = 16;       // rows per block iteration
 constexpr int kThreads = kGroups * 32;
-[[maybe_unused]] constexpr int kTileLd = kFin + 4;  // padded LDS row (the out-tile forms)
-#ifndef KGX_FUSED_BF16X3
-#define KGX_FUSED_BF16X3 1  // 0: f32-input MFMA (exact f32 products, 16x slower per clock)
-#endif
-// spmm_gemm_kernel's MFMA waves compute D^T and store four adjacent columns per
-// lane straight from the accumulators instead of through an f32 LDS out tile
-#ifndef KGX_FUSED_TSTORE
-#define KGX_FUSED_TSTORE 1
-#endif
+constexpr int kTileLd = kFin + 4;  // padded LDS row of the short-row kernel's f32 out tile
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// The transform's operand split (main, short-row and tiny-row kernels alike,
-// so their outputs stay bit-identical to each other): 2 = f16x2 (two fp16
-// planes with power-of-two row / column scales, three MFMAs per k-step, W's
-// fragments in 32 VGPRs; kgx_f16x2.h), 3 = bf16x3 (three bf16 planes, six
-// MFMAs, 48 VGPRs; kgx_bf16x3.h).
-#ifndef KGX_FUSED_SPLIT
-#define KGX_FUSED_SPLIT 3
-#endif
-constexpr bool kFH2 = KGX_FUSED_SPLIT == 2;
-constexpr int kFPlanes = kFH2 ? 2 : 3;
-static_assert(!kFH2 || (KGX_FUSED_BF16X3 && KGX_FUSED_TSTORE), "the f16x2 split replaces the bf16x3 transform");
+// The transform's operand split, the same in the main, short-row and tiny-row
+// kernels so their outputs stay bit-identical to each other: three bf16 planes
+// (hi / mid / lo), six MFMAs per k-step, W's fragments in 48 VGPRs
+// (kgx_bf16x3.h).  Measured alternatives (the f32-input MFMA, the f16x2 split,
+// f32 LDS out tiles in the main and tiny kernels) are kept out of this file:
+// tools/experiments/round4_variants.patch.
+constexpr int kFPlanes = 3;
 
 struct FusedArgs {
   const int32_t* rowptr;
@@ -90,7 +77,6 @@ struct FusedArgs {
   int share_gpu;    // launch 7/8 of the resident grid
   int relu;         // out = max(result, 0), after the accumulate
   float gin_scale;
-  int debug;        // experiment builds only (-DKGX_EXPERIMENTS, env KGX_FUSED_DEBUG): 1 skip MFMA, 2 skip stores (main / short kernels); 4 / 8 / 16 tiny kernel: skip MFMA, skip stores, gathers all from row 0
   int64_t n_short_end;  // items [n_long, n_short_end): spmm_gemm_short_kernel
   const int4* tpack;    // rows of degree <= 2 as {row, degree, col0, col1} (spmm_gemm_tiny_kernel)
   const float2* tw;     // their weights {w0, w1} (weighted reductions)
@@ -132,25 +118,11 @@ typedef short bf16x4_t __attribute__((ext_vector_type(4)));
 
 // W's split B-fragments for this lane's output column n_col: k-step s (0..3)
 // of lane group q covers k = 32 q + 8 s + j (j = 0..7), so each A fragment is
-// 8 contiguous elements of a tile row (one ds_read_b128).  bf16x3: hi / mid /
-// lo planes; f16x2: hi in wfh, lo in wfl (wfm unused), the column scaled by
-// its own power of two (the max over its four lane groups); returns the
-// column's unscale exponent (0 for bf16x3).
+// 8 contiguous elements of a tile row (one ds_read_b128); hi / mid / lo planes.
 template <bool NARROW, typename Args>
-__device__ __forceinline__ int load_w128(const Args& a, bool w_ok, int n_col, int q, bf16x8_t (&wfh)[4],
-                                         bf16x8_t (&wfm)[4], bf16x8_t (&wfl)[4]) {
+__device__ __forceinline__ void load_w128(const Args& a, bool w_ok, int n_col, int q, bf16x8_t (&wfh)[4],
+                                          bf16x8_t (&wfm)[4], bf16x8_t (&wfl)[4]) {
   auto wv = [&](int k) { return w_ok && (!NARROW || k < a.F_in) ? a.W[int64_t(k) * a.F_out + n_col] : 0.0f; };
-  int sh = 0;
-  if constexpr (kFH2) {
-    uint32_t m = 0;
-    for (int k = 32 * q; k < 32 * q + 32; ++k) {
-      const uint32_t b = abs_bits(wv(k));
-      m = max(m, b < 0x7f800000u ? b : 0u);
-    }
-    m = max(m, uint32_t(__shfl_xor(int(m), 16)));
-    m = max(m, uint32_t(__shfl_xor(int(m), 32)));
-    sh = h2_shift(m);
-  }
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
@@ -158,11 +130,8 @@ __device__ __forceinline__ int load_w128(const Args& a, bool w_ok, int n_col, in
 #pragma unroll
     for (int j = 0; j < 8; j += 2) {
       const float v0 = wv(32 * q + 8 * s + j), v1 = wv(32 * q + 8 * s + j + 1);
-      uint32_t h, m_ = 0, l;
-      if constexpr (kFH2)
-        split2h_pair(v0, v1, sh, h, l);
-      else
-        split3_pair(v0, v1, h, m_, l);
+      uint32_t h, m_, l;
+      split3_pair(v0, v1, h, m_, l);
       ph[j / 2] = h;
       pm[j / 2] = m_;
       pl[j / 2] = l;
@@ -171,21 +140,13 @@ __device__ __forceinline__ int load_w128(const Args& a, bool w_ok, int n_col, in
     wfm[s] = __builtin_bit_cast(bf16x8_t, pm);
     wfl[s] = __builtin_bit_cast(bf16x8_t, pl);
   }
-  return -sh;
 }
 
-// One k-step of a 16-row block on one accumulator: D^T += W^T x^T with the
-// split's products, small terms first (the tile's planes: bf16x3 hi / mid / lo,
-// f16x2 hi / lo in ah / am)
+// One k-step of a 16-row block on one accumulator, D^T += W^T x^T: the six
+// significant products of the split operands, small terms first (the tile's
+// planes ah / am / al)
 __device__ __forceinline__ f32x4 kstep_t(const bf16x8_t& wh, const bf16x8_t& wm, const bf16x8_t& wl,
                                          const bf16x8_t& ah, const bf16x8_t& am, const bf16x8_t& al, f32x4 d) {
-  if constexpr (kFH2) {
-    const kgx_h8_t Wh = __builtin_bit_cast(kgx_h8_t, wh), Wl = __builtin_bit_cast(kgx_h8_t, wl);
-    const kgx_h8_t Xh = __builtin_bit_cast(kgx_h8_t, ah), Xl = __builtin_bit_cast(kgx_h8_t, am);
-    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(Wh, Xl, d, 0, 0, 0);
-    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(Wl, Xh, d, 0, 0, 0);
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(Wh, Xh, d, 0, 0, 0);
-  }
   d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, al, d, 0, 0, 0);
   d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, ah, d, 0, 0, 0);
   d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, am, d, 0, 0, 0);
@@ -194,29 +155,21 @@ __device__ __forceinline__ f32x4 kstep_t(const bf16x8_t& wh, const bf16x8_t& wm,
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, ah, d, 0, 0, 0);
 }
 
-// f16x2, D = x W (the out-tile epilogues): kstep_t's products with the
-// operands swapped, same order -- the same bits, transposed
-__device__ __forceinline__ f32x4 kstep_n(const bf16x8_t& wh, const bf16x8_t& wl, const bf16x8_t& ah,
-                                         const bf16x8_t& al, f32x4 d) {
-  const kgx_h8_t Wh = __builtin_bit_cast(kgx_h8_t, wh), Wl = __builtin_bit_cast(kgx_h8_t, wl);
-  const kgx_h8_t Xh = __builtin_bit_cast(kgx_h8_t, ah), Xl = __builtin_bit_cast(kgx_h8_t, al);
-  d = __builtin_amdgcn_mfma_f32_16x16x32_f16(Xl, Wh, d, 0, 0, 0);
-  d = __builtin_amdgcn_mfma_f32_16x16x32_f16(Xh, Wl, d, 0, 0, 0);
-  return __builtin_amdgcn_mfma_f32_16x16x32_f16(Xh, Wh, d, 0, 0, 0);
+// The same products with the operands swapped, D += x W (the short-row
+// kernel's f32 out tile): same order, the same bits transposed
+__device__ __forceinline__ f32x4 kstep_n(const bf16x8_t& wh, const bf16x8_t& wm, const bf16x8_t& wl,
+                                         const bf16x8_t& ah, const bf16x8_t& am, const bf16x8_t& al, f32x4 d) {
+  d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, wh, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wl, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, wm, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, wh, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wm, d, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wh, d, 0, 0, 0);
 }
 
-// A tile row's split planes from this lane's four values (every lane of the
-// wave calls this together: the f16x2 scale is its 32-lane group's maximum);
-// returns the row's unscale exponent (0 for bf16x3).  bf16x3: the fast split,
-// or split3_a_lo (non-finite values to the lo plane) when the lane holds one.
-__device__ __forceinline__ int split_row128(const float (&v)[4], bf16x4_t& ph, bf16x4_t& pm, bf16x4_t& pl) {
-  if constexpr (kFH2) {
-    uint2 h, l;
-    const int ue = split_row_h2_half(v, h, l);
-    ph = __builtin_bit_cast(bf16x4_t, h);
-    pm = __builtin_bit_cast(bf16x4_t, l);
-    return ue;
-  }
+// A tile row's split planes from this lane's four values: the fast split, or
+// split3_a_lo (non-finite values to the lo plane) when the lane holds one.
+__device__ __forceinline__ void split_row128(const float (&v)[4], bf16x4_t& ph, bf16x4_t& pm, bf16x4_t& pl) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     short h, m_, l;
@@ -238,31 +191,15 @@ __device__ __forceinline__ int split_row128(const float (&v)[4], bf16x4_t& ph, b
       pl[k] = l;
     }
   }
-  return 0;
 }
 
-// accumulator value -> output value before the bias: f16x2 undoes the row's
-// and the column's scales (exact power-of-two ldexp)
-__device__ __forceinline__ float unscale(float d, int e) {
-  if constexpr (kFH2) return __builtin_ldexpf(d, e);
-  return d;
+// A row gather that is never exec-masked: lanes whose edge is absent (u >= the
+// row's degree, past-the-end items) read the zero row instead and the fold
+// masks them; see kgx_zero_row (kgx_vec.h).
+template <bool TWO>
+__device__ __forceinline__ const float* gsrc_or_zero(const FusedArgs& a, bool present, int32_t c, int fg) {
+  return present ? gsrc<TWO>(a, c) + fg : kgx_zero_row + fg;
 }
-
-#ifndef KGX_FUSED_QUAD_IDX
-#define KGX_FUSED_QUAD_IDX 0
-#endif
-
-#if KGX_FUSED_QUAD_IDX
-// value of lane (quad base + u) for every lane of each quad (DPP quad_perm [u,u,u,u])
-__device__ __forceinline__ int32_t quad_bcast(int32_t v, int u) {
-  switch (u) {
-    case 0: return __builtin_amdgcn_mov_dpp(v, 0x00, 0xF, 0xF, false);
-    case 1: return __builtin_amdgcn_mov_dpp(v, 0x55, 0xF, 0xF, false);
-    case 2: return __builtin_amdgcn_mov_dpp(v, 0xAA, 0xF, 0xF, false);
-    default: return __builtin_amdgcn_mov_dpp(v, 0xFF, 0xF, 0xF, false);
-  }
-}
-#endif
 
 template <int RED>
 struct Red {
@@ -308,18 +245,8 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
 #else
   constexpr int PF = 4;  // rows prefetched per group for the next tile (live across the MFMA phase)
 #endif
-#if KGX_FUSED_BF16X3
   __shared__ __attribute__((aligned(16))) short tile3[kFPlanes][kGroups][kFin + 8];  // split planes of the aggregated rows
-  __shared__ int32_t tile_ue[kGroups];                        // f16x2: the rows' unscale exponents
-  __shared__ __attribute__((aligned(16))) int ucol[kFin];     // f16x2: W columns' unscale exponents
-#else
-  __shared__ float tile[kGroups][kTileLd];
-#endif
-#if KGX_FUSED_TSTORE && KGX_FUSED_BF16X3
   __shared__ __attribute__((aligned(16))) float sbias[kFin];  // read at the stores (4 VGPRs fewer than a register copy)
-#else
-  __shared__ float otile[kGroups][kTileLd];  // MFMA results, re-read as whole rows
-#endif
   __shared__ int32_t tile_row[kGroups];
 
   const int tid = threadIdx.x;
@@ -336,66 +263,52 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
   const bool w_ok = mfma_wave && (!NARROW || n_col < a.F_out);  // W rows k >= F_in and columns >= F_out load as 0
 
   // W fragment for this wave's 16 columns, K permuted: k = 32 q + s.
-#if KGX_FUSED_BF16X3
   bf16x8_t wfh[4], wfm[4], wfl[4];
-  {
-    const int uc = load_w128<NARROW>(a, w_ok, n_col, q, wfh, wfm, wfl);
-    if (kFH2 && q == 0) ucol[n_col] = uc;  // first read after the tile barrier
-  }
-#else
-  float wb[32];
-#pragma unroll
-  for (int s = 0; s < 32; ++s) wb[s] = w_ok && (!NARROW || 32 * q + s < a.F_in) ? a.W[int64_t(32 * q + s) * a.F_out + n_col] : 0.0f;
-#endif
-#if KGX_FUSED_TSTORE && KGX_FUSED_BF16X3
+  load_w128<NARROW>(a, w_ok, n_col, q, wfh, wfm, wfl);
   const int c4 = wave * 16 + 4 * q;
   if (tid < kFin) sbias[tid] = (a.bias && tid < a.F_out) ? a.bias[tid] : 0.0f;  // first read after the tile barrier
-#else
-  const float bcol = (mfma_wave && a.bias) ? a.bias[n_col] : 0.0f;
-#endif
 
   const int64_t n_work = a.items ? a.n_long : a.n_rows;
   const int64_t stride = int64_t(gridDim.x) * kGroups;
 
-  // software pipeline: the next item's descriptor and its first U neighbour rows
+  // software pipeline: the next item's descriptor and its first PF neighbour rows
   // are loaded before the MFMA phase of the current tile, so the gathers are in
   // flight while the matrix pipe works.
   int32_t row = -1, beg = 0, end = 0, slot = -1;
   int pn = 0;
   float pv[PF][4], pw[PF];
   auto fetch = [&](int64_t it) {
-    row = -1;
-    beg = end = 0;
-    slot = -1;
-    if (it < n_work) {
-      if (a.items) {
-        const int4 v = a.items[it];
-        row = v.x;
-        beg = v.y;
-        end = v.z;
-        slot = v.w;
-      } else {
-        row = a.rows[it];
-        beg = a.rowptr[row];
-        end = a.rowptr[row + 1];
-      }
+    // the descriptor from a clamped slot (n_work >= 1 in a launched kernel),
+    // never under an exec mask; past-the-end groups get an empty item
+    const bool live = it < n_work;
+    const int64_t itc = live ? it : n_work - 1;
+    if (a.items) {
+      const int4 v = a.items[itc];
+      row = live ? v.x : -1;
+      beg = live ? v.y : 0;
+      end = live ? v.z : 0;
+      slot = live ? v.w : -1;
+    } else {
+      const int32_t rw = a.rows[itc];
+      const int32_t b0 = a.rowptr[rw], b1 = a.rowptr[rw + 1];
+      row = live ? rw : -1;
+      beg = live ? b0 : 0;
+      end = live ? b1 : 0;
+      slot = -1;
     }
     pn = (end - beg) < PF ? (end - beg) : PF;
-    // unconditional loads from clamped addresses (idx/w hold >= 1 element);
-    // masking happens when the values are folded in, never around a load
+    // unconditional loads: index / weight from clamped slots (idx / w hold >= 1
+    // element), rows past the item's edges from the zero row; masking happens
+    // when the values are folded in, never around a load
     int32_t c[PF];
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
       const int32_t ee = pn > 0 ? beg + (u < pn ? u : pn - 1) : 0;
-      const int32_t ci = a.idx[ee];
-      c[u] = pn > 0 ? ci : 0;
+      c[u] = a.idx[ee];
       if constexpr (WEIGHTED) pw[u] = a.w[ee];
     }
 #pragma unroll
-    for (int u = 0; u < PF; ++u) {
-      if (u < pn)  // exec-masked: rows of degree < PF issue no redundant loads
-        vload<4>(pv[u], gsrc<TWO>(a, c[u]) + fg);
-    }
+    for (int u = 0; u < PF; ++u) vload<4>(pv[u], gsrc_or_zero<TWO>(a, u < pn, c[u], fg));
   };
 
   fetch(int64_t(blockIdx.x) * kGroups + g);
@@ -415,30 +328,12 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
       const int n = end - e;
       int32_t c[B];
       float wt[B];
-#if KGX_FUSED_QUAD_IDX
-      // one index (and weight) load per lane instead of B: lane l fetches edge
-      // l % B of the block, so every quad of the group holds all B (B <= 4),
-      // and a quad_perm DPP broadcast hands edge u's values to every lane
-      {
-        const int q = lane & (B - 1);
-        const int32_t ee = q < n ? e + q : end - 1;
-        const int32_t cl = a.idx[ee];
-        float wl = 0.0f;
-        if constexpr (WEIGHTED) wl = a.w[ee];
-#pragma unroll
-        for (int u = 0; u < B; ++u) {
-          c[u] = quad_bcast(cl, u);
-          if constexpr (WEIGHTED) wt[u] = __builtin_bit_cast(float, quad_bcast(__builtin_bit_cast(int32_t, wl), u));
-        }
-      }
-#else
 #pragma unroll
       for (int u = 0; u < B; ++u) {
         const int32_t ee = u < n ? e + u : end - 1;
         c[u] = a.idx[ee];
         if constexpr (WEIGHTED) wt[u] = a.w[ee];
       }
-#endif
       float v[B][4];
 #pragma unroll
       for (int u = 0; u < B; ++u) vload<4>(v[u], gsrc<TWO>(a, c[u]) + fg);
@@ -470,78 +365,42 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
 #pragma unroll
       for (int k = 0; k < 4; ++k) r[k] = f_ok ? r[k] : 0.0f;
     }
-#if KGX_FUSED_BF16X3
     {
       bf16x4_t ph, pm, pl;
-      const int ue = split_row128(r, ph, pm, pl);
+      split_row128(r, ph, pm, pl);
       *reinterpret_cast<bf16x4_t*>(&tile3[0][g][f]) = ph;
       *reinterpret_cast<bf16x4_t*>(&tile3[1][g][f]) = pm;
-      if constexpr (!kFH2) *reinterpret_cast<bf16x4_t*>(&tile3[kFPlanes - 1][g][f]) = pl;
-      if (kFH2 && lane == 0) tile_ue[g] = ue;
+      *reinterpret_cast<bf16x4_t*>(&tile3[2][g][f]) = pl;
     }
-#else
-    *reinterpret_cast<float4*>(&tile[g][f]) = make_float4(r[0], r[1], r[2], r[3]);
-#endif
     if (lane == 0) tile_row[g] = full_row ? row : -1;
     lds_barrier();
 
     fetch(base + stride + g);  // next tile's first gathers fly during the MFMAs
 
-    if (mfma_wave && !(a.debug & 1)) {
+    if (mfma_wave) {
       const int m = wl & 15;
       f32x4 d0 = {0.0f, 0.0f, 0.0f, 0.0f};
-      f32x4 d1 = {0.0f, 0.0f, 0.0f, 0.0f};  // two chains: the f32 MFMA's dependent latency is 40 > 32 cycles
-#if KGX_FUSED_BF16X3
+      f32x4 d1 = {0.0f, 0.0f, 0.0f, 0.0f};  // two accumulation chains
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) {
         const bf16x8_t ah = *reinterpret_cast<const bf16x8_t*>(&tile3[0][m][32 * q + 8 * s4]);
         const bf16x8_t am = *reinterpret_cast<const bf16x8_t*>(&tile3[1][m][32 * q + 8 * s4]);
-        if constexpr (kFH2) {  // three products, alternating between the two chains by k-step
-          if (s4 & 1)
-            d1 = kstep_t(wfh[s4], wfm[s4], wfl[s4], ah, am, am, d1);
-          else
-            d0 = kstep_t(wfh[s4], wfm[s4], wfl[s4], ah, am, am, d0);
-          continue;
-        }
-        const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(&tile3[kFPlanes - 1][m][32 * q + 8 * s4]);
-        // small terms first
-#if KGX_FUSED_TSTORE  // D^T = W^T x^T (same products and k order)
+        const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(&tile3[2][m][32 * q + 8 * s4]);
+        // D^T = W^T x^T, small terms first
         d1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[s4], al, d1, 0, 0, 0);
         d0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfl[s4], ah, d0, 0, 0, 0);
         d1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfm[s4], am, d1, 0, 0, 0);
         d0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[s4], am, d0, 0, 0, 0);
         d1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfm[s4], ah, d1, 0, 0, 0);
         d0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[s4], ah, d0, 0, 0, 0);
-#else
-        d1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, wfh[s4], d1, 0, 0, 0);
-        d0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfl[s4], d0, 0, 0, 0);
-        d1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, wfm[s4], d1, 0, 0, 0);
-        d0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, wfh[s4], d0, 0, 0, 0);
-        d1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfm[s4], d1, 0, 0, 0);
-        d0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfh[s4], d0, 0, 0, 0);
-#endif
       }
-#else
-      constexpr int s_end = 32;
-#pragma unroll
-      for (int s0 = 0; s0 < s_end; s0 += 4) {
-        const float4 t4 = *reinterpret_cast<const float4*>(&tile[m][32 * q + s0]);
-        d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(t4.x, wb[s0 + 0], d0, 0, 0, 0);
-        d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(t4.y, wb[s0 + 1], d1, 0, 0, 0);
-        d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(t4.z, wb[s0 + 2], d0, 0, 0, 0);
-        d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(t4.w, wb[s0 + 3], d1, 0, 0, 0);
-      }
-#endif
-#if KGX_FUSED_TSTORE && KGX_FUSED_BF16X3
       // straight from the accumulators: lane (m, q) writes columns 16 wave + 4 q .. + 3 of tile row m
       const int rr = tile_row[m];
-      if (rr >= 0 && (!NARROW || c4 < a.F_out) && !(a.debug & 2)) {
+      if (rr >= 0 && (!NARROW || c4 < a.F_out)) {
         float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + c4);
         const float4 b4 = *reinterpret_cast<const float4*>(&sbias[c4]);
-        const int ue = kFH2 ? tile_ue[m] : 0;
-        const int4 uc = kFH2 ? *reinterpret_cast<const int4*>(&ucol[c4]) : make_int4(0, 0, 0, 0);
-        float4 v = make_float4(unscale(d0[0] + d1[0], ue + uc.x) + b4.x, unscale(d0[1] + d1[1], ue + uc.y) + b4.y,
-                               unscale(d0[2] + d1[2], ue + uc.z) + b4.z, unscale(d0[3] + d1[3], ue + uc.w) + b4.w);
+        float4 v = make_float4((d0[0] + d1[0]) + b4.x, (d0[1] + d1[1]) + b4.y, (d0[2] + d1[2]) + b4.z,
+                               (d0[3] + d1[3]) + b4.w);
         if (a.accumulate) {
           const float4 p = *dst;
           v = make_float4(__fadd_rn(p.x, v.x), __fadd_rn(p.y, v.y), __fadd_rn(p.z, v.z), __fadd_rn(p.w, v.w));
@@ -553,48 +412,23 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
     lds_barrier();  // every wave is done with the planes and tile_row before the next tile's are written
   }
 }
-#else
-#pragma unroll
-      for (int j = 0; j < 4; ++j) otile[4 * q + j][n_col] = (d0[j] + d1[j]) + bcol;
-    }
-    lds_barrier();
-    // whole-row dwordx4 stores: group g writes its tile row (F_out/4 lanes)
-    if (!(a.debug & 2)) {
-      const int rr = tile_row[g];
-      if (rr >= 0 && f < a.F_out) {
-        float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + f);
-        float4 v = *reinterpret_cast<const float4*>(&otile[g][f]);
-        if (a.accumulate) {
-          const float4 p = *dst;
-          v = make_float4(__fadd_rn(p.x, v.x), __fadd_rn(p.y, v.y), __fadd_rn(p.z, v.z), __fadd_rn(p.w, v.w));
-        }
-        if (a.relu) v = make_float4(fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f));
-        *dst = v;
-      }
-    }
-  }
-}
-#endif
 
 // Rows of degree <= KGX_SHORT_ROW_MAX (the schedule's suffix; 78 % of an R-MAT graph's
 // rows, 11 % of its edges).  spmm_gemm_kernel gives each row-group ONE row per
 // 16-row tile, so on these rows a group has one or two gathers in flight and
 // the tile's fixed chain (item, index, row, split, MFMA, store) dominates:
 // NS rows of degree <= 7 ran at 3.4 TB/s against 7.7 TB/s for the rest
-// (tools/exp_lowdeg.py).  Here a block iteration takes 64 rows, 4 per group,
-// whose first two edges are all gathered together, and the MFMA phase runs
-// four 16-row blocks per wave.
-static_assert(KGX_SHORT_ROW_MAX == 7, "the short kernel gathers two edges per row up front, then pairs");
+// (tools/exp_lowdeg.py).  Here a block iteration takes 32 rows, 2 per group,
+// whose first three edges are all gathered together, and the MFMA phase runs
+// two 16-row blocks per wave; the results go through an f32 LDS out tile and
+// are stored as whole rows (measured 0.98 against 0.99 ms for stores straight
+// from the accumulators).
+static_assert(KGX_SHORT_ROW_MAX == 7, "the short kernel gathers three edges per row up front, then pairs");
 #ifndef KGX_SHORT_RPG
 #define KGX_SHORT_RPG 2
 #endif
 #ifndef KGX_SHORT_PF
 #define KGX_SHORT_PF 3
-#endif
-// MFMA waves compute D^T and store four adjacent columns per lane straight from
-// the accumulators (no f32 LDS out tile, two barriers per tile instead of four)
-#ifndef KGX_SHORT_TSTORE
-#define KGX_SHORT_TSTORE 0  // measured +0.01 ms (0.99 vs 0.98): the out-tile form stays
 #endif
 constexpr int kRPG = KGX_SHORT_RPG;        // rows per group per tile
 constexpr int kSPF = KGX_SHORT_PF;         // edges per row gathered up front (all rows together)
@@ -603,17 +437,11 @@ constexpr int kShortRows = kGroups * kRPG;
 template <int RED, bool WEIGHTED, bool TWO, bool NARROW>
 __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs a) {  // 4 waves per SIMD: two blocks per CU
   using R = Red<RED>;
-  // split planes of the 64 aggregated rows; after the MFMAs the same bytes hold the f32 results
+  // split planes of the 32 aggregated rows; after the MFMAs the same bytes hold the f32 results
   __shared__ __attribute__((aligned(16))) short tile3[kFPlanes][kShortRows][kFin + 8];
   __shared__ int32_t tile_row[kShortRows];
-  __shared__ __attribute__((aligned(16))) int32_t tile_ue[kShortRows];  // f16x2: the rows' unscale exponents
-  __shared__ __attribute__((aligned(16))) int ucol[kFin];               // f16x2: W columns' unscale exponents
-#if KGX_SHORT_TSTORE
-  __shared__ __attribute__((aligned(16))) float sbias[kFin];  // read at the stores
-#else
   static_assert(sizeof(tile3) >= sizeof(float) * kShortRows * kTileLd, "output tile must fit the plane buffer");
   float(*otile)[kTileLd] = reinterpret_cast<float(*)[kTileLd]>(&tile3[0][0][0]);
-#endif
 
   const int tid = threadIdx.x;
   const int g = tid >> 5;
@@ -629,14 +457,8 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
   const bool w_ok = mfma_wave && (!NARROW || n_col < a.F_out);  // W rows k >= F_in and columns >= F_out load as 0
 
   bf16x8_t wfh[4], wfm[4], wfl[4];
-  const int uc_n = load_w128<NARROW>(a, w_ok, n_col, q, wfh, wfm, wfl);  // this lane's column's unscale exponent
-  if (kFH2 && q == 0) ucol[n_col] = uc_n;  // first read after two barriers
-#if KGX_SHORT_TSTORE
-  const int c4 = wave * 16 + 4 * q;
-  if (tid < kFin) sbias[tid] = (a.bias && tid < a.F_out) ? a.bias[tid] : 0.0f;  // first read after two barriers
-#else
+  load_w128<NARROW>(a, w_ok, n_col, q, wfh, wfm, wfl);
   const float bcol = (mfma_wave && a.bias) ? a.bias[n_col] : 0.0f;
-#endif
 
   for (int64_t base = a.n_long + int64_t(blockIdx.x) * kShortRows; base < a.n_short_end;
        base += int64_t(gridDim.x) * kShortRows) {
@@ -655,8 +477,8 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
       }
     }
     // the first kSPF edges of all the group's rows in flight together
-    // (unconditional index loads from clamped slots; row gathers exec-masked
-    // by degree)
+    // (unconditional loads: indices from clamped slots, absent edges' rows
+    // from the zero row; masked at the fold)
     float acc[kRPG][4];
     {
       int32_t c[kRPG][kSPF];
@@ -673,8 +495,7 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
 #pragma unroll
       for (int r = 0; r < kRPG; ++r)
 #pragma unroll
-        for (int u = 0; u < kSPF; ++u)
-          if (u < deg[r]) vload<4>(v[r][u], gsrc<TWO>(a, c[r][u]) + fg);
+        for (int u = 0; u < kSPF; ++u) vload<4>(v[r][u], gsrc_or_zero<TWO>(a, u < deg[r], c[r][u], fg));
 #pragma unroll
       for (int r = 0; r < kRPG; ++r)
 #pragma unroll
@@ -703,6 +524,9 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
         }
 #pragma unroll
         for (int u = 0; u < 2; ++u) vload<4>(v[u], gsrc<TWO>(a, c[u]) + fg);
+        // both loads stay unconditional: unweighted, hipcc otherwise sinks the
+        // second (masked at the fold when n == 1) into an exec-masked branch
+        asm volatile("" ::"v"(v[1][0]), "v"(v[1][1]), "v"(v[1][2]), "v"(v[1][3]));
 #pragma unroll
         for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -731,19 +555,16 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
         for (int k = 0; k < 4; ++k) v[k] = f_ok ? v[k] : 0.0f;
       }
       bf16x4_t ph, pm, pl;
-      const int ue = split_row128(v, ph, pm, pl);
+      split_row128(v, ph, pm, pl);
       const int tr = g + kGroups * r;
       *reinterpret_cast<bf16x4_t*>(&tile3[0][tr][f]) = ph;
       *reinterpret_cast<bf16x4_t*>(&tile3[1][tr][f]) = pm;
-      if constexpr (!kFH2) *reinterpret_cast<bf16x4_t*>(&tile3[kFPlanes - 1][tr][f]) = pl;
-      if (lane == 0) {
-        tile_row[tr] = row[r];
-        if constexpr (kFH2) tile_ue[tr] = ue;
-      }
+      *reinterpret_cast<bf16x4_t*>(&tile3[2][tr][f]) = pl;
+      if (lane == 0) tile_row[tr] = row[r];
     }
     lds_barrier();
     f32x4 d[kRPG];
-    if (mfma_wave && !(a.debug & 1)) {
+    if (mfma_wave) {
       const int m = wl & 15;
 #pragma unroll
       for (int rb = 0; rb < kRPG; ++rb) d[rb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -754,84 +575,34 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
           const int tr = 16 * rb + m;
           const bf16x8_t ah = *reinterpret_cast<const bf16x8_t*>(&tile3[0][tr][32 * q + 8 * s4]);
           const bf16x8_t am = *reinterpret_cast<const bf16x8_t*>(&tile3[1][tr][32 * q + 8 * s4]);
-          if constexpr (kFH2) {  // the tiny kernel's products in its order (bit-identical rows)
-            d[rb] = KGX_SHORT_TSTORE ? kstep_t(wfh[s4], wfm[s4], wfl[s4], ah, am, am, d[rb])
-                                     : kstep_n(wfh[s4], wfl[s4], ah, am, d[rb]);
-            continue;
-          }
-          const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(&tile3[kFPlanes - 1][tr][32 * q + 8 * s4]);
-#if KGX_SHORT_TSTORE  // D^T = W^T x^T (same products and k order): lane (m, q) gets 4 adjacent columns of row m
-          d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[s4], al, d[rb], 0, 0, 0);
-          d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfl[s4], ah, d[rb], 0, 0, 0);
-          d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfm[s4], am, d[rb], 0, 0, 0);
-          d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[s4], am, d[rb], 0, 0, 0);
-          d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfm[s4], ah, d[rb], 0, 0, 0);
-          d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[s4], ah, d[rb], 0, 0, 0);
-#else
-          d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, wfh[s4], d[rb], 0, 0, 0);
-          d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfl[s4], d[rb], 0, 0, 0);
-          d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, wfm[s4], d[rb], 0, 0, 0);
-          d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, wfh[s4], d[rb], 0, 0, 0);
-          d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfm[s4], d[rb], 0, 0, 0);
-          d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfh[s4], d[rb], 0, 0, 0);
-#endif
+          const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(&tile3[2][tr][32 * q + 8 * s4]);
+          d[rb] = kstep_n(wfh[s4], wfm[s4], wfl[s4], ah, am, al, d[rb]);
         }
       }
     }
-#if KGX_SHORT_TSTORE
-    // straight from the accumulators: one dwordx4 per lane per 16-row block (the
-    // next tile's first barrier keeps the planes and tile_row until every wave is done)
-    if (mfma_wave && !(a.debug & 2)) {
-      const int m = wl & 15;
-#pragma unroll
-      for (int rb = 0; rb < kRPG; ++rb) {
-        const int rr = tile_row[16 * rb + m];
-        if (rr >= 0 && (!NARROW || c4 < a.F_out)) {
-          float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + c4);
-          const float4 b4 = *reinterpret_cast<const float4*>(&sbias[c4]);
-          const int ue = kFH2 ? tile_ue[16 * rb + m] : 0;
-          const int4 uc = kFH2 ? *reinterpret_cast<const int4*>(&ucol[c4]) : make_int4(0, 0, 0, 0);
-          float4 v = make_float4(unscale(d[rb][0], ue + uc.x) + b4.x, unscale(d[rb][1], ue + uc.y) + b4.y,
-                                 unscale(d[rb][2], ue + uc.z) + b4.z, unscale(d[rb][3], ue + uc.w) + b4.w);
-          if (a.accumulate) {
-            const float4 p = *dst;
-            v = make_float4(__fadd_rn(p.x, v.x), __fadd_rn(p.y, v.y), __fadd_rn(p.z, v.z), __fadd_rn(p.w, v.w));
-          }
-          if (a.relu) v = make_float4(fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f));
-          *dst = v;
-        }
-      }
-    }
-#else
     lds_barrier();  // every wave has read the planes: their bytes now take the f32 results
     if (mfma_wave) {
 #pragma unroll
-      for (int rb = 0; rb < kRPG; ++rb) {
-        const int4 ue = kFH2 ? *reinterpret_cast<const int4*>(&tile_ue[16 * rb + 4 * q]) : make_int4(0, 0, 0, 0);
-        const int uej[4] = {ue.x, ue.y, ue.z, ue.w};
+      for (int rb = 0; rb < kRPG; ++rb)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) otile[16 * rb + 4 * q + j][n_col] = unscale(d[rb][j], uej[j] + uc_n) + bcol;
-      }
+        for (int j = 0; j < 4; ++j) otile[16 * rb + 4 * q + j][n_col] = d[rb][j] + bcol;
     }
     lds_barrier();
-    if (!(a.debug & 2)) {
 #pragma unroll
-      for (int r = 0; r < kRPG; ++r) {
-        const int tr = g + kGroups * r;
-        const int rr = tile_row[tr];
-        if (rr >= 0 && f < a.F_out) {
-          float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + f);
-          float4 v = *reinterpret_cast<const float4*>(&otile[tr][f]);
-          if (a.accumulate) {
-            const float4 p = *dst;
-            v = make_float4(__fadd_rn(p.x, v.x), __fadd_rn(p.y, v.y), __fadd_rn(p.z, v.z), __fadd_rn(p.w, v.w));
-          }
-          if (a.relu) v = make_float4(fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f));
-          *dst = v;
+    for (int r = 0; r < kRPG; ++r) {
+      const int tr = g + kGroups * r;
+      const int rr = tile_row[tr];
+      if (rr >= 0 && f < a.F_out) {
+        float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + f);
+        float4 v = *reinterpret_cast<const float4*>(&otile[tr][f]);
+        if (a.accumulate) {
+          const float4 p = *dst;
+          v = make_float4(__fadd_rn(p.x, v.x), __fadd_rn(p.y, v.y), __fadd_rn(p.z, v.z), __fadd_rn(p.w, v.w));
         }
+        if (a.relu) v = make_float4(fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f));
+        *dst = v;
       }
     }
-#endif
   }
 }
 
@@ -861,14 +632,6 @@ constexpr int kTinyGroups = 16;  // producer row groups
 #ifndef KGX_TINY_RPG1
 #define KGX_TINY_RPG1 4
 #endif
-// MFMA waves compute D^T so each lane stores four adjacent output columns (dwordx4)
-#ifndef KGX_TINY_TSTORE
-#define KGX_TINY_TSTORE 1
-#endif
-// accumulate mode: load the output rows before the MFMAs (experiment, 0 = after)
-#ifndef KGX_TINY_ACC_EARLY
-#define KGX_TINY_ACC_EARLY 0
-#endif
 template <int NG>
 constexpr int tiny_rows() { return kTinyGroups * (NG == 1 ? KGX_TINY_RPG1 : KGX_TINY_RPG); }
 
@@ -881,13 +644,9 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
   constexpr int kTinyRows = kTinyGroups * kTinyRPG;
   __shared__ __attribute__((aligned(16))) short planes[2][kFPlanes][kTinyRows][kFin + 8];
   __shared__ int32_t trow[2][kTinyRows];
-  __shared__ int32_t tue[2][kTinyRows];                   // f16x2: the rows' unscale exponents
-  __shared__ __attribute__((aligned(16))) int ucol[kFin];  // f16x2: W columns' unscale exponents
-#if KGX_TINY_TSTORE
   __shared__ __attribute__((aligned(16))) float sbias[kFin];  // read at the stores
   if (threadIdx.x < kFin)  // first read after a hand-off barrier
     sbias[threadIdx.x] = (a.bias && int(threadIdx.x) < a.F_out) ? a.bias[threadIdx.x] : 0.0f;
-#endif
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t n_tiles = (a.n_tiny + kTinyRows - 1) / kTinyRows;
@@ -900,37 +659,14 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
     const bool mfma_wave = wave * 16 < a.F_out;
     const bool w_ok = mfma_wave && (!NARROW || n_col < a.F_out);
     bf16x8_t wfh[4], wfm[4], wfl[4];
-    {
-      const int uc = load_w128<NARROW>(a, w_ok, n_col, q, wfh, wfm, wfl);
-      if (kFH2 && q == 0) ucol[n_col] = uc;  // first read after a hand-off barrier
-    }
-#if KGX_TINY_TSTORE
+    load_w128<NARROW>(a, w_ok, n_col, q, wfh, wfm, wfl);
     const int c4 = wave * 16 + 4 * q;
-#else
-    const float bcol = (mfma_wave && a.bias) ? a.bias[n_col] : 0.0f;
-#endif
     for (int64_t i = 0; i <= my_tiles; ++i) {
       if (i >= 1 && mfma_wave) {
         const int b = int((i - 1) & 1);
         f32x4 d[kTinyRPG];
 #pragma unroll
         for (int rb = 0; rb < kTinyRPG; ++rb) d[rb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-#if KGX_TINY_TSTORE && KGX_TINY_ACC_EARLY
-        // accumulate mode: the rows added to are loaded before the MFMAs, so their
-        // latency runs under the matrix work instead of after it
-        float4 pacc[kTinyRPG];
-        if (a.accumulate) {
-#pragma unroll
-          for (int rb = 0; rb < kTinyRPG; ++rb) {
-            const int rr = trow[b][16 * rb + m];
-            pacc[rb] = rr >= 0 && (!NARROW || c4 < a.F_out) ? *reinterpret_cast<const float4*>(a.out + int64_t(rr) * a.ld_o + c4)
-                                               : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-          }
-        }
-#endif
-#ifdef KGX_EXPERIMENTS  // cost decomposition (KGX_FUSED_DEBUG 4: no MFMAs, 8: no stores, 16: gathers all hit row 0)
-        if (!(a.debug & 4))
-#endif
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) {
 #pragma unroll
@@ -938,74 +674,28 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
             const int tr = 16 * rb + m;
             const bf16x8_t ah = *reinterpret_cast<const bf16x8_t*>(&planes[b][0][tr][32 * q + 8 * s4]);
             const bf16x8_t am = *reinterpret_cast<const bf16x8_t*>(&planes[b][1][tr][32 * q + 8 * s4]);
-            if constexpr (kFH2) {
-              d[rb] = kstep_t(wfh[s4], wfm[s4], wfl[s4], ah, am, am, d[rb]);
-              continue;
-            }
-            const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(&planes[b][kFPlanes - 1][tr][32 * q + 8 * s4]);
-#if KGX_TINY_TSTORE  // D^T = W^T x^T: same products, same k order, lane (m, q) gets 4 adjacent columns of row m
-            d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[s4], al, d[rb], 0, 0, 0);
-            d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfl[s4], ah, d[rb], 0, 0, 0);
-            d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfm[s4], am, d[rb], 0, 0, 0);
-            d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[s4], am, d[rb], 0, 0, 0);
-            d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfm[s4], ah, d[rb], 0, 0, 0);
-            d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[s4], ah, d[rb], 0, 0, 0);
-#else
-            d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, wfh[s4], d[rb], 0, 0, 0);
-            d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfl[s4], d[rb], 0, 0, 0);
-            d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, wfm[s4], d[rb], 0, 0, 0);
-            d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, wfh[s4], d[rb], 0, 0, 0);
-            d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfm[s4], d[rb], 0, 0, 0);
-            d[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, wfh[s4], d[rb], 0, 0, 0);
-#endif
+            const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(&planes[b][2][tr][32 * q + 8 * s4]);
+            // D^T = W^T x^T: same products, same k order as the short-row kernel
+            d[rb] = kstep_t(wfh[s4], wfm[s4], wfl[s4], ah, am, al, d[rb]);
           }
         }
-        // lane (m, q) holds column n_col of rows 16 rb + 4 q + j: four 64-byte
-        // row segments per store instruction (the wave next door writes the
-        // other half of each 128-byte line)
-#ifdef KGX_EXPERIMENTS
-        if (!(a.debug & 8))
-#endif
-#if KGX_TINY_TSTORE
         // lane (m, q) holds columns 16 wave + 4 q .. + 3 of tile row 16 rb + m: one
-        // dwordx4 per lane, four store instructions per tile instead of sixteen
+        // dwordx4 per lane, four store instructions per tile
 #pragma unroll
         for (int rb = 0; rb < kTinyRPG; ++rb) {
           const int rr = trow[b][16 * rb + m];
           if (rr >= 0 && (!NARROW || c4 < a.F_out)) {
             float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + c4);
             const float4 b4 = *reinterpret_cast<const float4*>(&sbias[c4]);
-            const int ue = kFH2 ? tue[b][16 * rb + m] : 0;
-            const int4 uc = kFH2 ? *reinterpret_cast<const int4*>(&ucol[c4]) : make_int4(0, 0, 0, 0);
-            float4 v = make_float4(unscale(d[rb][0], ue + uc.x) + b4.x, unscale(d[rb][1], ue + uc.y) + b4.y,
-                                   unscale(d[rb][2], ue + uc.z) + b4.z, unscale(d[rb][3], ue + uc.w) + b4.w);
+            float4 v = make_float4(d[rb][0] + b4.x, d[rb][1] + b4.y, d[rb][2] + b4.z, d[rb][3] + b4.w);
             if (a.accumulate) {
-#if KGX_TINY_ACC_EARLY
-              const float4 p = pacc[rb];
-#else
               const float4 p = *dst;
-#endif
               v = make_float4(__fadd_rn(p.x, v.x), __fadd_rn(p.y, v.y), __fadd_rn(p.z, v.z), __fadd_rn(p.w, v.w));
             }
             if (a.relu) v = make_float4(fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f));
             *dst = v;
           }
         }
-#else
-#pragma unroll
-        for (int rb = 0; rb < kTinyRPG; ++rb)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int rr = trow[b][16 * rb + 4 * q + j];
-            if (rr >= 0 && (!NARROW || n_col < a.F_out)) {
-              float* dst = a.out + int64_t(rr) * a.ld_o + n_col;
-              float v = d[rb][j] + bcol;
-              if (a.accumulate) v = __fadd_rn(*dst, v);
-              if (a.relu) v = fmaxf(v, 0.0f);
-              *dst = v;
-            }
-          }
-#endif
       }
       lds_barrier();
     }
@@ -1036,14 +726,8 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
   auto gather = [&](const Rec& r, f4 (&v)[kTinyRPG][NG]) {
 #pragma unroll
     for (int j = 0; j < kTinyRPG; ++j) {
-#ifdef KGX_EXPERIMENTS
-      const bool hit = a.debug & 16;
-      v[j][0] = *reinterpret_cast<const f4*>(gsrc<TWO>(a, hit ? 0 : r.p[j].z) + fg);
-      if constexpr (NG == 2) v[j][1] = *reinterpret_cast<const f4*>(gsrc<TWO>(a, hit ? 0 : r.p[j].w) + fg);
-#else
       v[j][0] = *reinterpret_cast<const f4*>(gsrc<TWO>(a, r.p[j].z) + fg);
       if constexpr (NG == 2) v[j][1] = *reinterpret_cast<const f4*>(gsrc<TWO>(a, r.p[j].w) + fg);
-#endif
     }
   };
   auto produce = [&](int64_t i, const auto& c, const f4 (&v)[kTinyRPG][NG]) {
@@ -1077,15 +761,12 @@ __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedAr
         for (int k = 0; k < 4; ++k) o[k] = f_ok ? o[k] : 0.0f;
       }
       bf16x4_t ph, pm, pl;
-      const int ue = split_row128(o, ph, pm, pl);
+      split_row128(o, ph, pm, pl);
       const int tr = g + kTinyGroups * j;
       *reinterpret_cast<bf16x4_t*>(&planes[b][0][tr][f]) = ph;
       *reinterpret_cast<bf16x4_t*>(&planes[b][1][tr][f]) = pm;
-      if constexpr (!kFH2) *reinterpret_cast<bf16x4_t*>(&planes[b][kFPlanes - 1][tr][f]) = pl;
-      if (lane == 0) {
-        trow[b][tr] = row;
-        if constexpr (kFH2) tue[b][tr] = ue;
-      }
+      *reinterpret_cast<bf16x4_t*>(&planes[b][2][tr][f]) = pl;
+      if (lane == 0) trow[b][tr] = row;
     }
   };
   // Pipeline, at iteration i: issue tile i+2's records, issue tile i+1's row
@@ -1296,10 +977,10 @@ extern "C" int kgx_spmm_gemm_ex3(int reduce, const int32_t* rowptr, const int32_
   hipStream_t stream = as_stream(stream_);
   KGX_REQUIRE(!x2 || (n_x1 >= 0 && n_x1 < (int64_t(1) << 31) && reinterpret_cast<uintptr_t>(x2) % 16 == 0),
               KGX_ERR_ARG, "kgx_spmm_gemm: x2 must be 16-byte aligned and 0 <= n_x1 < 2^31");
-  KGX_REQUIRE(!x2 || (reduce == KGX_SUM && !(flags & KGX_FUSED_PRE_GIN) && F_in == kFin && F_out % 16 == 0),
-              KGX_ERR_UNSUPPORTED,
-              "kgx_spmm_gemm: two-table gathers are implemented for plain sums at F_in 128, F_out %% 16 == 0 "
-              "(the sharded GCN pass)");
+  // (GIN's pre-scale reads the rows' own x: rows of the first table, local rows)
+  KGX_REQUIRE(!x2 || (reduce == KGX_SUM && F_in == kFin && F_out % 16 == 0), KGX_ERR_UNSUPPORTED,
+              "kgx_spmm_gemm: two-table gathers are implemented for sums at F_in 128, F_out %% 16 == 0 "
+              "(the sharded GCN / GIN passes)");
   KGX_REQUIRE(!items || tiny_pack || n_short_end == n_items, KGX_ERR_ARG,
               "kgx_spmm_gemm: without tiny_pack, n_short_end must equal n_items");
   KGX_REQUIRE(!items || (n_long_items >= 0 && n_long_items <= n_short_end && n_short_end <= n_items), KGX_ERR_ARG,
@@ -1365,15 +1046,6 @@ extern "C" int kgx_spmm_gemm_ex3(int reduce, const int32_t* rowptr, const int32_
   a.share_gpu = (flags & KGX_FUSED_SHARE_GPU) != 0;
   a.relu = (flags & KGX_FUSED_RELU) != 0;
   a.gin_scale = gin_scale;
-#ifdef KGX_EXPERIMENTS  // cost-decomposition knob; never in a product build (it changes results)
-  static const int dbg = [] {
-    const char* h = getenv("KGX_FUSED_DEBUG");
-    return h ? atoi(h) : 0;
-  }();
-  a.debug = dbg;
-#else
-  a.debug = 0;
-#endif
   const bool wt = w != nullptr;
   if (x2) return wt ? launch<KGX_SUM, true, true>(a, stream) : launch<KGX_SUM, false, true>(a, stream);
   if (F_in < kFin || F_out % 16 != 0) {  // the masked instantiations (SAGEConv at C5: 100 -> 100)

@@ -25,7 +25,6 @@
 #include <cstdlib>
 
 #include "kgx_bf16x3.h"
-#include "kgx_f16x2.h"
 #include "kgx_internal.h"
 #include "kgx_red.h"
 #include "kgx_vec.h"
@@ -40,20 +39,11 @@ constexpr int kColBlocks = 16;     // 16-column blocks of F_out: two per wave
 constexpr int kThreads = kWaves * 64;
 constexpr int kLd = kF + 8;        // LDS plane row (bf16): +16 B keeps the B-fragment reads conflict-free
 constexpr int kSteps = kF / 32;    // k-steps of 32 per MFMA chain
-// cost-decomposition builds only (make variant NAME=.. DEFS=-DKGX_F256_DBG=n; changes results):
-// 1 = no MFMAs / fragment reads, 2 = no output stores, 4 = every gather reads row 0 (cache hits)
-#ifndef KGX_F256_DBG
-#define KGX_F256_DBG 0
-#endif
-// The transform's operand split: 2 = f16x2 (two fp16 planes per operand with
-// power-of-two row / column scales, three MFMAs per k-step, W entirely in
-// registers; kgx_f16x2.h), 3 = bf16x3 (three bf16 planes, six MFMAs per k-step,
-// W's lo plane in LDS; kgx_bf16x3.h).
-#ifndef KGX_F256_SPLIT
-#define KGX_F256_SPLIT 3
-#endif
-constexpr bool kH2 = KGX_F256_SPLIT == 2;
-constexpr int kPlanes = kH2 ? 2 : 3;  // activation planes per tile row
+// The transform's operand split: three bf16 planes (kgx_bf16x3.h), six MFMAs
+// per k-step, W's lo plane in LDS.  The measured f16x2 split (three products,
+// 2^-20.4-accurate: outside the f32 contract) and the cost-decomposition
+// builds are kept out of this file: tools/experiments/round4_variants.patch.
+constexpr int kPlanes = 3;  // activation planes per tile row
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short bf16x8_t __attribute__((ext_vector_type(8)));
@@ -115,7 +105,7 @@ __device__ __forceinline__ void lds_barrier() {
 // W fragments of this wave's two 16-column blocks, k permuted: k-step s of lane
 // group q covers k = 64 q + 8 s + j (j = 0..7), so each x fragment is 8
 // contiguous bf16 of a tile row.  hi / mid planes to registers, lo to LDS.
-[[maybe_unused]] __device__ __forceinline__ void load_w(const F256Args& a, int wave, int wl, bf16x8_t (&wfh)[2][kSteps],
+__device__ __forceinline__ void load_w(const F256Args& a, int wave, int wl, bf16x8_t (&wfh)[2][kSteps],
                                        bf16x8_t (&wfm)[2][kSteps], u32x4_t* wlo) {
   const int cl = wl & 15, q = wl >> 4;
 #pragma unroll
@@ -143,96 +133,11 @@ __device__ __forceinline__ void lds_barrier() {
   }
 }
 
-// f16x2: W fragments of this wave's two 16-column blocks (same k permutation),
-// each column scaled by its own power of two (kgx_f16x2.h): hi plane to wfh, lo
-// plane to wfl, both in registers; the column's unscale exponent to ucol.
-__device__ __forceinline__ void load_w_h2(const F256Args& a, int wave, int wl, bf16x8_t (&wfh)[2][kSteps],
-                                          bf16x8_t (&wfl)[2][kSteps], int* ucol) {
-  const int cl = wl & 15, q = wl >> 4;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int n_col = 32 * wave + 16 * i + cl;
-    const bool on = n_col < a.F_out;  // F_out % 16 == 0: whole column blocks
-    uint32_t m = 0;                   // the column's largest finite magnitude (its 4 lane groups)
-    for (int k = 64 * q; k < 64 * q + 64; ++k) {
-      const uint32_t b = on ? abs_bits(a.W[int64_t(k) * a.F_out + n_col]) : 0u;
-      m = max(m, b < 0x7f800000u ? b : 0u);
-    }
-    m = max(m, uint32_t(__shfl_xor(int(m), 16)));
-    m = max(m, uint32_t(__shfl_xor(int(m), 32)));
-    const int sh = h2_shift(m);
-    if (q == 0 && on) ucol[n_col] = -sh;
-#pragma unroll
-    for (int s = 0; s < kSteps; ++s) {
-      u32x4_t ph, pl;
-#pragma unroll
-      for (int j = 0; j < 8; j += 2) {
-        const int k = 64 * q + 8 * s + j;
-        const float v0 = on ? a.W[int64_t(k) * a.F_out + n_col] : 0.0f;
-        const float v1 = on ? a.W[int64_t(k + 1) * a.F_out + n_col] : 0.0f;
-        uint32_t h, l;
-        split2h_pair(v0, v1, sh, h, l);
-        ph[j / 2] = h;
-        pl[j / 2] = l;
-      }
-      wfh[i][s] = __builtin_bit_cast(bf16x8_t, ph);
-      wfl[i][s] = __builtin_bit_cast(bf16x8_t, pl);
-    }
-  }
-}
-
-// f16x2: one aggregated row (this lane's 4 features; every lane of the wave
-// calls it for the same row) into the two fp16 planes of LDS tile row t,
-// scaled by the row's power of two; returns the row's unscale exponent
-// (wave-uniform: the scale comes from the wave's maximum).
-__device__ __forceinline__ int put_row_h2(short (*tile2)[kRows][kLd], int t, int f, const float (&v)[4]) {
-  const uint32_t m =
-      wave_max_u32(max(max(abs_bits(v[0]), abs_bits(v[1])), max(abs_bits(v[2]), abs_bits(v[3]))));
-  uint32_t h0, l0, h1, l1;
-  int sh;
-  if (m < 0x7f800000u) {
-    sh = h2_shift(m);
-    split2h_pair(v[0], v[1], sh, h0, l0);
-    split2h_pair(v[2], v[3], sh, h1, l1);
-  } else {  // inf / NaN in the row (wave-uniform branch): the scale of its finite values
-    uint32_t mf = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t b = abs_bits(v[k]);
-      mf = max(mf, b < 0x7f800000u ? b : 0u);
-    }
-    sh = h2_shift(wave_max_u32(mf));
-    split2h_pair_nf(v[0], v[1], sh, h0, l0);
-    split2h_pair_nf(v[2], v[3], sh, h1, l1);
-  }
-  *reinterpret_cast<uint2*>(&tile2[0][t][f]) = make_uint2(h0, h1);
-  *reinterpret_cast<uint2*>(&tile2[1][t][f]) = make_uint2(l0, l1);
-  return -sh;
-}
-
-// f16x2 MFMA chain of one k-step for one 16-column block (small terms first)
-__device__ __forceinline__ f32x4 mfma_h2(bf16x8_t wh, bf16x8_t wlo, bf16x8_t xh, bf16x8_t xl, f32x4 d) {
-  const kgx_h8_t Wh = __builtin_bit_cast(kgx_h8_t, wh), Wl = __builtin_bit_cast(kgx_h8_t, wlo);
-  const kgx_h8_t Xh = __builtin_bit_cast(kgx_h8_t, xh), Xl = __builtin_bit_cast(kgx_h8_t, xl);
-  d = __builtin_amdgcn_mfma_f32_16x16x32_f16(Wh, Xl, d, 0, 0, 0);
-  d = __builtin_amdgcn_mfma_f32_16x16x32_f16(Wl, Xh, d, 0, 0, 0);
-  return __builtin_amdgcn_mfma_f32_16x16x32_f16(Wh, Xh, d, 0, 0, 0);
-}
-
-// The epilogue's value: accumulator (unscaled by the row's and column's
-// exponents with f16x2) + bias
-__device__ __forceinline__ float4 unscale_bias(const f32x4& d, int ue, int4 uc, float4 b4) {
-  if constexpr (kH2)
-    return make_float4(__builtin_ldexpf(d[0], ue + uc.x) + b4.x, __builtin_ldexpf(d[1], ue + uc.y) + b4.y,
-                       __builtin_ldexpf(d[2], ue + uc.z) + b4.z, __builtin_ldexpf(d[3], ue + uc.w) + b4.w);
-  return make_float4(d[0] + b4.x, d[1] + b4.y, d[2] + b4.z, d[3] + b4.w);
-}
-
 // One aggregated row (this lane's 4 features) into the split planes of LDS tile row t.
 // Fast path: split3_pair_rn (three packed conversions per pair, equal to
 // split3_a whenever both bf16 values are finite, which split_fast_ok checks);
 // otherwise the per-value split3_a_lo (non-finite values to the lo plane).
-[[maybe_unused]] __device__ __forceinline__ void put_row(short (*tile3)[kRows][kLd], int t, int f, const float (&v)[4]) {
+__device__ __forceinline__ void put_row(short (*tile3)[kRows][kLd], int t, int f, const float (&v)[4]) {
   uint32_t h0, m0, l0, h1, m1, l1;
   split3_pair_rn(v[0], v[1], h0, m0, l0);
   split3_pair_rn(v[2], v[3], h1, m1, l1);
@@ -258,27 +163,17 @@ __device__ __forceinline__ float4 unscale_bias(const f32x4& d, int ue, int4 uc, 
 __device__ __forceinline__ void transform_tile(const F256Args& a, const short (*tile3)[kRows][kLd],
                                                const bf16x8_t (&wfh)[2][kSteps], const bf16x8_t (&wfm)[2][kSteps],
                                                const u32x4_t* wlo, const float* sbias, const int32_t* tile_row,
-                                               const int32_t* tile_ue, const int* ucol, int wave, int wl) {
+                                               int wave, int wl) {
   const int cl = wl & 15, q = wl >> 4;
   const bool mf0 = 32 * wave < a.F_out, mf1 = 32 * wave + 16 < a.F_out;
   if (!mf0) return;
   f32x4 d[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
 #pragma unroll
-  for (int s = 0; s < ((KGX_F256_DBG & 1) ? 0 : kSteps); ++s) {
+  for (int s = 0; s < kSteps; ++s) {
     const int kk = 64 * q + 8 * s;
-    if constexpr (kH2) {  // wfh / wfm hold W's fp16 hi / lo planes
-      const bf16x8_t xh = *reinterpret_cast<const bf16x8_t*>(&tile3[0][cl][kk]);
-      const bf16x8_t xl = *reinterpret_cast<const bf16x8_t*>(&tile3[1][cl][kk]);
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        if (i == 1 && !mf1) break;
-        d[i] = mfma_h2(wfh[i][s], wfm[i][s], xh, xl, d[i]);
-      }
-      continue;
-    }
     const bf16x8_t xh = *reinterpret_cast<const bf16x8_t*>(&tile3[0][cl][kk]);
     const bf16x8_t xm = *reinterpret_cast<const bf16x8_t*>(&tile3[1][cl][kk]);
-    const bf16x8_t xl = *reinterpret_cast<const bf16x8_t*>(&tile3[kPlanes - 1][cl][kk]);
+    const bf16x8_t xl = *reinterpret_cast<const bf16x8_t*>(&tile3[2][cl][kk]);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       if (i == 1 && !mf1) break;
@@ -293,21 +188,19 @@ __device__ __forceinline__ void transform_tile(const F256Args& a, const short (*
   }
   const int rr = tile_row[cl];
   if (rr < 0) return;
-  const int ue = kH2 ? tile_ue[cl] : 0;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     if (i == 1 && !mf1) break;
     const int c4 = 32 * wave + 16 * i + 4 * q;
     float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + c4);
     const float4 b4 = *reinterpret_cast<const float4*>(&sbias[c4]);
-    const int4 uc = kH2 ? *reinterpret_cast<const int4*>(&ucol[c4]) : make_int4(0, 0, 0, 0);
-    float4 v = unscale_bias(d[i], ue, uc, b4);
+    float4 v = make_float4(d[i][0] + b4.x, d[i][1] + b4.y, d[i][2] + b4.z, d[i][3] + b4.w);
     if (a.accumulate) {
       const float4 p = *dst;
       v = make_float4(__fadd_rn(p.x, v.x), __fadd_rn(p.y, v.y), __fadd_rn(p.z, v.z), __fadd_rn(p.w, v.w));
     }
     if (a.relu) v = make_float4(fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f));
-    if (!(KGX_F256_DBG & 2)) *dst = v;
+    *dst = v;
   }
 }
 
@@ -320,13 +213,10 @@ __device__ __forceinline__ void transform_tile(const F256Args& a, const short (*
 #ifndef KGX_F256_MID_PF
 #define KGX_F256_MID_PF 6
 #endif
-// pre_gin: load the rows' own x rows with the next tile's prefetch instead of
-// after the fold, where their latency was exposed once per tile (C4 layer
-// 21.51-21.53 -> 21.20-21.21 ms interleaved; 8 more VGPRs spilled in a kernel
-// already at 256, which costs less than the wait)
-#ifndef KGX_F256_ROOT_PF
-#define KGX_F256_ROOT_PF 1
-#endif
+// pre_gin: the rows' own x rows are loaded with the next tile's prefetch
+// instead of after the fold, where their latency was exposed once per tile
+// (C4 layer 21.51-21.53 -> 21.20-21.21 ms interleaved; 8 more VGPRs spilled
+// in a kernel already at 256, which costs less than the wait)
 template <int RED, bool WEIGHTED, int PF, bool TWO>
 __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_kernel(F256Args a) {
   using R = RowRed<RED>;
@@ -335,21 +225,16 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_kernel(F256Args a) {
 #else
   constexpr int U = 4;  // gathers in flight per row in the two-row loop (8 per wave)
 #endif
-  __shared__ u32x4_t wlo[kH2 ? 1 : kColBlocks * kSteps * 64];  // bf16x3: W lo-plane B-fragments, 128 KB
+  __shared__ u32x4_t wlo[kColBlocks * kSteps * 64];  // W lo-plane B-fragments, 128 KB
   __shared__ __attribute__((aligned(16))) short tile3[kPlanes][kRows][kLd];  // the split planes of the tile's rows
   __shared__ __attribute__((aligned(16))) float sbias[kF];
-  __shared__ __attribute__((aligned(16))) int ucol[kF];  // f16x2: W columns' unscale exponents
   __shared__ int32_t tile_row[kRows];
-  __shared__ int32_t tile_ue[kRows];  // f16x2: tile rows' unscale exponents
 
   const int wave = threadIdx.x >> 6;  // reduces tile rows 2 wave, 2 wave + 1; owns output columns [32 wave, +32)
   const int wl = threadIdx.x & 63;
   const int f = wl * 4;
-  bf16x8_t wfh[2][kSteps], wfm[2][kSteps];  // f16x2: W's hi / lo planes
-  if constexpr (kH2)
-    load_w_h2(a, wave, wl, wfh, wfm, ucol);
-  else
-    load_w(a, wave, wl, wfh, wfm, wlo);
+  bf16x8_t wfh[2][kSteps], wfm[2][kSteps];
+  load_w(a, wave, wl, wfh, wfm, wlo);
   if (threadIdx.x < kF) sbias[threadIdx.x] = (a.bias && int(threadIdx.x) < a.F_out) ? a.bias[threadIdx.x] : 0.0f;
   // (both are first read after the first tile's barrier)
 
@@ -359,9 +244,7 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_kernel(F256Args a) {
   int32_t row[2], beg[2], end[2], slot[2];
   int pn[2];
   float pv[2][PF][4], pw[2][PF];
-#if KGX_F256_ROOT_PF
   float px[2][4];  // pre_gin: the rows' own x rows, loaded with the prefetch
-#endif
   // descriptors of items it, it + 1 and their first PF gathers
   auto fetch = [&](int64_t it) {
     int32_t c[2][PF];
@@ -397,12 +280,10 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_kernel(F256Args a) {
 #pragma unroll
       for (int u = 0; u < PF; ++u)
         if (u < pn[r]) vload<4>(pv[r][u], gsrc256<TWO>(a, c[r][u]) + f);
-#if KGX_F256_ROOT_PF
     if (a.pre_gin) {  // wave-uniform; clamped rows, unconditional per lane
 #pragma unroll
       for (int r = 0; r < 2; ++r) vload<4>(px[r], a.x + int64_t(row[r] >= 0 ? row[r] : 0) * a.ld_x + f);
     }
-#endif
   };
 
   fetch(int64_t(blockIdx.x) * kRows + 2 * wave);
@@ -489,29 +370,18 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_kernel(F256Args a) {
       for (int k = 0; k < 4; ++k) v[k] = full_row ? R::finish(acc[r][k], end[r] - beg[r]) : 0.0f;
       if (full_row && a.pre_gin) {
         float xv[4];
-#if KGX_F256_ROOT_PF
 #pragma unroll
         for (int k = 0; k < 4; ++k) xv[k] = px[r][k];
-#else
-        vload<4>(xv, a.x + int64_t(row[r]) * a.ld_x + f);
-#endif
 #pragma unroll
         for (int k = 0; k < 4; ++k) v[k] = __fadd_rn(__fmul_rn(a.gin_scale, xv[k]), v[k]);
       }
       if (full_row && a.agg_out) vstore<4>(a.agg_out + int64_t(row[r]) * a.ld_agg + f, v);
-      int ue = 0;
-      if constexpr (kH2)
-        ue = put_row_h2(tile3, 2 * wave + r, f, v);
-      else
-        put_row(tile3, 2 * wave + r, f, v);
-      if (wl == 0) {
-        tile_row[2 * wave + r] = full_row ? row[r] : -1;
-        if constexpr (kH2) tile_ue[2 * wave + r] = ue;
-      }
+      put_row(tile3, 2 * wave + r, f, v);
+      if (wl == 0) tile_row[2 * wave + r] = full_row ? row[r] : -1;
     }
     lds_barrier();
     fetch(base + stride + 2 * wave);  // the next tile's first gathers fly during the MFMAs
-    transform_tile(a, tile3, wfh, wfm, wlo, sbias, tile_row, tile_ue, ucol, wave, wl);
+    transform_tile(a, tile3, wfh, wfm, wlo, sbias, tile_row, wave, wl);
     lds_barrier();  // the planes and tile_row are free for the next tile
   }
 }
@@ -536,21 +406,18 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Arg
   using R = RowRed<RED>;
   constexpr int RPW = 2;  // rows per wave per tile
   constexpr int kHalf = kSteps / 2;
-  __shared__ u32x4_t wlo[kH2 ? 1 : kColBlocks * kHalf * 64];  // bf16x3: lo plane, k-steps 4..7: 64 KB
+  __shared__ u32x4_t wlo[kColBlocks * kHalf * 64];  // lo plane, k-steps 4..7: 64 KB
   __shared__ __attribute__((aligned(16))) short tile3[2][kPlanes][kRows][kLd];  // two tiles of split planes
   __shared__ __attribute__((aligned(16))) float sbias[kF];
-  __shared__ __attribute__((aligned(16))) int ucol[kF];  // f16x2: W columns' unscale exponents
   __shared__ int32_t tile_row[2][kRows];
-  __shared__ int32_t tile_ue[2][kRows];  // f16x2: tile rows' unscale exponents
 
   const int wave = threadIdx.x >> 6;
   const int wl = threadIdx.x & 63;
   const int f = wl * 4;
   const int cl = wl & 15, q = wl >> 4;
-  bf16x8_t wfh[2][kSteps], wfm[2][kSteps], wfl[2][kH2 ? 1 : kHalf];  // f16x2: wfh / wfm = W's hi / lo planes
-  if constexpr (kH2) load_w_h2(a, wave, wl, wfh, wfm, ucol);
+  bf16x8_t wfh[2][kSteps], wfm[2][kSteps], wfl[2][kHalf];
 #pragma unroll
-  for (int i = 0; i < (kH2 ? 0 : 2); ++i) {
+  for (int i = 0; i < 2; ++i) {
     const int n_col = 32 * wave + 16 * i + cl;
     const bool on = n_col < a.F_out;
 #pragma unroll
@@ -570,7 +437,7 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Arg
       wfh[i][st] = __builtin_bit_cast(bf16x8_t, ph);
       wfm[i][st] = __builtin_bit_cast(bf16x8_t, pm);
       if (st < kHalf)
-        wfl[i][kH2 ? 0 : st] = __builtin_bit_cast(bf16x8_t, pl);
+        wfl[i][st] = __builtin_bit_cast(bf16x8_t, pl);
       else
         wlo[((2 * wave + i) * kHalf + st - kHalf) * 64 + wl] = pl;
     }
@@ -632,15 +499,8 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Arg
         val[k] = rid[r] >= 0 ? v : 0.0f;
       }
       if (!FAST && rid[r] >= 0 && a.agg_out) vstore<4>(a.agg_out + int64_t(rid[r]) * a.ld_agg + f, val);
-      int ue = 0;
-      if constexpr (kH2)
-        ue = put_row_h2(tile3[pb], RPW * wave + r, f, val);
-      else
-        put_row(tile3[pb], RPW * wave + r, f, val);
-      if (wl == 0) {
-        tile_row[pb][RPW * wave + r] = rid[r];
-        if constexpr (kH2) tile_ue[pb][RPW * wave + r] = ue;
-      }
+      put_row(tile3[pb], RPW * wave + r, f, val);
+      if (wl == 0) tile_row[pb][RPW * wave + r] = rid[r];
     }
   };
   // tile in plane buffer pb times W; FASTS = unconditional stores (every row valid)
@@ -651,25 +511,15 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Arg
     if (!mf0) return;
     f32x4 d[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
 #pragma unroll
-    for (int st = 0; st < ((KGX_F256_DBG & 1) ? 0 : kSteps); ++st) {
+    for (int st = 0; st < kSteps; ++st) {
       const int kk = 64 * q + 8 * st;
-      if constexpr (kH2) {
-        const bf16x8_t xh = *reinterpret_cast<const bf16x8_t*>(&t3[0][cl][kk]);
-        const bf16x8_t xl = *reinterpret_cast<const bf16x8_t*>(&t3[1][cl][kk]);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          if (i == 1 && !mf1) break;
-          d[i] = mfma_h2(wfh[i][st], wfm[i][st], xh, xl, d[i]);
-        }
-        continue;
-      }
       const bf16x8_t xh = *reinterpret_cast<const bf16x8_t*>(&t3[0][cl][kk]);
       const bf16x8_t xm = *reinterpret_cast<const bf16x8_t*>(&t3[1][cl][kk]);
-      const bf16x8_t xl = *reinterpret_cast<const bf16x8_t*>(&t3[kPlanes - 1][cl][kk]);
+      const bf16x8_t xl = *reinterpret_cast<const bf16x8_t*>(&t3[2][cl][kk]);
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         if (i == 1 && !mf1) break;
-        const bf16x8_t wf_lo = st < kHalf ? wfl[i][(st < kHalf && !kH2) ? st : 0]
+        const bf16x8_t wf_lo = st < kHalf ? wfl[i][st < kHalf ? st : 0]
                                           : __builtin_bit_cast(bf16x8_t, wlo[((2 * wave + i) * kHalf + (st >= kHalf ? st - kHalf : 0)) * 64 + wl]);
         d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[i][st], xl, d[i], 0, 0, 0);
         d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf_lo, xh, d[i], 0, 0, 0);
@@ -681,21 +531,19 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Arg
     }
     const int rr = tile_row[pb][cl];
     if (!FASTS && rr < 0) return;
-    const int ue = kH2 ? tile_ue[pb][cl] : 0;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       if (i == 1 && !mf1) break;
       const int c4 = 32 * wave + 16 * i + 4 * q;
       float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + c4);
       const float4 b4 = *reinterpret_cast<const float4*>(&sbias[c4]);
-      const int4 uc = kH2 ? *reinterpret_cast<const int4*>(&ucol[c4]) : make_int4(0, 0, 0, 0);
-      float4 v = unscale_bias(d[i], ue, uc, b4);
+      float4 v = make_float4(d[i][0] + b4.x, d[i][1] + b4.y, d[i][2] + b4.z, d[i][3] + b4.w);
       if (!FASTS && a.accumulate) {
         const float4 p = *dst;
         v = make_float4(__fadd_rn(p.x, v.x), __fadd_rn(p.y, v.y), __fadd_rn(p.z, v.z), __fadd_rn(p.w, v.w));
       }
       if (a.relu) v = make_float4(fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f));
-      if (!(KGX_F256_DBG & 2)) *dst = v;
+      *dst = v;
     }
   };
   // period t (parity p): tile t's MFMAs; tile t+1 folded into buffer p^1; tile

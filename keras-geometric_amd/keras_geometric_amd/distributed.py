@@ -1145,8 +1145,11 @@ class ShardedGCNConv(Layer):
                 with kops.sharing_gpu() if later else contextlib.nullcontext():
                     sg.backend.aggregate_transform(g_b, x_local, self.kernel, bias=bias, out=out, x2=halo,
                                                    accumulate=False)
-                if a_late:
-                    sg.backend.aggregate_transform(g_a, x_local, self.kernel, bias=bias, out=out, accumulate=False)
+                if a_late:  # later groups are still in flight: leave block slots to their RCCL kernels
+                    # (pinned by one-rank simulations only until an N > 1 RCCL run measures it)
+                    with kops.sharing_gpu() if later else contextlib.nullcontext():
+                        sg.backend.aggregate_transform(g_a, x_local, self.kernel, bias=bias, out=out,
+                                                       accumulate=False)
             for n, (i, g, lo, hi) in enumerate(later):
                 wait_step(i)
                 with kops.sharing_gpu() if n + 1 < len(later) else contextlib.nullcontext():

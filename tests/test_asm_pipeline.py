@@ -44,12 +44,16 @@ import isa_hazard_check as H  # noqa: E402
 # (source, extra flags, kernel-name patterns checked; [] = every kernel in the file)
 SOURCES = {
     "spmm": ("spmm.hip", ["-std=c++17"], ["spmm_hub_kernel", "spmm_kernel", "spmm_short_kernel"]),
-    # sum / weighted sum (GCN, GIN) instantiations of the fused 128-wide kernels, tiny tails included
-    "spmm_gemm": ("spmm_gemm.hip", ["-std=c++17"], ["ILi0ELb1E", "ILi0ELb0E"]),
+    # every instantiation of the fused 128-wide kernels: sum, mean, max, min, weighted
+    # or not, one or two tables, narrow or not; short and tiny tails, fix-ups
+    "spmm_gemm": ("spmm_gemm.hip", ["-std=c++17"], ["ILi0E", "ILi1E", "ILi2E", "ILi3E"]),
     "spmm_gemm256": ("spmm_gemm256.hip", ["-std=c++17"], []),
     "dense": ("dense.hip", ["-std=c++20", "-fno-slp-vectorize"], ["dense_kernel"]),
 }
 BARRIER_HANDOFF_OK = ("spmm_hub_kernel",)
+# held to the exec-masked row-load rule too (tools/isa_hazard_check.py): every
+# gather and descriptor load of the 128-wide fused kernels is issued with full exec
+EXEC_RULE = ("spmm_gemm_kernel", "spmm_gemm_short_kernel", "spmm_gemm_tiny_kernel")
 
 
 def _check(job):
@@ -58,7 +62,7 @@ def _check(job):
     import isa_hazard_check as HC
 
     with contextlib.redirect_stdout(io.StringIO()):
-        return name, HC.check_kernel(body, name, 0)
+        return name, HC.check_kernel(body, name, 0, exec_rule=any(p in name for p in EXEC_RULE))
 
 
 def _compile(tmp: Path, key: str) -> str:
@@ -86,7 +90,8 @@ def test_kernels_have_no_inflight_hazards(tmp_path):
             if "at s_barrier" in why and any(p in name for p in BARRIER_HANDOFF_OK):
                 continue
             bad.append(f"{name}: line {line}: {why}: {ins}")
-    assert checked >= 100, checked  # every family present
+    assert checked >= 200, checked  # every family present
+    assert sum(any(p in name for p in EXEC_RULE) for name, _ in jobs) >= 90
     assert not bad, "\n".join(bad[:20])
 
 
@@ -125,3 +130,43 @@ def test_checker_flags_planted_hazards():
                "global_load_dword v1, v[10:11], off", ".LBB0_1:", "s_waitcnt vmcnt(1)",
                "v_mov_b32_e32 v2, v0", "s_endpgm"]
     assert any("read of a register" in w for w in hazards(branchy))
+
+
+def test_exec_rule_flags_masked_prefetch():
+    """The exec-masked row-load rule: a 16-byte gather issued inside an
+    s_and_saveexec region and folded after the region's join (the round-4
+    fused prefetch, `if (u < pn) vload(pv[u])`) is reported; the same gather
+    issued after the join (full exec, the zero-row form) is not; a gather
+    consumed inside its region, or joined only out of an inner loop, is not."""
+    masked = [
+        "k:",
+        "s_and_saveexec_b64 s[0:1], vcc",
+        "s_cbranch_execz .LBB0_1",
+        "global_load_dwordx4 v[4:7], v[10:11], off",
+        ".LBB0_1:",
+        "s_or_b64 exec, exec, s[0:1]",
+        "s_waitcnt vmcnt(0)",
+        "v_mul_f32_e32 v8, v4, v9",
+        "s_endpgm",
+    ]
+
+    def hazards(lines):
+        with contextlib.redirect_stdout(io.StringIO()):
+            return [why for (_, why), _ in H.check_kernel(lines, "t", 0, exec_rule=True)]
+
+    assert any("exec-masked" in w for w in hazards(masked))
+    # off by default (the hand-pipelined kernels are checked for wait counts only)
+    with contextlib.redirect_stdout(io.StringIO()):
+        assert H.check_kernel(masked, "t", 0) == []
+    full = ["k:", "s_and_saveexec_b64 s[0:1], vcc", "s_cbranch_execz .LBB0_1", "v_mov_b32_e32 v10, v12",
+            ".LBB0_1:", "s_or_b64 exec, exec, s[0:1]", "global_load_dwordx4 v[4:7], v[10:11], off",
+            "s_waitcnt vmcnt(0)", "v_mul_f32_e32 v8, v4, v9", "s_endpgm"]
+    assert hazards(full) == []
+    inside = masked[:4] + ["s_waitcnt vmcnt(0)", "v_mul_f32_e32 v8, v4, v9"] + masked[4:6] + ["s_endpgm"]
+    assert hazards(inside) == []
+    # a divergent loop inside the region: its exit join does not leave the load's region
+    loop = ["k:", "s_and_saveexec_b64 s[0:1], vcc", "global_load_dwordx4 v[4:7], v[10:11], off",
+            "s_mov_b64 s[2:3], 0", ".LBB0_2:", "s_or_b64 s[2:3], vcc, s[2:3]", "s_andn2_b64 exec, exec, s[2:3]",
+            "s_cbranch_execnz .LBB0_2", "s_or_b64 exec, exec, s[2:3]", "s_waitcnt vmcnt(0)",
+            "v_mul_f32_e32 v8, v4, v9", "s_or_b64 exec, exec, s[0:1]", "s_endpgm"]
+    assert hazards(loop) == []

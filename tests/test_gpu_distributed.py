@@ -435,3 +435,70 @@ def test_sharded_gcn_no_halo_hip(dev):
     ref = layer([x, ei]).detach().cpu().numpy()
     got = np.concatenate([res[r][0] for r in range(world)])
     assert (np.abs(got - ref) / np.maximum(1.0, np.abs(ref))).max() <= 1e-5
+
+
+def _run_wide_rank(rank, hub, dev, x128, x256, out):
+    try:
+        comm = ThreadComm(hub, rank)
+        res = {}
+        # GIN sum, 128 -> first Dense 128: the fused two-table pass with GIN's
+        # pre-scale (kgx_spmm_gemm_ex3, x2 + KGX_FUSED_PRE_GIN)
+        sg = kd.ShardedGraph.rmat(N, E, seed=10, device=dev, comm=comm, n_features=128, self_loops=False,
+                                  gcn_norm=False, halo_chunks=2)
+        gin = kd.ShardedGINConv(32, sg, mlp_hidden=[128], aggregator="sum", eps_init=0.5)
+        xl = x128[sg.lo: sg.lo + sg.n_local]
+        assert gin._fused(xl.contiguous())
+        with torch.no_grad():
+            res["gin"] = (gin(xl).cpu().numpy(), gin.conv.get_weights())
+        # GCN 256 -> 256: the weighted two-table 256-wide kernels (kgx_spmm_gemm_f256_ex)
+        sg2 = kd.ShardedGraph.rmat(N, E, seed=11, device=dev, comm=comm, n_features=256, halo_chunks=2)
+        gcn = kd.ShardedGCNConv(256, sg2)
+        xl2 = x256[sg2.lo: sg2.lo + sg2.n_local]
+        with torch.no_grad():
+            res["gcn"] = (gcn(xl2).cpu().numpy(), [gcn.kernel.detach().cpu().numpy()])
+        torch.cuda.synchronize()
+        out[rank] = res
+    except BaseException as e:
+        out[rank] = e
+        hub.barrier.abort()
+
+
+def test_sharded_fused_two_table_gin128_gcn256(dev):
+    """The fused two-table passes the sharded layers route to: GIN
+    sum at F_in 128 with a 128-unit first Dense (pre-scale with two tables in
+    the 128-wide kernels) and GCN 256 -> 256 (the 256-wide weighted kernels),
+    against the single-GPU layers with rank 0's weights, within the forward-
+    error bound of the re-associated row sums."""
+    import keras_geometric_amd as kgx
+    from keras_geometric_amd import synthetic
+
+    world = 2
+    x128 = torch.randn(N, 128, generator=torch.Generator().manual_seed(5)).to(dev)
+    x256 = torch.randn(N, 256, generator=torch.Generator().manual_seed(6)).to(dev)
+    hub = ThreadHub(world)
+    res = {}
+    threads = [threading.Thread(target=_run_wide_rank, args=(r, hub, dev, x128, x256, res)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=240)
+    for r in range(world):
+        if isinstance(res.get(r), BaseException):
+            raise res[r]
+    for key, seed, x, make in (
+            ("gin", 10, x128, lambda: kgx.GINConv(32, mlp_hidden=[128], aggregator="sum", eps_init=0.5, exact=True)),
+            ("gcn", 11, x256, lambda: kgx.GCNConv(256, exact=True))):
+        ei = synthetic.rmat_edge_index(N, E, seed=seed, device=dev)
+        w = res[0][key][1]
+        if key == "gcn":
+            w = w + [np.zeros(256, np.float32)]
+        layer, layer_abs = make(), make()
+        layer([x, ei])
+        layer.set_weights(w)
+        ref = layer([x, ei]).detach().cpu().numpy()
+        layer_abs([x, ei])
+        layer_abs.set_weights([np.abs(a) for a in w])
+        scale = np.abs(layer_abs([x.abs(), ei]).detach().cpu().numpy())
+        got = np.concatenate([res[r][key][0] for r in range(world)])
+        err = np.abs(got - ref) / np.maximum(1.0, scale)
+        assert err.max() <= 1e-5, (key, err.max())

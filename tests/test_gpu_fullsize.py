@@ -127,17 +127,43 @@ def test_tiny_tail_bit_identical_fullsize(big):
     gen = torch.Generator(device=x.device).manual_seed(7)
     W = torch.randn(F, F, device=x.device, generator=gen) * (1.0 / F) ** 0.5
     b = torch.randn(F, device=x.device, generator=gen)
+    import fused_ref
+
     saved = g._kgx_tiny
     assert saved[0] is not None
     for red, weighted in (("sum", True), ("max", False)):
+        ref = fused_ref.reference(g, x, W, red, weighted, b)
         y_tiny = kops.aggregate_transform(g, x, W, red, weighted=weighted, bias=b)
+        fused_ref.check(y_tiny, g, ref, f"NS {red} tail on records")
         g._kgx_tiny = (None, None, -1, 0)
         try:
             y_short = kops.aggregate_transform(g, x, W, red, weighted=weighted, bias=b)
+            fused_ref.check(y_short, g, ref, f"NS {red} tail on short rows")
         finally:
             g._kgx_tiny = saved
         assert torch.equal(y_tiny, y_short), red
-        del y_tiny, y_short
+        del y_tiny, y_short, ref
+
+
+@pytest.mark.parametrize("red", ["sum", "mean", "max", "min"])
+def test_ns_fused_all_reductions_vs_reference(big, red):
+    """aggregate_transform at the north-star size (hundreds of 16-row tiles per
+    block of the main kernel, hundreds of 64-row tiles per block of the tiny
+    kernel), every reduction, weighted and not, against the float64
+    restatement on EVERY row (tests/fused_ref.py: a failure names the row,
+    feature and kernel).  Round 4's one wrong row came from the weighted min."""
+    import fused_ref
+
+    _, g, x = big
+    gen = torch.Generator(device=x.device).manual_seed(13)
+    W = torch.randn(F, F, device=x.device, generator=gen) * 0.1
+    b = torch.randn(F, device=x.device, generator=gen)
+    for weighted in (True, False):
+        ref = fused_ref.reference(g, x, W, red, weighted, b)
+        y = kops.aggregate_transform(g, x, W, red, weighted=weighted, bias=b)
+        mx = fused_ref.check(y, g, ref, f"NS {red} weighted={weighted}")
+        print(f"NS fused {red} weighted={weighted}: max scaled err {mx:.3e} over {g.n_dst} rows")
+        del y, ref
 
 
 def test_ns_gcn_layer_vs_oracle_sampled(big):
@@ -174,7 +200,10 @@ def test_fused_kernels_run_to_run_bit_identical(big):
     gen = torch.Generator(device=x.device).manual_seed(11)
     W = torch.randn(F, F, device=x.device, generator=gen) * (1.0 / F) ** 0.5
     b = torch.randn(F, device=x.device, generator=gen)
+    import fused_ref
+
     first = kops.aggregate_transform(g, x, W, "sum", weighted=True, bias=b)
+    fused_ref.check(first, g, fused_ref.reference(g, x, W, "sum", True, b), "NS weighted sum, first launch")
     for i in range(9):
         assert torch.equal(kops.aggregate_transform(g, x, W, "sum", weighted=True, bias=b), first), i
     del first
@@ -187,5 +216,7 @@ def test_fused_kernels_run_to_run_bit_identical(big):
     assert kops.fused_transform_supported(f, f)
     kw = dict(bias=b2, pre_gin=True, gin_scale=1.25)
     first = kops.aggregate_transform(g2, x2, W2, "sum", **kw)
+    fused_ref.check(first, g2, fused_ref.reference(g2, x2, W2, "sum", False, b2, pre_gin=True, gin_scale=1.25),
+                    "256-wide GIN sum, first launch")
     for i in range(9):
         assert torch.equal(kops.aggregate_transform(g2, x2, W2, "sum", **kw), first), i

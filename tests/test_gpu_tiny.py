@@ -38,15 +38,22 @@ def _with_tiny(g):
 @pytest.mark.parametrize("red", ["sum", "mean", "max", "min"])
 @pytest.mark.parametrize("weighted", [True, False])
 def test_tiny_tail_bit_identical(dev, red, weighted):
+    """Each launch is first held to the float64 restatement on every row
+    (tests/fused_ref.py), so a wrong row is named with its kernel; then the two
+    launches must agree bit for bit."""
+    import fused_ref
+
     g, _ = _graph(dev, self_loops=True, gcn_norm=True)
     gen = torch.Generator(device=dev).manual_seed(1)
     x = torch.randn(g.rowptr.numel() - 1, 128, device=dev, generator=gen)
     W = torch.randn(128, 128, device=dev, generator=gen) * 0.1
     b = torch.randn(128, device=dev, generator=gen)
+    ref = fused_ref.reference(g, x, W, red, weighted, b)
     outs = []
     for on in (False, True):
         _with_tiny(g) if on else _no_tiny(g)
         outs.append(kops.aggregate_transform(g, x, W, red, weighted=weighted, bias=b))
+        fused_ref.check(outs[-1], g, ref, f"{red} weighted={weighted} tail on {'records' if on else 'short rows'}")
     torch.testing.assert_close(outs[1], outs[0], rtol=0, atol=0)
 
 

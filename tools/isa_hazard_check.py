@@ -26,10 +26,27 @@ clobbers it); the barrier hand-offs above.  Inline asm (`;;#ASMSTART`) is
 treated like compiled code: the point is to check hand-counted waits
 (spmm_hub_kernel, dense_kernel) together with everything hipcc emitted.
 
-Not modelled: exec masks (a masked-off lane's register is treated as
-written), instruction-level hazards the hardware resolves by s_nop (VALU ->
-DPP / MFMA forwarding), and which LDS bytes a barrier actually hands off (any
-LDS op in flight at a barrier counts).
+Exec-masked row loads (round 5; check_kernel(exec_rule=True)): a 16-byte VMEM load (a row gather or a
+record / item descriptor) issued while exec is not known to be full (inside
+an s_and_saveexec region or a divergent loop) writes only the active lanes;
+the other lanes keep the register's older value.  If such a register is then
+read as data (a floating-point / select / MFMA / packed op, not address
+arithmetic) after exec was widened again (s_or_b64 / s_mov_b64 / s_xor_b64
+exec: the join of a divergent region) and before anything rewrote it, a
+partial write crosses a join -- the pattern of the round-4 fused kernels'
+prefetch (`if (u < pn) vload(pv[u], ...)`, folded at the next tile).  The
+hardware does what the ISA says here; the rule marks a form whose
+correctness rests on the register allocator keeping the masked lanes, which
+the 128-wide fused kernels now avoid (every gather and descriptor load is
+issued with full exec; absent edges read kgx_zero_row).  Reported as "data
+read of a register an exec-masked 16-byte load wrote, after an exec join"
+(tests/test_asm_pipeline.py holds those kernels to zero).
+
+Not modelled: which lanes a mask holds (any partial exec counts), partial
+writes by VALU instructions (loop-carried sums under a divergent loop are the
+compiler's ordinary phis), instruction-level hazards the hardware resolves by
+s_nop (VALU -> DPP / MFMA forwarding), and which LDS bytes a barrier actually
+hands off (any LDS op in flight at a barrier counts).
 """
 
 from __future__ import annotations
@@ -89,12 +106,14 @@ class State:
     ds: {reg: younger LDS-op count}; ds_w / ds_r: pending LDS writes / reads
     (younger LDS-op counts); sm: regs of pending scalar loads."""
 
-    __slots__ = ("vm", "vm_n", "ds", "ds_w", "ds_r", "sm", "line")
+    __slots__ = ("vm", "vm_n", "ds", "ds_w", "ds_r", "sm", "pm", "ex", "line")
 
     def __init__(self):
         self.vm, self.vm_n = {}, frozenset()
         self.ds, self.ds_w, self.ds_r = {}, frozenset(), frozenset()
         self.sm = set()
+        self.pm = {}  # reg -> (crossed a join out of its region, load line, region depth): exec-masked load dst
+        self.ex = ()  # exec narrowings in force (saved-mask pairs / "n"); () = every lane of the wave on
         self.line = -1
 
     def copy(self):
@@ -102,11 +121,14 @@ class State:
         s.vm, s.vm_n = dict(self.vm), self.vm_n
         s.ds, s.ds_w, s.ds_r = dict(self.ds), self.ds_w, self.ds_r
         s.sm = set(self.sm)
+        s.pm = dict(self.pm)
+        s.ex = self.ex
         return s
 
     def key(self):
         return (tuple(sorted(self.vm.items())), tuple(sorted(self.vm_n)), tuple(sorted(self.ds.items())),
-                tuple(sorted(self.ds_w)), tuple(sorted(self.ds_r)), tuple(sorted(self.sm)))
+                tuple(sorted(self.ds_w)), tuple(sorted(self.ds_r)), tuple(sorted(self.sm)),
+                tuple(sorted(self.pm.items())), self.ex)
 
     def join(self, o: "State") -> "State":
         """Pending on either path; younger counts: the minimum (the worst case)."""
@@ -119,11 +141,75 @@ class State:
         for name in ("vm_n", "ds_w", "ds_r"):
             setattr(s, name, getattr(self, name) | getattr(o, name))
         s.sm = self.sm | o.sm
+        for r in set(self.pm) | set(o.pm):
+            s.pm[r] = max(self.pm.get(r, (False, -1, 0)), o.pm.get(r, (False, -1, 0)))
+        s.ex = max(self.ex, o.ex, key=lambda e: (len(e), str(e)))  # the more narrowed (conservative)
         return s
 
 
-def step(st: State, line: str, report) -> State:
+# data uses (not address arithmetic): float / select / conversion / packed / matrix ops
+_DATA_READ = re.compile(r"^v_(\w*_f32|\w*_f16|\w*bf16\w*|cndmask\w*|pk_\w+|mfma\w*|max\w*|min\w*|med3\w*|perm\w*)")
+_EXEC_WIDEN = ("s_or_b64", "s_mov_b64", "s_xor_b64", "s_or_saveexec_b64", "s_andn2_saveexec_b64", "s_not_b64")
+
+
+def _exec_step(st: State, op: str, toks: list, line: str, report) -> None:
+    """The exec-masked load rule (module docstring): reads of crossed registers,
+    then this instruction's effect on the partial-write set."""
+    kind = classify(op, line)
+    if not toks or kind == "wait":
+        return
+    load = kind in ("vmem_load", "vmem_atomic_ret")
+    writes_dst = kind in ("vmem_load", "vmem_atomic_ret", "ds_read") or (
+        kind in ("alu", "smem") and not op.startswith(("s_cmp", "s_bitcmp", "s_cbranch", "s_branch", "s_nop", "s_set",
+                                                      "s_sleep", "s_endpgm", "s_sendmsg", "s_waitcnt", "s_barrier")))
+    dst = parse_regs(toks[0]) if writes_dst else set()
+    srcs = set()
+    for t in (toks[1:] if writes_dst else toks):
+        srcs |= parse_regs(t)
+    if op.startswith("v_pk_") and writes_dst:
+        srcs = _pk_sources(toks, line)
+    crossed = sorted(r for r in srcs if st.pm.get(r, (False,))[0])
+    if crossed and _DATA_READ.match(op):
+        report("data read of a register an exec-masked 16-byte load wrote, after an exec join"
+               f" [loads at lines {sorted({st.pm[r][1] for r in crossed})}]", line)
+    for r in dst:
+        st.pm.pop(r, None)
+    if load and st.ex and len(dst) >= 4:
+        for r in dst:
+            st.pm[r] = (False, st.line, len(st.ex))
+    # the structured exec stack hipcc emits: s_and_saveexec s[x] opens a region,
+    # s_and(n2)_b64 exec, exec, .. narrows (divergent loops, masked stores),
+    # s_or_b64 exec, exec, s[x] / s_mov_b64 exec, s[x] closes back to x
+    if op in ("s_and_saveexec_b64", "s_andn2_saveexec_b64", "s_or_saveexec_b64"):
+        x = _pair(toks[0])
+        ex = list(st.ex)
+        if op != "s_and_saveexec_b64" and ex:
+            # the else branch of the region just opened (s_and_saveexec s[y]; s_xor
+            # s[x], exec, s[y]; s_andn2_saveexec s[x], s[x]): s[x] now closes it
+            ex = ex[:-1]
+        st.ex = (tuple(ex) + (x,))[-6:]  # bounded (a fixed point over loops)
+    elif toks[0] == "exec":
+        if op in ("s_and_b64", "s_andn2_b64"):
+            if not st.ex or st.ex[-1] != "n":  # a divergent loop narrows once per iteration: one entry
+                st.ex = (st.ex + ("n",))[-6:]
+        else:
+            x = _pair(toks[2]) if op == "s_or_b64" and len(toks) == 3 else (_pair(toks[1]) if len(toks) == 2 else None)
+            ex = list(st.ex)
+            if x in ex:
+                ex = ex[: ex.index(x)]
+            else:  # a loop's exit mask (not a saved region): undo the loop's narrowing
+                while ex and ex[-1] == "n":
+                    ex.pop()
+            st.ex = tuple(ex)
+        if op in _EXEC_WIDEN and st.pm:  # a join that leaves the load's region: the value crosses it
+            d = len(st.ex)
+            st.pm = {r: (c or d < dep, ln, dep) for r, (c, ln, dep) in st.pm.items()}
+
+
+def step(st: State, line: str, report, exec_rule: bool = False) -> State:
     op, toks = operands(line)
+    if exec_rule:
+        _exec_step(st, op, toks, line, report)
     kind = classify(op, line)
     pend = set(st.vm) | set(st.ds) | st.sm
     if kind == "wait":
@@ -380,9 +466,13 @@ def flags_step(flags: dict, line: str) -> dict:
     return f
 
 
-def check_kernel(body: list, name: str, verbose: int = 5) -> list:
+def check_kernel(body: list, name: str, verbose: int = 5, exec_rule: bool = False) -> list:
     """Path-sensitive in the scalar flags (flags_step): a block's entry states
-    are kept per flag assignment and joined only within one."""
+    are kept per flag assignment and joined only within one.  exec_rule: also
+    apply the exec-masked row-load rule (module docstring) -- the kernels built
+    to it (the 128-wide fused ones); the hand-pipelined kernels keep exec-masked
+    loads by design (role branches, masked descriptor loads) and are checked
+    for their wait counts only."""
     lines = []
     for l in body:
         l = l.split(";")[0].strip()
@@ -409,7 +499,7 @@ def check_kernel(body: list, name: str, verbose: int = 5) -> list:
             if not l or l.startswith(".") or l.endswith(":"):
                 continue
             st.line = k
-            st = step(st, l, lambda why, ins_, k=k: hazards.setdefault((k, why), ins_))
+            st = step(st, l, lambda why, ins_, k=k: hazards.setdefault((k, why), ins_), exec_rule)
             flags = flags_step(flags, l)
             last = l
         nxt = list(succ[i])
