@@ -96,8 +96,9 @@ def pmc_traffic(config: str, kernels) -> tuple[float | None, str | None]:
 
 
 def log(msg: str) -> None:
-    if int(os.environ.get("RANK", "0")) == 0:
-        print(f"[bench] {msg}", file=sys.stderr, flush=True)
+    r = int(os.environ.get("RANK", "0"))
+    if r == 0 or int(os.environ.get("WORLD_SIZE", "1")) > 1:  # N > 1: every rank reports its own progress
+        print(f"[bench r{r}] {msg}", file=sys.stderr, flush=True)
 
 
 def host_cpus() -> dict:
@@ -360,13 +361,20 @@ def main() -> None:
             with torch.no_grad():
                 return layer([x, ei])
     else:
+        from keras_geometric_amd.distributed import heartbeat
+
         log(f"world={world}: generating shards of R-MAT N={n_global} E={e_global}")
         t0 = time.perf_counter()
-        sg, x, layer = _build_sharded(kind, n_global, e_global, f_in, f_out, args.seed, args.exact, dev, comm)
+        # a line per rank at least every KGX_HEARTBEAT_S (30 s) while the shard
+        # build and the first forward (plans, the KGX_TUNE_BUDGET_S-bounded
+        # exchange tuner) run, so a stall names its rank and phase
+        with heartbeat(rank, "shard build"):
+            sg, x, layer = _build_sharded(kind, n_global, e_global, f_in, f_out, args.seed, args.exact, dev, comm)
+            torch.cuda.synchronize()
         log(f"shard graph built in {time.perf_counter() - t0:.1f} s; first forward (plans, exchange tuner)")
-        with torch.no_grad():
+        with heartbeat(rank, "first forward (plans, exchange tuner)"), torch.no_grad():
             layer(x)  # build, plans, and (GCN) the halo chunk count measured at the first forward
-        torch.cuda.synchronize()
+            torch.cuda.synchronize()
         graph_build_ms = first_call_ms = (time.perf_counter() - t0) * 1e3  # incl. shard generation + halo plan
         e_agg, n_rows, max_deg = sg.graph.kept, sg.n_local, sg.graph.max_degree
 

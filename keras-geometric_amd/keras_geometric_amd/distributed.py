@@ -32,6 +32,8 @@ from __future__ import annotations
 
 import contextlib
 import os
+import sys
+import threading
 import time
 from dataclasses import dataclass
 
@@ -92,6 +94,11 @@ class KgxBackend:
 
     def restrict_rows(self, g, row_mask):
         return G.restrict_rows(g, row_mask)
+
+    def gatv2(self, g, h_src, h_dst, att, heads, channels, negative_slope, bias=None, exact=False):
+        """GATv2 attention over g (kgx_gatv2: score, segment softmax, weighted
+        sum, + bias); h_src rows index g's sources, h_dst its rows."""
+        return kops.gatv2_aggregate(g, h_src, h_dst, att, heads, channels, negative_slope, bias=bias, exact=exact)
 
     def aggregate(self, g, table, reduce="sum", weighted=False, epilogue=nat.EPI_NONE, bias=None, xroot=None,
                   gin_scale=1.0, exact=False):
@@ -181,13 +188,45 @@ def _inference_only(layer: Layer, weights) -> None:
             "training runs on the single-GPU layers")
 
 
-def _progress(sg, msg: str) -> None:
-    """One progress line on stderr from rank 0 when KGX_LOG is set (bench.py
-    sets it for N > 1: long first forwards -- the exchange tuner -- stay visible)."""
-    if os.environ.get("KGX_LOG") and sg.rank == 0:
-        import sys
+# where progress and heartbeat lines go (stderr; tests substitute a buffer)
+LOG_STREAM = None
 
-        print(f"[kgx] {msg}", file=sys.stderr, flush=True)
+
+def _log_line(rank: int, msg: str) -> None:
+    print(f"[kgx r{rank}] {msg}", file=LOG_STREAM or sys.stderr, flush=True)
+
+
+def _progress(sg, msg: str) -> None:
+    """One progress line per rank on stderr when KGX_LOG is set (bench.py sets
+    it for N > 1: the shard build, each exchange plan and each tuner
+    candidate stay visible, rank by rank, so a stalled rank is named)."""
+    if os.environ.get("KGX_LOG"):
+        _log_line(sg.rank, msg)
+
+
+@contextlib.contextmanager
+def heartbeat(rank: int, what: str, every_s: float | None = None):
+    """While the block runs, a line '[kgx r<rank>] <what>: running, <t> s' every
+    KGX_HEARTBEAT_S seconds (default 30) from a daemon thread, plus one when
+    it ends: a first forward that stalls (a collective waiting on a peer, a
+    long tune) is reported, not silent.  bench.py wraps the N > 1 shard build
+    and first forward in it."""
+    every = float(os.environ.get("KGX_HEARTBEAT_S", "30")) if every_s is None else float(every_s)
+    stop = threading.Event()
+    t0 = time.perf_counter()
+
+    def beat():
+        while not stop.wait(every):
+            _log_line(rank, f"{what}: running, {time.perf_counter() - t0:.0f} s")
+
+    th = threading.Thread(target=beat, name=f"kgx-heartbeat-{rank}", daemon=True)
+    th.start()
+    try:
+        yield
+    finally:
+        stop.set()
+        th.join(timeout=5)
+        _log_line(rank, f"{what}: done in {time.perf_counter() - t0:.1f} s")
 
 
 def equal_bounds(n_global: int, world: int) -> list[int]:
@@ -338,6 +377,7 @@ class ShardedGraph:
     merge_unit: str | None = None  # merged_passes' unit ("step" / "chunk" / "none"); None: KGX_HALO_MERGE or "step"
     tuning_s: float | None = None  # wall time tune_exchange took on this rank
     tuning_skipped: int = 0  # candidates left untimed once KGX_TUNE_BUDGET_S was spent
+    self_loops: bool = True  # the shard graph carries utils/main.py:8-16's self loops (GCN, GATv2)
 
     @property
     def lo(self) -> int:
@@ -373,6 +413,9 @@ class ShardedGraph:
             raise ValueError("ShardedGraph.build: an edge's destination lies outside this rank's range")
         if src.numel() and (int(src.min()) < 0 or int(src.max()) >= bounds[-1]):
             raise IndexError("ShardedGraph.build: source id outside the global node range")
+        log = bool(os.environ.get("KGX_LOG"))
+        if log:
+            _log_line(rank, f"shard build: rows [{lo}, {hi}), {src.numel()} in-edges; halo request lists")
         local = (src >= lo) & (src < hi)
         halo_ids = torch.unique(src[~local])  # sorted -> grouped by owner
         bt = torch.tensor(bounds[1:-1], dtype=torch.long, device=dev)
@@ -398,11 +441,14 @@ class ShardedGraph:
             col = torch.cat([col, ar])
             row = torch.cat([row, ar])
         n_src = n_local + int(halo_ids.numel())
+        if log:
+            _log_line(rank, f"shard build: {halo_ids.numel()} halo rows; shard CSR + schedule")
         g = backend.build_graph(col.to(torch.int32).contiguous(), row.to(torch.int32).contiguous(), n_src, n_local,
                                 n_features)
         sg = cls(rank=rank, world=world, n_global=bounds[-1], bounds=list(bounds), graph=g,
                  send_counts=send_counts, recv_counts=recv_counts, halo_ids=halo_table_ids.to(torch.int32),
-                 chunks=chunks, dinv_table=None, backend=backend, comm=comm, exact=exact, chunks_fixed=chunks_fixed)
+                 chunks=chunks, dinv_table=None, backend=backend, comm=comm, exact=exact, chunks_fixed=chunks_fixed,
+                 self_loops=self_loops)
         if gcn_norm:
             dinv_local = backend.dinv(g.deg)
             table = torch.empty((n_src, 1), dtype=torch.float32, device=dev)
@@ -1329,3 +1375,48 @@ class ShardedSAGEConv(_ShardedWrap):
             else:
                 aggr = sg.propagate(x_local, conv.actual_aggregator)
             return conv.update_nodes(x_local, aggr)
+
+
+class ShardedGATv2Conv(_ShardedWrap):
+    """GATv2Conv over a ShardedGraph (gatv2_conv.py:176-352 per shard).
+
+    h = x W on the owner's rows (the layer's shared linear map, kgx_dense), the
+    halo's h rows pulled over the shard's all-to-all plan, then ONE fused
+    attention pass (kgx_gatv2) over [own h | halo h]: every destination's
+    scores, segment softmax (gatv2_conv.py:291-311) and alpha-weighted sum run
+    on its owner, whose shard CSR holds all of that row's in-edges in global
+    input order -- so EXACT mode is bit-identical to the single-GPU layer.  The
+    halo moves h, not partial sums: the softmax of a row needs every score
+    a . leaky_relu(h_i + h_j), and h_i lives on the owner only.  Shard graph:
+    self loops iff the layer adds them (default), no GCN norm
+    (ShardedGraph.build(..., gcn_norm=False)).  Inference engine, like the
+    other sharded layers."""
+
+    def __init__(self, output_dim: int, sg: ShardedGraph, **gat_kwargs):
+        from .layers.gatv2_conv import GATv2Conv
+
+        super().__init__(GATv2Conv(output_dim, exact=sg.exact, **gat_kwargs), sg)
+        if self.conv.add_self_loops_flag != sg.self_loops:
+            raise ValueError(f"ShardedGATv2Conv: add_self_loops={self.conv.add_self_loops_flag} needs a shard graph "
+                             f"built with self_loops={self.conv.add_self_loops_flag}")
+
+    def forward(self, x_local: torch.Tensor, training=None) -> torch.Tensor:
+        self._ensure_built(x_local)
+        _inference_only(self, self.conv.weights)
+        sg, conv = self.sg, self.conv
+        H, C = conv.heads, conv.features_per_head
+        n = sg.n_local
+        use_b = conv.use_bias and conv.bias is not None
+        with torch.no_grad():
+            h = sg.backend.transform(x_local.contiguous(), conv.linear_transform.kernel)
+            table = sg.new_table(H * C, h)
+            table[:n] = h
+            del h
+            sg.halo_exchange(table)
+            out = sg.backend.gatv2(sg.graph, table, table[:n], conv.att, H, C, conv.negative_slope,
+                                   bias=conv.bias if (use_b and conv.concat) else None, exact=sg.exact)
+            if not conv.concat:  # gatv2_conv.py:341-346
+                out = out.view(n, H, C).mean(dim=1)
+                if use_b:
+                    out = out + conv.bias
+        return out

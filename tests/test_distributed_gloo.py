@@ -123,6 +123,30 @@ class OracleBackend:
         return out
 
 
+def _oracle_gatv2(g, h_src, h_dst, att, heads, channels, negative_slope, bias=None, exact=False):
+    """GATv2 attention over a shard CSR with the oracle's ops in its order
+    (oracle/reference.py gatv2_forward, gatv2_conv.py:241-352): per-edge score,
+    segment max / exp / segment sum by destination, alpha-weighted sum of h_j."""
+    n = g.n_dst
+    rows = torch.repeat_interleave(torch.arange(n), g.deg.long())
+    hs = h_src.reshape(-1, heads, channels)
+    hd = h_dst.reshape(-1, heads, channels)
+    h_j = K.take(hs, g.col.long(), axis=0)
+    h_i = K.take(hd, rows, axis=0)
+    z = K.leaky_relu(K.add(h_i, h_j), negative_slope)
+    scores = torch.sum(K.multiply(z, K.convert(att)), dim=-1)
+    mx = K.segment_max(scores, rows, n)
+    ex = torch.exp(torch.subtract(scores, K.take(mx, rows, axis=0)))
+    ssum = K.segment_sum(ex, rows, n)
+    alpha = K.divide(ex, K.add(K.take(ssum, rows, axis=0), 1e-10))
+    msg = torch.unsqueeze(alpha, -1) * h_j
+    out = K.segment_sum(msg.reshape(-1, heads * channels), rows, n)
+    return out + K.convert(bias) if bias is not None else out
+
+
+OracleBackend.gatv2 = staticmethod(_oracle_gatv2)
+
+
 class UnfusedOracleBackend(OracleBackend):
     def supports_fused(self, f_in, f_out):
         return False
@@ -580,3 +604,139 @@ def test_sharded_uneven_halo_tuner_agrees():
                       torch.from_numpy(b)).numpy()
     got = np.concatenate([res[r][4] for r in range(world)])
     assert (np.abs(got - y) / np.maximum(1, np.abs(y))).max() <= 1e-5
+
+
+def _gat_worker(rank, world, port, q):
+    """ShardedGATv2Conv (concat and mean over heads) on a shard graph with self loops."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        s, d, x, _, _ = _graph()
+        bounds = kd.equal_bounds(N, world)
+        lo, hi = bounds[rank], bounds[rank + 1]
+        keep = (d >= lo) & (d < hi)
+        sg = kd.ShardedGraph.build(torch.from_numpy(s[keep]), torch.from_numpy(d[keep]), bounds,
+                                   backend=OracleBackend(), n_features=F_IN, gcn_norm=False, halo_chunks=2)
+        assert sg.n_halo > 0
+        xl = torch.from_numpy(x[lo:hi])
+        outs = []
+        for layer in (kd.ShardedGATv2Conv(4, sg, heads=3, bias_initializer="glorot_uniform"),
+                      kd.ShardedGATv2Conv(5, sg, heads=2, concat=False, negative_slope=0.1,
+                                          bias_initializer="glorot_uniform")):
+            layer._ensure_built(xl)
+            with pytest.raises(NotImplementedError):  # inference-only
+                layer(xl)
+            with torch.no_grad():
+                outs.append((layer(xl).numpy(), list(layer.conv.get_weights())))
+        with pytest.raises(ValueError):  # a shard graph without loops for a layer that adds them
+            sg_nl = kd.ShardedGraph.build(torch.from_numpy(s[keep]), torch.from_numpy(d[keep]), bounds,
+                                          backend=OracleBackend(), n_features=F_IN, self_loops=False,
+                                          gcn_norm=False)
+            kd.ShardedGATv2Conv(4, sg_nl)
+        q.put((rank, outs))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_sharded_gatv2_layer_bitwise():
+    """ShardedGATv2Conv at world 2 (pulled h halo in two chunks, one attention
+    pass per owner) equals oracle.reference.gatv2_forward on the whole graph
+    with rank 0's weights BIT FOR BIT: every destination's scores, softmax and
+    weighted sum run on its owner over its in-edges in global input order
+    (gatv2_conv.py:176-352)."""
+    if torch.cuda.is_initialized():
+        pytest.skip("never start processes from a process that has initialised the GPU")
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gat_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=90) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    s, d, x, _, _ = _graph()
+    X, EI = torch.from_numpy(x), torch.from_numpy(np.stack([s, d]))
+    for i, (heads, concat, slope) in enumerate(((3, True, 0.2), (2, False, 0.1))):
+        for a, b in zip(res[0][i][1], res[1][i][1]):  # broadcast: identical weights on every rank
+            np.testing.assert_array_equal(a, b)
+        # Layer.weights order: att, final_bias, then linear_transform's kernel
+        att, bias, kernel = (torch.from_numpy(a) for a in res[0][i][1])
+        ref = R.gatv2_forward(X, EI, kernel, att, bias, heads=heads, concat=concat, negative_slope=slope).numpy()
+        got = np.concatenate([res[r][i][0] for r in range(world)])
+        np.testing.assert_array_equal(got, ref)
+
+
+def _progress_worker(rank, world, port, q):
+    """The N > 1 progress reporting: per-rank shard-build and tuner lines, a
+    heartbeat while the first forward runs, and the KGX_TUNE_BUDGET_S bound."""
+    import io
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KGX_LOG="1", KGX_HEARTBEAT_S="0.02")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    buf = io.StringIO()
+    kd.LOG_STREAM = buf
+    try:
+        s, d, x, W, b = _graph()
+        bounds = kd.equal_bounds(N, world)
+        lo, hi = bounds[rank], bounds[rank + 1]
+        keep = (d >= lo) & (d < hi)
+        sg = kd.ShardedGraph.build(torch.from_numpy(s[keep]), torch.from_numpy(d[keep]), bounds,
+                                   backend=OracleBackend(), n_features=F_OUT)
+        layer = kd.ShardedGCNConv(F_OUT, sg)
+        layer._build_device = torch.device("cpu")
+        layer.build((hi - lo, F_IN))
+        n_cands = len(sg.exchange_candidates())
+        os.environ["KGX_TUNE_BUDGET_S"] = "0"  # the first candidate is timed, the rest left untimed
+        try:
+            with kd.heartbeat(rank, "first forward"), torch.no_grad():
+                import time as _t
+
+                _t.sleep(0.1)  # a slow first forward: the heartbeat must tick meanwhile
+                layer(torch.from_numpy(x[lo:hi]))
+        finally:
+            del os.environ["KGX_TUNE_BUDGET_S"]
+        q.put((rank, buf.getvalue(), sg.tuning_skipped, n_cands, sg.tuning_s, sorted(sg.tuning.items())))
+    finally:
+        kd.LOG_STREAM = None
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_n_gt_1_progress_and_tune_budget():
+    """What a stalled N > 1 first forward leaves on stderr: every rank prints its
+    shard build, each exchange plan and tuner candidate, and a heartbeat line at
+    least every KGX_HEARTBEAT_S while the forward runs (bench.py wraps the
+    shard build and the first forward in distributed.heartbeat, 30 s by
+    default); KGX_TUNE_BUDGET_S bounds the tune (candidates past it untimed,
+    the same on every rank)."""
+    if torch.cuda.is_initialized():
+        pytest.skip("never start processes from a process that has initialised the GPU")
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_progress_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r = q.get(timeout=120)
+        res[r[0]] = r[1:]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        text, skipped, n_cands, tuning_s, tuning = res[r]
+        lines = text.splitlines()
+        assert all(ln.startswith(f"[kgx r{r}] ") for ln in lines), lines[:3]
+        assert any("shard build:" in ln for ln in lines)
+        assert any("tune:" in ln and "budget 0 s" in ln for ln in lines)
+        assert sum("first forward: running" in ln for ln in lines) >= 2  # ticks during the forward
+        assert any("first forward: done in" in ln for ln in lines)
+        assert n_cands > 1 and skipped == n_cands - 1 and tuning_s is not None
+        assert sum(v != float("inf") for _, v in tuning) == 1
+    assert res[0][4] == res[1][4]  # the same candidates timed / skipped on every rank
