@@ -105,6 +105,14 @@ class KgxBackend:
         return kops.aggregate(g, table, reduce, weighted=weighted, epilogue=epilogue, bias=bias, xroot=xroot,
                               gin_scale=gin_scale, exact=exact)
 
+    def aggregate_transposed(self, g, t, weighted=True):
+        """The backward of a (weighted) row sum over g: for every SOURCE row j of
+        g, sum over its out-edges e = (j -> i) of w_e t[i] -- one kgx_spmm over
+        g's transpose (graph.transpose: rows = g's sources, each row's edges in
+        input order)."""
+        gt = G.transpose(g)
+        return kops.aggregate(gt, t, "sum", weighted=weighted)
+
     def aggregate_accumulate(self, g, table, out, weighted=False, epilogue=nat.EPI_ACCUM, bias=None, xroot=None,
                              gin_scale=1.0, table2=None):
         """out += the (weighted) row sums of table over g, in place (KGX_EPI_ACCUM);
@@ -139,6 +147,10 @@ class TorchComm:
     def broadcast(self, t, src: int = 0) -> None:
         dist.broadcast(t, src=src, group=self.group)
 
+    def all_reduce(self, t) -> None:
+        """t <- the sum of every rank's t (the sharded backward's dW / db)."""
+        dist.all_reduce(t, group=self.group)
+
     def all_gather(self, out, inp) -> None:
         """out = [rank 0's inp | rank 1's inp | ...] (equal sizes)."""
         dist.all_gather_into_tensor(out, inp, group=self.group)
@@ -168,6 +180,11 @@ class HostStagedComm(TorchComm):
         dist.broadcast(h, src=src, group=self.group)
         t.copy_(h)
 
+    def all_reduce(self, t) -> None:
+        h = t.detach().cpu()
+        dist.all_reduce(h, group=self.group)
+        t.copy_(h)
+
     def all_gather(self, out, inp) -> None:
         h = inp.detach().cpu()
         parts = [torch.empty_like(h) for _ in range(dist.get_world_size(self.group))]
@@ -185,7 +202,7 @@ def _inference_only(layer: Layer, weights) -> None:
     if torch.is_grad_enabled() and any(p.requires_grad for p in weights):
         raise NotImplementedError(
             f"{type(layer).__name__} is inference-only: call it under torch.no_grad() (or freeze its weights); "
-            "training runs on the single-GPU layers")
+            "training runs on the single-GPU layers and on ShardedGCNConv")
 
 
 # where progress and heartbeat lines go (stderr; tests substitute a buffer)
@@ -1022,6 +1039,27 @@ class ShardedGraph:
             wait_step(len(steps) - 1)
         return out
 
+    def reverse_halo_exchange(self, g_src: torch.Tensor) -> torch.Tensor:
+        """The backward of halo_exchange: g_src [n_local + n_halo, F] holds
+        gradients w.r.t. this rank's table rows; each halo row's gradient goes
+        back to the rank that owns the row (the forward all-to-all with the
+        splits swapped) and is added to that row's own gradient.  Returns
+        [n_local, F].  Within one (chunk, peer) slice the rows are distinct,
+        and slices are added in chunk, then rank order: deterministic."""
+        n = self.n_local
+        dx = g_src[:n].clone()
+        halo = g_src[n:]
+        F = g_src.shape[1]
+        for c in self.chunks:
+            recv = g_src.new_empty((int(sum(c.send_splits)), F))
+            self.comm.all_to_all_single(recv, halo[c.lo: c.hi].contiguous(), c.send_splits, c.recv_splits)
+            off = 0
+            for cnt in c.send_splits:
+                if cnt:
+                    dx.index_add_(0, c.send_rows[off: off + cnt].long(), recv[off: off + cnt])
+                off += cnt
+        return dx
+
     def propagate(self, x_local: torch.Tensor, reduce: str = "sum", **kw) -> torch.Tensor:
         """Sharded MessagePassing.propagate with the default message x_j."""
         table = self.new_table(x_local.shape[1], x_local)
@@ -1058,7 +1096,10 @@ class ShardedGCNConv(Layer):
         if not self.built:
             self._build_device = x_local.device
             self.build(tuple(x_local.shape))
-        _inference_only(self, self.weights)
+        if torch.is_grad_enabled() and (x_local.requires_grad or any(p.requires_grad for p in self.weights)):
+            # training: the sharded forward + backward (_ShardedGCNFn)
+            use_b = self.use_bias and self.bias is not None
+            return _ShardedGCNFn.apply(x_local, self.kernel, self.bias if use_b else None, self)
         sg = self.sg
         use_b = self.use_bias and self.bias is not None
         if not sg.exact and sg.backend.supports_fused(x_local.shape[1], self.output_dim):
@@ -1203,6 +1244,54 @@ class ShardedGCNConv(Layer):
             # every step, used or not: also orders the side stream's reads of x_local
             wait_step(len(steps) - 1)
         return out
+
+
+class _ShardedGCNFn(torch.autograd.Function):
+    """ShardedGCNConv with gradients (the reference's model.fit path,
+    tests/performance/test_large_graphs.py:341-357, on sharded rows).
+
+    forward:  table = [x_local | pulled halo x] (halo_exchange);
+              agg = A_shard table (weighted sum over the shard CSR, in each
+              row's global input order), y = agg W + b
+              (= the reference's sum_e norm_e x_j W + b, gcn_conv.py:233-272).
+    backward: dagg = dY W^T;  G = A_shard^T dagg over the shard's sources
+              (graph.transpose: own rows and halo rows);  the halo rows' G goes
+              back to their owners (reverse_halo_exchange) and is added to
+              their own G: dX_local;  dW = sum over ranks of agg^T dY and db =
+              sum over ranks of sum_i dY_i (all-reduce)."""
+
+    @staticmethod
+    def forward(ctx, x_local, kernel, bias, layer):
+        sg = layer.sg
+        with torch.no_grad():
+            x_local = x_local.contiguous()
+            table = sg.new_table(x_local.shape[1], x_local)
+            table[: sg.n_local] = x_local
+            sg.halo_exchange(table)
+            agg = sg.backend.aggregate(sg.graph, table, "sum", weighted=True, exact=sg.exact)
+            del table
+            y = sg.backend.transform(agg, kernel, bias)
+        ctx.layer = layer
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(agg, kernel)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        agg, kernel = ctx.saved_tensors
+        sg = ctx.layer.sg
+        dy = dy.contiguous()
+        dx = dW = db = None
+        if ctx.needs_input_grad[0]:
+            dagg = sg.backend.transform(dy, kernel.t().contiguous())
+            dx = sg.reverse_halo_exchange(sg.backend.aggregate_transposed(sg.graph, dagg))
+        if ctx.needs_input_grad[1]:
+            dW = torch.matmul(agg.t(), dy)
+            sg.comm.all_reduce(dW)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = dy.sum(0)
+            sg.comm.all_reduce(db)
+        return dx, dW, db, None
 
 
 def use_merged_halo() -> bool:

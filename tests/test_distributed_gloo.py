@@ -29,7 +29,7 @@ class OracleBackend:
     def build_graph(self, src, dst, n_src, n_dst, n_features):
         rowptr, col, eid, deg = R.csr_by_destination(src.numpy(), dst.numpy(), n_src, n_dst, self_loops=False)
         t = torch.from_numpy
-        return SimpleNamespace(rowptr=t(rowptr), col=t(col), eid=t(eid), deg=t(deg), n_dst=n_dst,
+        return SimpleNamespace(rowptr=t(rowptr), col=t(col), eid=t(eid), deg=t(deg), n_dst=n_dst, n_src=n_src,
                                kept=int(rowptr[-1]), dinv=None, w=None, device=torch.device("cpu"))
 
     def dinv(self, deg):
@@ -147,6 +147,18 @@ def _oracle_gatv2(g, h_src, h_dst, att, heads, channels, negative_slope, bias=No
 OracleBackend.gatv2 = staticmethod(_oracle_gatv2)
 
 
+def _oracle_aggregate_transposed(self, g, t, weighted=True):
+    """sum over every source row's out-edges of (w_e) t[dst_e], in CSR slot order."""
+    rows = torch.repeat_interleave(torch.arange(g.n_dst), g.deg.long())
+    msg = t[rows]
+    if weighted:
+        msg = msg * g.w.unsqueeze(1)
+    return R.aggregate("sum", msg, g.col.long(), g.n_src)
+
+
+OracleBackend.aggregate_transposed = _oracle_aggregate_transposed
+
+
 class UnfusedOracleBackend(OracleBackend):
     def supports_fused(self, f_in, f_out):
         return False
@@ -220,8 +232,6 @@ def _worker(rank, world, chunks, port, q):
         with torch.no_grad():
             layer.kernel.copy_(torch.from_numpy(W))
             layer.bias.copy_(torch.from_numpy(b))
-        with pytest.raises(NotImplementedError):  # inference-only: grad mode with trainable weights
-            layer(torch.from_numpy(x[lo:hi]))
         with torch.no_grad():
             y = layer(torch.from_numpy(x[lo:hi]))  # push-pull halo (the default)
         pp = sg._pp
@@ -740,3 +750,78 @@ def test_n_gt_1_progress_and_tune_budget():
         assert n_cands > 1 and skipped == n_cands - 1 and tuning_s is not None
         assert sum(v != float("inf") for _, v in tuning) == 1
     assert res[0][4] == res[1][4]  # the same candidates timed / skipped on every rank
+
+
+def _train_worker(rank, world, port, q):
+    """ShardedGCNConv with gradients: forward on the pulled halo table, backward
+    through the transposed shard CSR, halo gradients pushed back, dW / db all-reduced."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        s, d, x, W, b = _graph()
+        bounds = kd.equal_bounds(N, world)
+        lo, hi = bounds[rank], bounds[rank + 1]
+        keep = (d >= lo) & (d < hi)
+        sg = kd.ShardedGraph.build(torch.from_numpy(s[keep]), torch.from_numpy(d[keep]), bounds,
+                                   backend=OracleBackend(), n_features=F_OUT, halo_chunks=2)
+        layer = kd.ShardedGCNConv(F_OUT, sg)
+        layer._build_device = torch.device("cpu")
+        layer.build((hi - lo, F_IN))
+        with torch.no_grad():
+            layer.kernel.copy_(torch.from_numpy(W))
+            layer.bias.copy_(torch.from_numpy(b))
+        xl = torch.from_numpy(x[lo:hi]).clone().requires_grad_(True)
+        y = layer(xl)
+        r = torch.from_numpy(np.random.default_rng(3).standard_normal((N, F_OUT)).astype(np.float32))[lo:hi]
+        (y * r).sum().backward()
+        with torch.no_grad():
+            y_inf = layer(torch.from_numpy(x[lo:hi]))  # the inference path: the same forward values
+        q.put((rank, y.detach().numpy(), xl.grad.numpy(), layer.kernel.grad.numpy(), layer.bias.grad.numpy(),
+               y_inf.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_sharded_gcn_backward():
+    """Sharded GCNConv training step at world 2 against torch autograd through
+    the oracle's whole-graph forward (oracle.reference.gcn_forward): the output,
+    dX (every rank's rows), dW and db (all-reduced) within 1e-5 of max(1, |ref|)
+    (dW / db: sums over all rows, sqrt(N) * 1e-5 as the single-GPU backward
+    tests use)."""
+    if torch.cuda.is_initialized():
+        pytest.skip("never start processes from a process that has initialised the GPU")
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_train_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r = q.get(timeout=120)
+        res[r[0]] = r[1:]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    s, d, x, W, b = _graph()
+    X = torch.from_numpy(x).clone().requires_grad_(True)
+    Wt = torch.from_numpy(W).clone().requires_grad_(True)
+    bt = torch.from_numpy(b).clone().requires_grad_(True)
+    y = R.gcn_forward(X, torch.from_numpy(np.stack([s, d])), Wt, bt)
+    rr = torch.from_numpy(np.random.default_rng(3).standard_normal((N, F_OUT)).astype(np.float32))
+    (y * rr).sum().backward()
+
+    def close(got, ref, tol):
+        err = np.abs(got - ref) / np.maximum(1.0, np.abs(ref))
+        assert err.max() <= tol, err.max()
+
+    close(np.concatenate([res[r][0] for r in range(world)]), y.detach().numpy(), 1e-5)
+    close(np.concatenate([res[r][4] for r in range(world)]), y.detach().numpy(), 1e-5)
+    close(np.concatenate([res[r][1] for r in range(world)]), X.grad.numpy(), 1e-5)
+    for r in range(world):  # all-reduced: the same on every rank
+        np.testing.assert_array_equal(res[r][2], res[0][2])
+        np.testing.assert_array_equal(res[r][3], res[0][3])
+    close(res[0][2], Wt.grad.numpy(), 1e-5 * np.sqrt(N))
+    close(res[0][3], bt.grad.numpy(), 1e-5 * np.sqrt(N))
