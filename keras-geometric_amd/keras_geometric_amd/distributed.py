@@ -328,6 +328,35 @@ class _Works:
                 h.wait()
 
 
+def halo_first_frac() -> float | None:
+    """KGX_HALO_FIRST (0 < f < 1): the push-pull plan's first exchange chunk
+    takes this fraction of every peer list and the other K - 1 chunks split the
+    rest evenly -- a small first chunk lands sooner, so the passes that need
+    halo rows start earlier while the larger chunks are on the links.  Unset:
+    K even chunks."""
+    v = os.environ.get("KGX_HALO_FIRST")
+    if not v:
+        return None
+    f = float(v)
+    if not 0.0 < f < 1.0:
+        raise ValueError(f"KGX_HALO_FIRST must lie in (0, 1), got {v!r}")
+    return f
+
+
+def chunk_slice(count: int, k: int, K: int, first: float | None = None) -> tuple[int, int]:
+    """[a, b) of chunk k of a list of `count` rows cut K ways: evenly
+    (floor(count k / K)), or with chunk 0 holding floor(count * first) rows and
+    chunks 1..K-1 splitting the rest evenly.  Requester and owner compute it
+    from the same count, so both sides agree on every chunk."""
+    if first is None or K == 1:
+        return count * k // K, count * (k + 1) // K
+    f = int(count * first)
+    if k == 0:
+        return 0, f
+    rest = count - f
+    return f + rest * (k - 1) // (K - 1), f + rest * k // (K - 1)
+
+
 def _prefix(v: list) -> list:
     out = [0]
     for c in v:
@@ -542,7 +571,8 @@ class ShardedGraph:
             raise ValueError("push_pull_plan(weighted=True): the shard graph has no edge weights")
         if self._pp_by_k is None:
             self._pp_by_k = {}
-        key = ("pull" if pull_only else "halo", K, weighted)
+        first = halo_first_frac() if K > 1 else None
+        key = ("pull" if pull_only else "halo", K, weighted, first)
         if key in self._pp_by_k:
             self._pp = self._pp_by_k[key]
             return self._pp
@@ -616,11 +646,11 @@ class ShardedGraph:
             lo_k = off
             rows, pull_send, pull_recv = [], [], []
             for r in range(world):
-                a, b = sp[r] + s_pull[r] * k // K, sp[r] + s_pull[r] * (k + 1) // K
+                a, b = (sp[r] + v for v in chunk_slice(s_pull[r], k, K, first))
                 rows.append(req_pull[a:b])
                 pull_send.append(b - a)
             for p in range(world):  # receiver side: where chunk k's pulled rows from p land
-                a, b = r_pull[p] * k // K, r_pull[p] * (k + 1) // K
+                a, b = chunk_slice(r_pull[p], k, K, first)
                 pull_pos[rp[p] + a: rp[p] + b] = torch.arange(off, off + b - a, device=dev)
                 off += b - a
                 pull_recv.append(b - a)
@@ -629,7 +659,7 @@ class ShardedGraph:
             cols, slots, ws, push_send, push_recv = [], [], [], [], []
             n_slots, push_lo = 0, off
             for r in range(world):
-                j0, j1 = s_push[r] * k // K, s_push[r] * (k + 1) // K
+                j0, j1 = chunk_slice(s_push[r], k, K, first)
                 sl = req_slot[spe[r]: spe[r + 1]]
                 m = (sl >= j0) & (sl < j1)
                 cols.append(req_src[spe[r]: spe[r + 1]][m])
@@ -638,7 +668,7 @@ class ShardedGraph:
                 n_slots += j1 - j0
                 push_send.append(j1 - j0)
             for p in range(world):  # receiver side: where chunk k's partials from p land
-                j0, j1 = r_push[p] * k // K, r_push[p] * (k + 1) // K
+                j0, j1 = chunk_slice(r_push[p], k, K, first)
                 push_pos[ru[p] + j0: ru[p] + j1] = torch.arange(off, off + j1 - j0, device=dev)
                 off += j1 - j0
                 push_recv.append(j1 - j0)

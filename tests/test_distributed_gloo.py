@@ -266,6 +266,18 @@ def _worker(rank, world, chunks, port, q):
                 y_pull = layer(torch.from_numpy(x[lo:hi]))  # pull-only halo
         finally:
             del os.environ["KGX_HALO_PUSH"]
+        y_first = y
+        if chunks > 1:  # a small first chunk (KGX_HALO_FIRST): the same rows, other chunk bounds
+            os.environ["KGX_HALO_FIRST"] = "0.2"
+            try:
+                with torch.no_grad():
+                    y_first = layer(torch.from_numpy(x[lo:hi]))
+                ppf = sg._pp
+                assert ppf is not pp and ppf.n_rows == pp.n_rows and len(ppf.chunks) == chunks
+                sizes = [c.hi - c.lo for c in ppf.chunks]
+                assert sizes[0] <= 0.25 * pp.n_rows + world, sizes
+            finally:
+                del os.environ["KGX_HALO_FIRST"]
         # K left open: the first forward times K = 1 / 2 / 4 (collective) and keeps the fastest
         sg2 = kd.ShardedGraph.build(torch.from_numpy(s[keep]), torch.from_numpy(d[keep]), bounds,
                                     backend=OracleBackend(), n_features=F_OUT)
@@ -331,7 +343,7 @@ def _worker(rank, world, chunks, port, q):
         assert torch.equal(y_again, y)
         q.put((rank, gcn.numpy(), mx.numpy(), sg.n_halo, sum(sg.send_counts), y.numpy(), y_pull.numpy(), pp.n_push,
                y_tuned.numpy(), y_unfused.numpy(), y_wide.numpy(), y_unmerged.numpy(), ys_gather[0], ys_gather[1],
-               y_chunk.numpy(), y_pullplan))
+               y_chunk.numpy(), y_pullplan, y_first.numpy()))
     finally:
         dist.destroy_process_group()
 
@@ -373,7 +385,7 @@ def test_sharded_equals_unsharded_bitwise(world, chunks):
     # overlapped layer path, push-pull and pull-only halos: own-source part, then
     # one part per halo chunk per row (re-associated sums)
     assert sum(results[r][6] for r in range(world)) > 0  # partial sums were pushed
-    for i in (4, 5, 7, 8, 10, 11, 12, 13, 14):
+    for i in (4, 5, 7, 8, 10, 11, 12, 13, 14, 15):
         y_split = np.concatenate([results[r][i] for r in range(world)])
         err = np.abs(y_split - y) / np.maximum(1, np.abs(y))
         assert err.max() <= 1e-5
@@ -825,3 +837,17 @@ def test_sharded_gcn_backward():
         np.testing.assert_array_equal(res[r][3], res[0][3])
     close(res[0][2], Wt.grad.numpy(), 1e-5 * np.sqrt(N))
     close(res[0][3], bt.grad.numpy(), 1e-5 * np.sqrt(N))
+
+
+def test_chunk_slice_bounds():
+    """chunk_slice: even cuts, or a first chunk of floor(count * f) rows and the
+    rest split evenly; the slices tile [0, count) for any count and K."""
+    for count in (0, 1, 7, 100, 12345):
+        for K in (1, 2, 3, 4):
+            for first in (None, 0.1, 0.5):
+                cuts = [kd.chunk_slice(count, k, K, first) for k in range(K)]
+                assert cuts[0][0] == 0 and cuts[-1][1] == count
+                assert all(a <= b for a, b in cuts) and all(cuts[k][1] == cuts[k + 1][0] for k in range(K - 1))
+                if first is not None and K > 1:
+                    assert cuts[0][1] == int(count * first)
+    assert kd.chunk_slice(10, 1, 4) == (2, 5)
