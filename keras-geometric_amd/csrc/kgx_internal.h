@@ -87,6 +87,42 @@ inline int64_t shared_cap(int64_t full) {
   return c > 0 ? c : 1;
 }
 
+// A per-host-thread side stream and fork / join events, one set per
+// translation unit (each .hip file's launches fork onto its own stream).
+// Thread-local: concurrent launches from several host threads (one rank per
+// thread in the tests) never share events.
+struct ForkJoin {
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  int device = -1;
+};
+namespace {
+inline ForkJoin& fork_join() {
+  thread_local ForkJoin fj;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (fj.device != dev) {
+    (void)hipStreamCreateWithFlags(&fj.side, hipStreamNonBlocking);
+    (void)hipEventCreateWithFlags(&fj.fork, hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&fj.join, hipEventDisableTiming);
+    fj.device = dev;
+  }
+  return fj;
+}
+}  // namespace
+
+// Joins a forked side stream back into the caller's stream on every return
+// after the fork, so no error path leaves the caller's stream unordered
+// against the forked kernel (whose outputs the caching allocator could
+// otherwise hand out again while it still writes them).
+struct JoinGuard {
+  ForkJoin* fj = nullptr;
+  hipStream_t s = nullptr;
+  ~JoinGuard() {
+    if (fj) (void)hipStreamWaitEvent(s, fj->join, 0);
+  }
+};
+
 inline int next_pow2(int v) {
   int p = 1;
   while (p < v) p <<= 1;

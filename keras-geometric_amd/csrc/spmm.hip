@@ -824,39 +824,6 @@ __global__ __launch_bounds__(kBlock) void spmm_std_kernel(SpmmArgs a) {
 
 
 
-// A per-host-thread side stream and fork / join events (EXACT mode's hub kernel
-// beside spmm_kernel).  Thread-local: concurrent launches from several host
-// threads (one rank per thread in the tests) never share events.
-struct ForkJoin {
-  hipStream_t side = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-  int device = -1;
-};
-ForkJoin& fork_join() {
-  thread_local ForkJoin fj;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  if (fj.device != dev) {
-    (void)hipStreamCreateWithFlags(&fj.side, hipStreamNonBlocking);
-    (void)hipEventCreateWithFlags(&fj.fork, hipEventDisableTiming);
-    (void)hipEventCreateWithFlags(&fj.join, hipEventDisableTiming);
-    fj.device = dev;
-  }
-  return fj;
-}
-
-// Joins a forked side stream back into the caller's stream on every return
-// after the fork, so no error path leaves the caller's stream unordered
-// against the forked kernel (whose outputs the caching allocator could
-// otherwise hand out again while it still writes them).
-struct JoinGuard {
-  ForkJoin* fj = nullptr;
-  hipStream_t s = nullptr;
-  ~JoinGuard() {
-    if (fj) (void)hipStreamWaitEvent(s, fj->join, 0);
-  }
-};
-
 template <int VEC, int NT, int RED, bool W, bool TWO = false>
 int launch_main(const SpmmArgs& a_in, hipStream_t s) {
   SpmmArgs a = a_in;

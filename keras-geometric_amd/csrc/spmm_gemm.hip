@@ -859,9 +859,60 @@ __global__ __launch_bounds__(256) void spmm_gemm_fixup_kernel(FusedArgs a) {
   }
 }
 
+// KGX_FUSED_FORK=1 (measurement A/B): the degree <= 2 tail's tiny-row launches
+// run on a forked side stream beside the main and short-row kernels (disjoint
+// output rows), so their latency-bound launches fill the others' last waves
+// instead of starting after them; joined before the hub fix-up.
+inline bool fused_fork_on() {
+  static const bool on = [] {
+    const char* h = getenv("KGX_FUSED_FORK");
+    return h && atoi(h) != 0;
+  }();
+  return on;
+}
+
+template <int RED, bool W, bool TWO, bool NARROW>
+int launch_tiny(const FusedArgs& a, hipStream_t s) {
+  const bool extra = a.pre_gin || a.agg_out;
+  for (int part = 0; part < 2; ++part) {  // one 1024-thread block per CU; degree-2 head, then the degree <= 1 rest
+    FusedArgs b = a;
+    b.tpack = a.tpack + (part ? a.n_tiny2 : 0);
+    b.tw = a.tw ? a.tw + (part ? a.n_tiny2 : 0) : nullptr;
+    b.n_tiny = part ? a.n_tiny - a.n_tiny2 : a.n_tiny2;
+    if (b.n_tiny <= 0) continue;
+    auto k = part ? (extra ? spmm_gemm_tiny_kernel<RED, W, true, 1, TWO, NARROW>
+                           : spmm_gemm_tiny_kernel<RED, W, false, 1, TWO, NARROW>)
+                  : (extra ? spmm_gemm_tiny_kernel<RED, W, true, 2, TWO, NARROW>
+                           : spmm_gemm_tiny_kernel<RED, W, false, 2, TWO, NARROW>);
+    const int rows = part ? tiny_rows<1>() : tiny_rows<2>();
+    const int64_t need = (b.n_tiny + rows - 1) / rows;
+    const int64_t cap = a.share_gpu ? shared_cap(int64_t(cu_count())) : int64_t(cu_count());
+    hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kTinyThreads), 0, s, b);
+    KGX_CHECK_LAUNCH();
+  }
+  return KGX_OK;
+}
+
 template <int RED, bool W, bool TWO = false, bool NARROW = false>
 int launch(const FusedArgs& a, hipStream_t s) {
   const int64_t work = a.items ? a.n_long : a.n_rows;
+  JoinGuard guard;
+  ForkJoin* joined = nullptr;
+  if (a.tpack && a.n_tiny > 0 && fused_fork_on()) {
+    ForkJoin& fj = fork_join();
+    if (hipEventRecord(fj.fork, s) != hipSuccess || hipStreamWaitEvent(fj.side, fj.fork, 0) != hipSuccess) {
+      set_error("kgx_spmm_gemm: stream fork failed");
+      return KGX_ERR_HIP;
+    }
+    if (launch_tiny<RED, W, TWO, NARROW>(a, fj.side) != KGX_OK) return KGX_ERR_HIP;
+    if (hipEventRecord(fj.join, fj.side) != hipSuccess) {
+      set_error("kgx_spmm_gemm: stream join failed");
+      return KGX_ERR_HIP;
+    }
+    joined = &fj;
+    guard.fj = &fj;
+    guard.s = s;
+  }
   if (work > 0) {
     static int cus = 0;
     if (cus == 0) {
@@ -899,24 +950,14 @@ int launch(const FusedArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kThreads), 0, s, a);
     KGX_CHECK_LAUNCH();
   }
-  if (a.tpack && a.n_tiny > 0) {  // one 1024-thread block per CU; degree-2 head, then the degree <= 1 rest
-    const bool extra = a.pre_gin || a.agg_out;
-    for (int part = 0; part < 2; ++part) {
-      FusedArgs b = a;
-      b.tpack = a.tpack + (part ? a.n_tiny2 : 0);
-      b.tw = a.tw ? a.tw + (part ? a.n_tiny2 : 0) : nullptr;
-      b.n_tiny = part ? a.n_tiny - a.n_tiny2 : a.n_tiny2;
-      if (b.n_tiny <= 0) continue;
-      auto k = part ? (extra ? spmm_gemm_tiny_kernel<RED, W, true, 1, TWO, NARROW>
-                             : spmm_gemm_tiny_kernel<RED, W, false, 1, TWO, NARROW>)
-                    : (extra ? spmm_gemm_tiny_kernel<RED, W, true, 2, TWO, NARROW>
-                             : spmm_gemm_tiny_kernel<RED, W, false, 2, TWO, NARROW>);
-      const int rows = part ? tiny_rows<1>() : tiny_rows<2>();
-      const int64_t need = (b.n_tiny + rows - 1) / rows;
-      const int64_t cap = a.share_gpu ? shared_cap(int64_t(cu_count())) : int64_t(cu_count());
-      hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kTinyThreads), 0, s, b);
-      KGX_CHECK_LAUNCH();
+  if (joined) {
+    guard.fj = nullptr;  // joined here, with the status checked
+    if (hipStreamWaitEvent(s, joined->join, 0) != hipSuccess) {
+      set_error("kgx_spmm_gemm: stream join failed");
+      return KGX_ERR_HIP;
     }
+  } else if (a.tpack && a.n_tiny > 0 && launch_tiny<RED, W, TWO, NARROW>(a, s) != KGX_OK) {
+    return KGX_ERR_HIP;
   }
   if (a.items && a.n_split > 0) {
     const int64_t blocks = (a.n_split + 7) / 8;
