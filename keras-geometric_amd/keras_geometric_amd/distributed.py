@@ -313,6 +313,7 @@ class PushPullPlan:
     weighted: bool = True  # receiver edges carry the GCN norms (else weight 1, plain partial sums)
     kind: str = "halo"  # "halo" (push-pull all-to-all), "pull" (the same all-to-all, pulled rows only) or "allgather" (every rank's rows, chunked)
     merged: dict | None = None  # unit -> (own pass, first-group pass, later groups, first wait): merged_passes
+    row_group: object = None  # kind "group": each local row's destination group (group_passes)
 
 
 class _Works:
@@ -536,7 +537,7 @@ class ShardedGraph:
         return x_local.new_empty((0, x_local.shape[1]))
 
     def push_pull_plan(self, n_chunks: int | None = None, weighted: bool | None = None,
-                       pull_only: bool = False) -> PushPullPlan:
+                       pull_only: bool = False, groups: bool = False) -> PushPullPlan:
         """A smaller halo for the weighted-sum (GCN) path.  Collective: every
         rank calls it once (ShardedGCNConv does, on its first forward).
 
@@ -563,7 +564,19 @@ class ShardedGraph:
         pull_only (exchange kind "pull"): every halo edge is served by pulling
         its source -- more rows on the links, but no partial sums for the
         owner to compute and write and the receiver to read back; which wins
-        depends on the link rate, so the tuner times both."""
+        depends on the link rate, so the tuner times both.
+
+        groups (exchange kind "group"): the chunks follow DESTINATION row
+        groups instead of slices of the request lists.  The local rows with
+        halo edges are cut into K groups of about equal halo-edge counts (the
+        first one KGX_HALO_FIRST of them when set); chunk k carries group k's
+        pushed partials and the pulled sources group k needs that no earlier
+        group needed (a source goes with the first group that reads it).  So
+        once chunk k has landed, every halo row of group k's rows is present
+        and ONE two-table pass writes each of those rows once
+        (ShardedGraph.group_passes) -- no accumulating pass re-reads and
+        rewrites a row per chunk.  The bytes moved are the same as the
+        slice-chunked plan's."""
         K = n_chunks or self.halo_k or len(self.chunks)
         if weighted is None:
             weighted = self.graph.w is not None
@@ -572,7 +585,7 @@ class ShardedGraph:
         if self._pp_by_k is None:
             self._pp_by_k = {}
         first = halo_first_frac() if K > 1 else None
-        key = ("pull" if pull_only else "halo", K, weighted, first)
+        key = ("group" if groups else ("pull" if pull_only else "halo"), K, weighted, first)
         if key in self._pp_by_k:
             self._pp = self._pp_by_k[key]
             return self._pp
@@ -610,20 +623,61 @@ class ShardedGraph:
         pe_row, pe_src, pe_w = pe_row[order], hs[pe][order], hw[pe][order]
         pe_owner = push_owner[pe_row]
         pe_cnt = torch.bincount(pe_owner, minlength=world)
-        pe_slot = pe_row - (torch.cumsum(push_cnt, 0) - push_cnt)[pe_owner]  # push row index within its owner
-        counts = torch.stack([pull_cnt, push_cnt, pe_cnt], 1).reshape(-1).contiguous()
+        pull_owner = torch.bucketize(pull_ids, bt, right=True)
+        if groups:
+            # destination groups of about equal halo-edge counts, in row order
+            hdeg = torch.bincount(hd, minlength=n_local)
+            cum = torch.cumsum(hdeg, 0) - hdeg  # halo edges of the rows before each row
+            tot = max(int(hdeg.sum()), 1)
+            if first is None:
+                grp = (cum * K) // tot
+            else:  # group 0: the first `first` of the halo edges, the rest in K - 1 even groups
+                f = int(tot * first)
+                grp = torch.where(cum < f, torch.zeros_like(cum), 1 + ((cum - f) * (K - 1)) // max(tot - f, 1))
+            grp = grp.clamp_(max=K - 1)
+            # a pulled source travels with the first group that reads it; a partial with its row's group
+            ce = grp[hd]
+            src_chunk = torch.full((us.numel(),), K, dtype=torch.long, device=dev)
+            src_chunk.scatter_reduce_(0, inv_s[via_pull], ce[via_pull], "amin")
+            pull_chunk = src_chunk[pulled]
+            push_chunk = grp[push_keys % stride]
+            # (owner, chunk, id) order for the pull list, (owner, chunk, row) for the push list
+            pull_perm = torch.argsort(pull_owner * K + pull_chunk, stable=True)
+            push_perm = torch.argsort(push_owner * K + push_chunk, stable=True)
+            push_rank = torch.empty_like(push_perm)
+            push_rank[push_perm] = torch.arange(push_perm.numel(), device=dev)
+            # push row index within its owner, in the new order
+            pe_slot = push_rank[pe_row] - (torch.cumsum(push_cnt, 0) - push_cnt)[pe_owner]
+            pull_cnt_k = torch.bincount(pull_owner * K + pull_chunk, minlength=world * K).view(world, K)
+            push_cnt_k = torch.bincount(push_owner * K + push_chunk, minlength=world * K).view(world, K)
+        else:
+            pull_perm = push_perm = None
+            pe_slot = pe_row - (torch.cumsum(push_cnt, 0) - push_cnt)[pe_owner]  # push row index within its owner
+            pull_cnt_k = pull_cnt.view(world, 1)
+            push_cnt_k = push_cnt.view(world, 1)
+        kk = pull_cnt_k.shape[1]
+        counts = torch.cat([pull_cnt_k, push_cnt_k, pe_cnt.view(world, 1)], 1).reshape(-1).contiguous()
         counts_in = torch.empty_like(counts)
         comm.all_to_all_single(counts_in, counts)
-        co, ci = counts.view(world, 3).cpu().tolist(), counts_in.view(world, 3).cpu().tolist()
-        r_pull, r_push, r_pe = ([c[i] for c in co] for i in range(3))
-        s_pull, s_push, s_pe = ([c[i] for c in ci] for i in range(3))
+        co, ci = counts.view(world, 2 * kk + 1).cpu().tolist(), counts_in.view(world, 2 * kk + 1).cpu().tolist()
+        r_pull_k, r_push_k = [c[:kk] for c in co], [c[kk: 2 * kk] for c in co]
+        s_pull_k, s_push_k = [c[:kk] for c in ci], [c[kk: 2 * kk] for c in ci]
+        r_pull, r_push, r_pe = [sum(v) for v in r_pull_k], [sum(v) for v in r_push_k], [c[2 * kk] for c in co]
+        s_pull, s_push, s_pe = [sum(v) for v in s_pull_k], [sum(v) for v in s_push_k], [c[2 * kk] for c in ci]
+
+        def cut(count_k, count, k):
+            """[a, b) of chunk k within one peer's list: per-group counts, or chunk_slice."""
+            if groups:
+                a = sum(count_k[:k])
+                return a, a + count_k[k]
+            return chunk_slice(count, k, K, first)
 
         def exchange(t, dtype, s, r):
             out = torch.empty(sum(s), dtype=dtype, device=dev)
             comm.all_to_all_single(out, t.contiguous(), s, r)
             return out
 
-        req_pull = exchange(pull_ids, torch.long, s_pull, r_pull) - lo
+        req_pull = exchange(pull_ids if pull_perm is None else pull_ids[pull_perm], torch.long, s_pull, r_pull) - lo
         req_slot = exchange(pe_slot, torch.long, s_pe, r_pe)
         req_src = exchange(pe_src, torch.long, s_pe, r_pe) - lo
         req_w = exchange(pe_w, torch.float32, s_pe, r_pe)
@@ -646,11 +700,11 @@ class ShardedGraph:
             lo_k = off
             rows, pull_send, pull_recv = [], [], []
             for r in range(world):
-                a, b = (sp[r] + v for v in chunk_slice(s_pull[r], k, K, first))
+                a, b = (sp[r] + v for v in cut(s_pull_k[r], s_pull[r], k))
                 rows.append(req_pull[a:b])
                 pull_send.append(b - a)
             for p in range(world):  # receiver side: where chunk k's pulled rows from p land
-                a, b = chunk_slice(r_pull[p], k, K, first)
+                a, b = cut(r_pull_k[p], r_pull[p], k)
                 pull_pos[rp[p] + a: rp[p] + b] = torch.arange(off, off + b - a, device=dev)
                 off += b - a
                 pull_recv.append(b - a)
@@ -659,7 +713,7 @@ class ShardedGraph:
             cols, slots, ws, push_send, push_recv = [], [], [], [], []
             n_slots, push_lo = 0, off
             for r in range(world):
-                j0, j1 = chunk_slice(s_push[r], k, K, first)
+                j0, j1 = cut(s_push_k[r], s_push[r], k)
                 sl = req_slot[spe[r]: spe[r + 1]]
                 m = (sl >= j0) & (sl < j1)
                 cols.append(req_src[spe[r]: spe[r + 1]][m])
@@ -668,7 +722,7 @@ class ShardedGraph:
                 n_slots += j1 - j0
                 push_send.append(j1 - j0)
             for p in range(world):  # receiver side: where chunk k's partials from p land
-                j0, j1 = chunk_slice(r_push[p], k, K, first)
+                j0, j1 = cut(r_push_k[p], r_push[p], k)
                 push_pos[ru[p] + j0: ru[p] + j1] = torch.arange(off, off + j1 - j0, device=dev)
                 off += j1 - j0
                 push_recv.append(j1 - j0)
@@ -681,6 +735,13 @@ class ShardedGraph:
                                   send_rows=none_i32, send_graph=send_graph)
             chunks.append(HaloChunk(lo=lo_k, hi=off, recv_splits=[], send_splits=[], send_rows=none_i32,
                                     steps=[pull_step, push_step]))
+        if groups:  # positions were assigned in the (owner, chunk, ...) order: back to sorted-id / key order
+            pp_sorted = torch.empty_like(pull_pos)
+            pp_sorted[pull_perm] = pull_pos
+            pull_pos = pp_sorted
+            pu_sorted = torch.empty_like(push_pos)
+            pu_sorted[push_perm] = push_pos
+            push_pos = pu_sorted
         # receiver CSR over the received rows: pulled rows keep their edges and
         # weights; a pushed partial is one edge of weight 1 into its row
         pidx = torch.searchsorted(pull_ids, hs[via_pull])
@@ -696,6 +757,8 @@ class ShardedGraph:
             step_parts = list(self.backend.split_by_source(rg, [0, 0] + [st.hi for c in chunks for st in c.steps])[1:])
         self._pp = PushPullPlan(chunks=chunks, parts=parts, n_rows=off, n_pull=rp[-1], n_push=ru[-1], recv_graph=rg,
                                 step_parts=step_parts, weighted=weighted, kind=key[0])
+        if groups:
+            self._pp.row_group = grp  # [n_local]: the destination group of each row with halo edges
         self._pp_by_k[key] = self._pp
         return self._pp
 
@@ -757,9 +820,10 @@ class ShardedGraph:
         kind = self.exchange or os.environ.get("KGX_EXCHANGE", "halo")
         if kind == "allgather":
             return self.allgather_plan(n_chunks or self.halo_k or len(self.chunks), weighted)
-        return self.push_pull_plan(n_chunks, weighted, pull_only=kind == "pull")
+        return self.push_pull_plan(n_chunks, weighted, pull_only=kind == "pull", groups=kind == "group")
 
-    def exchange_candidates(self, halo_ks=(1, 2, 4), gather_ks=(1, 2, 4), units=("step", "chunk", "none")) -> list:
+    def exchange_candidates(self, halo_ks=(1, 2, 4), gather_ks=(1, 2, 4), units=("step", "chunk", "none"),
+                            group_ks=()) -> list:
         """(exchange, K, merge unit) triples worth timing: the push-pull halo at
         each K and merge unit (merged_passes), and the all-gather when its table
         (every rank's rows) is at most 4x the largest pull-only halo over the
@@ -778,6 +842,8 @@ class ShardedGraph:
         # free (11.96-12.78 vs 11.16-11.18 ms) and at 400 GB/s (22.5 vs 12.9 ms)
         halo_kind = "pull" if fixed == "pull" else "halo"
         cands = [(halo_kind, k, u) for k in halo_ks for u in dict.fromkeys(halo_units)]
+        # destination-group chunks (the GCN layer's grouped passes; the unit is implied)
+        cands += [("group", k, "group") for k in group_ks]
         n = torch.full((self.world,), self.n_halo, dtype=torch.long, device=self.graph.col.device)
         every = torch.empty_like(n)
         self.comm.all_to_all_single(every, n)
@@ -906,6 +972,48 @@ class ShardedGraph:
         later = [t for t in groups[1:] if t[1].kept]
         pp.merged[unit] = (g_a, g_b, later, groups[0][0])
         return pp.merged[unit]
+
+    def group_passes(self, pp: PushPullPlan):
+        """(g_a, [(wait step, g_k)]) for a destination-group plan (kind "group"):
+        g_a = the own-source CSR restricted to the rows with no halo edge (they
+        need nothing from the exchange); g_k = group k's rows with their own
+        edges, then their halo edges (sources >= n_local index the halo
+        buffer, every chunk <= k), for ONE two-table pass that writes each row
+        once after chunk k's last step has landed (cached on the plan)."""
+        if pp.merged is None:
+            pp.merged = {}
+        if "group" in pp.merged:
+            return pp.merged["group"]
+        g_own, _ = self.own_halo_parts()
+        n_local = self.n_local
+        dev = g_own.col.device
+        rg = pp.recv_graph
+        has_halo = torch.zeros(n_local, dtype=torch.bool, device=dev)
+        if rg is not None:
+            has_halo = rg.deg > 0
+        g_a = self.backend.restrict_rows(g_own, ~has_halo)
+        ar = torch.arange(n_local, device=dev)
+        r_own = torch.repeat_interleave(ar, g_own.deg.long(), output_size=g_own.kept)
+        passes = []
+        if rg is not None:
+            r_h = torch.repeat_interleave(ar, rg.deg.long(), output_size=rg.kept)
+            grp = pp.row_group
+            steps_before = 0
+            for k, c in enumerate(pp.chunks):
+                steps_before += len(c.steps)
+                in_k = has_halo & (grp == k)
+                if not bool(in_k.any()):
+                    continue
+                keep_o, keep_h = in_k[r_own], in_k[r_h]
+                rows = torch.cat([r_own[keep_o], r_h[keep_h]])
+                cols = torch.cat([g_own.col[keep_o].long(), rg.col[keep_h].long() + n_local])
+                g_k = self.backend.build_graph(cols.to(torch.int32), rows.to(torch.int32), n_local + pp.n_rows,
+                                               n_local, 128)
+                if pp.weighted:
+                    g_k.w = torch.cat([g_own.w[keep_o], rg.w[keep_h]])[g_k.eid.long()].contiguous()
+                passes.append((steps_before - 1, self.backend.restrict_rows(g_k, in_k)))
+        pp.merged["group"] = (g_a, passes)
+        return pp.merged["group"]
 
     def halo_exchange(self, table: torch.Tensor) -> None:
         """table[n_local:] <- rows other ranks own (one all-to-all-v over RCCL
@@ -1168,7 +1276,7 @@ class ShardedGCNConv(Layer):
             return sg.halo_k
         with torch.no_grad():
             sg.tune_exchange(lambda kind, K: self._forward_overlapped(x_local, self.bias if use_b else None, K),
-                             sg.exchange_candidates())
+                             sg.exchange_candidates(group_ks=(2, 4)))
         return sg.halo_k
 
     def _forward_overlapped(self, x_local: torch.Tensor, bias, n_chunks: int | None = None) -> torch.Tensor:
@@ -1193,6 +1301,8 @@ class ShardedGCNConv(Layer):
             chunks, g_chunks, n_rows = pp.chunks, pp.parts, pp.n_rows
         x_local = x_local.contiguous()
         halo = sg.halo_buffer(x_local.shape[1], x_local, n_rows)
+        if pp is not None and pp.kind == "group":
+            return self._forward_grouped(x_local, bias, pp, halo)
         if pp is not None and (use_merged_halo() or pp.kind == "allgather"):
             return self._forward_merged(x_local, bias, pp, halo)
         with torch.no_grad():
@@ -1213,6 +1323,39 @@ class ShardedGCNConv(Layer):
                     sg.backend.aggregate_transform(g, halo[c.lo: c.hi], self.kernel, out=out)
         return out
 
+
+    def _forward_grouped(self, x_local: torch.Tensor, bias, pp: PushPullPlan, halo: torch.Tensor) -> torch.Tensor:
+        """Destination-group exchange (kind "group"): side stream as
+        _forward_merged; main stream: out[rows with no halo edge] = b + (A_own X) W
+        while the exchange is in flight, then per group k, once chunk k has
+        landed, out[group k] = b + (A_own X + A_halo halo) W in one two-table
+        pass -- every row written once."""
+        sg = self.sg
+        g_a, passes = sg.group_passes(pp)
+        steps = [st for c in pp.chunks for st in c.steps]
+        with torch.no_grad():
+            works = sg.start_halo_exchange(x_local, halo, pp.chunks)
+            handles = []
+            for w, c in zip(works, pp.chunks):
+                handles.extend(w.handles if w is not None else [None] * len(c.steps))
+            waited = set()
+
+            def wait_step(i):
+                for j in range(i + 1):  # steps land in issue order on the comm stream
+                    if j not in waited:
+                        waited.add(j)
+                        if handles[j] is not None:
+                            handles[j].wait()
+
+            with kops.sharing_gpu():  # the exchange's packing and RCCL kernels run beside this pass
+                out = sg.backend.aggregate_transform(g_a, x_local, self.kernel, bias=bias)
+            for n, (i, g) in enumerate(passes):
+                wait_step(i)
+                with kops.sharing_gpu() if n + 1 < len(passes) else contextlib.nullcontext():
+                    sg.backend.aggregate_transform(g, x_local, self.kernel, bias=bias, out=out, x2=halo,
+                                                   accumulate=False)
+            wait_step(len(steps) - 1)  # also orders the side stream's reads of x_local
+        return out
 
     def _forward_merged(self, x_local: torch.Tensor, bias, pp: PushPullPlan, halo: torch.Tensor) -> torch.Tensor:
         """The default path with the first exchange step merged into its rows

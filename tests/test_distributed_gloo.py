@@ -293,8 +293,10 @@ def _worker(rank, world, chunks, port, q):
         # (this small graph's remote sources cover most rows) the all-gather at K = 1 / 2 / 4
         units = ("step", "chunk", "none")
         assert sorted(sg2.tuning) == sorted([f"halo:{k}:{u}" for k in (1, 2, 4) for u in units]
-                                            + [f"allgather:{k}:{u}" for k in (1, 2, 4) for u in ("step", "none")])
-        assert sg2.exchange in ("halo", "allgather") and sg2.halo_k in (1, 2, 4) and sg2.merge_unit in units
+                                            + [f"allgather:{k}:{u}" for k in (1, 2, 4) for u in ("step", "none")]
+                                            + [f"group:{k}:group" for k in (2, 4)])
+        assert sg2.exchange in ("halo", "allgather", "group") and sg2.halo_k in (1, 2, 4)
+        assert sg2.merge_unit in units + ("group",)
         assert len(sg2._pp.chunks) == sg2.halo_k and sg2._pp.kind == sg2.exchange
         # the all-gather exchange on its own (K = 1 and 3), within the tolerance of the reference
         ys_gather = []
@@ -303,6 +305,15 @@ def _worker(rank, world, chunks, port, q):
             with torch.no_grad():
                 ys_gather.append(layer2(torch.from_numpy(x[lo:hi])).numpy())
             assert sg2._pp.kind == "allgather" and len(sg2._pp.chunks) == kk
+        # destination-group chunks: every row with halo edges written once, by its group's pass
+        ys_group = []
+        for kk in (2, 3):
+            sg2.exchange, sg2.halo_k = "group", kk
+            with torch.no_grad():
+                ys_group.append(layer2(torch.from_numpy(x[lo:hi])).numpy())
+            ppg = sg2._pp
+            assert ppg.kind == "group" and len(ppg.chunks) == kk and ppg.merged["group"] is not None
+            assert ppg.n_rows == ppg.n_pull + ppg.n_push == ppg.chunks[-1].hi
         # the pull-only halo through the merged passes (no partial sums pushed)
         sg2.exchange, sg2.halo_k = "pull", 2
         with torch.no_grad():
@@ -343,7 +354,7 @@ def _worker(rank, world, chunks, port, q):
         assert torch.equal(y_again, y)
         q.put((rank, gcn.numpy(), mx.numpy(), sg.n_halo, sum(sg.send_counts), y.numpy(), y_pull.numpy(), pp.n_push,
                y_tuned.numpy(), y_unfused.numpy(), y_wide.numpy(), y_unmerged.numpy(), ys_gather[0], ys_gather[1],
-               y_chunk.numpy(), y_pullplan, y_first.numpy()))
+               y_chunk.numpy(), y_pullplan, y_first.numpy(), ys_group[0], ys_group[1]))
     finally:
         dist.destroy_process_group()
 
@@ -385,7 +396,7 @@ def test_sharded_equals_unsharded_bitwise(world, chunks):
     # overlapped layer path, push-pull and pull-only halos: own-source part, then
     # one part per halo chunk per row (re-associated sums)
     assert sum(results[r][6] for r in range(world)) > 0  # partial sums were pushed
-    for i in (4, 5, 7, 8, 10, 11, 12, 13, 14, 15):
+    for i in (4, 5, 7, 8, 10, 11, 12, 13, 14, 15, 16, 17):
         y_split = np.concatenate([results[r][i] for r in range(world)])
         err = np.abs(y_split - y) / np.maximum(1, np.abs(y))
         assert err.max() <= 1e-5
