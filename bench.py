@@ -232,14 +232,15 @@ def _build_sharded(kind: str, n_global: int, e_global: int, f_in: int, f_out: in
                    dev, comm):
     from keras_geometric_amd import distributed as kd
 
-    if kind == "gat":
-        raise SystemExit("--config c3 (GATv2) is a one-GPU config (BASELINE.json configs[2])")
     gcn = kind == "gcn"
-    sg = kd.ShardedGraph.rmat(n_global, e_global, seed=seed, device=dev, comm=comm, self_loops=gcn,
+    # GATv2 (BASELINE configs[2] is one GPU; N > 1 runs it weak-scaled like NS): self loops, no norm
+    sg = kd.ShardedGraph.rmat(n_global, e_global, seed=seed, device=dev, comm=comm, self_loops=kind in ("gcn", "gat"),
                               gcn_norm=gcn, exact=exact, n_features=f_in)
     x = torch.randn(sg.n_local, f_in, device=dev)
     if kind == "gcn":
         layer = kd.ShardedGCNConv(f_out, sg)
+    elif kind == "gat":
+        layer = kd.ShardedGATv2Conv(f_out // GAT_HEADS, sg, heads=GAT_HEADS)
     elif kind == "gin":
         layer = kd.ShardedGINConv(f_out, sg, aggregator="sum")
     else:
