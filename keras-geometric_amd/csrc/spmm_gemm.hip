@@ -859,16 +859,26 @@ __global__ __launch_bounds__(256) void spmm_gemm_fixup_kernel(FusedArgs a) {
   }
 }
 
-// KGX_FUSED_FORK=1 (measurement A/B): the degree <= 2 tail's tiny-row launches
-// run on a forked side stream beside the main and short-row kernels (disjoint
-// output rows), so their latency-bound launches fill the others' last waves
-// instead of starting after them; joined before the hub fix-up.
-inline bool fused_fork_on() {
-  static const bool on = [] {
-    const char* h = getenv("KGX_FUSED_FORK");
-    return h && atoi(h) != 0;
-  }();
-  return on;
+// KGX_FUSED_FORK (measurement A/B): 1 = the degree <= 2 tail's tiny-row
+// launches run on a forked side stream beside the main and short-row kernels;
+// 2 = the short-row launch goes to the side stream too (before the tiny ones).
+// Disjoint output rows; the latency-bound tail launches fill the main kernel's
+// gathers instead of starting after it; joined before the hub fix-up.
+inline int fused_fork_mode() {  // read per launch (tests switch it in-process)
+  const char* h = getenv("KGX_FUSED_FORK");
+  return h ? atoi(h) : 0;
+}
+
+template <int RED, bool W, bool TWO, bool NARROW>
+int launch_short(const FusedArgs& a, hipStream_t s) {
+  int per_cu = 0;
+  auto k = spmm_gemm_short_kernel<RED, W, TWO, NARROW>;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, 0) != hipSuccess || per_cu <= 0) per_cu = 2;
+  const int64_t need = (a.n_short_end - a.n_long + kShortRows - 1) / kShortRows;
+  const int64_t cap = a.share_gpu ? shared_cap(int64_t(per_cu) * cu_count()) : int64_t(per_cu) * cu_count();
+  hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kThreads), 0, s, a);
+  KGX_CHECK_LAUNCH();
+  return KGX_OK;
 }
 
 template <int RED, bool W, bool TWO, bool NARROW>
@@ -898,13 +908,17 @@ int launch(const FusedArgs& a, hipStream_t s) {
   const int64_t work = a.items ? a.n_long : a.n_rows;
   JoinGuard guard;
   ForkJoin* joined = nullptr;
-  if (a.tpack && a.n_tiny > 0 && fused_fork_on()) {
+  const bool has_short = a.items && a.n_long < a.n_short_end;
+  const int fork = fused_fork_mode();
+  const bool short_forked = fork == 2 && has_short;
+  if ((a.tpack && a.n_tiny > 0 && fork >= 1) || short_forked) {
     ForkJoin& fj = fork_join();
     if (hipEventRecord(fj.fork, s) != hipSuccess || hipStreamWaitEvent(fj.side, fj.fork, 0) != hipSuccess) {
       set_error("kgx_spmm_gemm: stream fork failed");
       return KGX_ERR_HIP;
     }
-    if (launch_tiny<RED, W, TWO, NARROW>(a, fj.side) != KGX_OK) return KGX_ERR_HIP;
+    if (short_forked && launch_short<RED, W, TWO, NARROW>(a, fj.side) != KGX_OK) return KGX_ERR_HIP;
+    if (a.tpack && a.n_tiny > 0 && launch_tiny<RED, W, TWO, NARROW>(a, fj.side) != KGX_OK) return KGX_ERR_HIP;
     if (hipEventRecord(fj.join, fj.side) != hipSuccess) {
       set_error("kgx_spmm_gemm: stream join failed");
       return KGX_ERR_HIP;
@@ -933,23 +947,7 @@ int launch(const FusedArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kThreads), 0, s, a);
     KGX_CHECK_LAUNCH();
   }
-  if (a.items && a.n_long < a.n_short_end) {
-    int per_cu = 0;
-    auto k = spmm_gemm_short_kernel<RED, W, TWO, NARROW>;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, 0) != hipSuccess || per_cu <= 0)
-      per_cu = 2;
-    static int cus2 = 0;
-    if (cus2 == 0) {
-      int dev = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&cus2, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus2 <= 0)
-        cus2 = 256;
-    }
-    const int64_t need = (a.n_short_end - a.n_long + kShortRows - 1) / kShortRows;
-    const int64_t cap = a.share_gpu ? shared_cap(int64_t(per_cu) * cus2) : int64_t(per_cu) * cus2;
-    hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kThreads), 0, s, a);
-    KGX_CHECK_LAUNCH();
-  }
+  if (has_short && !short_forked && launch_short<RED, W, TWO, NARROW>(a, s) != KGX_OK) return KGX_ERR_HIP;
   if (joined) {
     guard.fj = nullptr;  // joined here, with the status checked
     if (hipStreamWaitEvent(s, joined->join, 0) != hipSuccess) {

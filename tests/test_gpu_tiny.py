@@ -122,3 +122,27 @@ def test_tiny_tail_gcn_vs_oracle(dev):
     err = ((y - ref).abs() / ref.abs().clamp_min(1.0)).max().item()
     assert err <= 1e-5, err
     assert np.isfinite(y.numpy()).all()
+
+
+@pytest.mark.parametrize("fork", ["1", "2"])
+def test_fused_fork_bit_identical(dev, fork, monkeypatch):
+    """KGX_FUSED_FORK: the tail launches on a forked side stream (1: tiny rows;
+    2: short and tiny rows) beside the main kernel give the same bits as the
+    sequential launches (disjoint rows, same kernels), and the forked launch
+    is joined: the next op on the stream sees every row."""
+    import fused_ref
+
+    g, _ = _graph(dev, self_loops=True, gcn_norm=True)
+    _with_tiny(g)
+    gen = torch.Generator(device=dev).manual_seed(9)
+    x = torch.randn(g.rowptr.numel() - 1, 128, device=dev, generator=gen)
+    W = torch.randn(128, 128, device=dev, generator=gen) * 0.1
+    b = torch.randn(128, device=dev, generator=gen)
+    monkeypatch.setenv("KGX_FUSED_FORK", "0")
+    y0 = kops.aggregate_transform(g, x, W, "sum", weighted=True, bias=b)
+    monkeypatch.setenv("KGX_FUSED_FORK", fork)
+    y1 = kops.aggregate_transform(g, x, W, "sum", weighted=True, bias=b)
+    s1 = y1.sum(1)  # consumed right away on the same stream
+    torch.testing.assert_close(y1, y0, rtol=0, atol=0)
+    torch.testing.assert_close(s1, y0.sum(1), rtol=0, atol=0)
+    fused_ref.check(y1, g, fused_ref.reference(g, x, W, "sum", True, b), f"fork {fork}")
