@@ -722,7 +722,6 @@ def _progress_worker(rank, world, port, q):
         layer = kd.ShardedGCNConv(F_OUT, sg)
         layer._build_device = torch.device("cpu")
         layer.build((hi - lo, F_IN))
-        n_cands = len(sg.exchange_candidates())
         os.environ["KGX_TUNE_BUDGET_S"] = "0"  # the first candidate is timed, the rest left untimed
         try:
             with kd.heartbeat(rank, "first forward"), torch.no_grad():
@@ -732,6 +731,8 @@ def _progress_worker(rank, world, port, q):
                 layer(torch.from_numpy(x[lo:hi]))
         finally:
             del os.environ["KGX_TUNE_BUDGET_S"]
+        n_cands = len(sg.tuning)  # the layer's own candidate list (GCN adds group:2 / group:4)
+        assert n_cands >= len(sg.exchange_candidates())
         q.put((rank, buf.getvalue(), sg.tuning_skipped, n_cands, sg.tuning_s, sorted(sg.tuning.items())))
     finally:
         kd.LOG_STREAM = None
