@@ -405,8 +405,11 @@ template <int RED, bool WEIGHTED, bool GIN, bool FAST, bool TWO>
 __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Args a) {
   using R = RowRed<RED>;
   constexpr int RPW = 2;  // rows per wave per tile
-  constexpr int kHalf = kSteps / 2;
-  __shared__ u32x4_t wlo[kColBlocks * kHalf * 64];  // lo plane, k-steps 4..7: 64 KB
+#ifndef KGX_T2_LO_REG
+#define KGX_T2_LO_REG 4
+#endif
+  constexpr int kHalf = KGX_T2_LO_REG;  // lo-plane k-steps held in registers; the rest in LDS
+  __shared__ u32x4_t wlo[kColBlocks * (kSteps - kHalf) * 64];  // lo plane, k-steps 4..7: 64 KB
   __shared__ __attribute__((aligned(16))) short tile3[2][kPlanes][kRows][kLd];  // two tiles of split planes
   __shared__ __attribute__((aligned(16))) float sbias[kF];
   __shared__ int32_t tile_row[2][kRows];
@@ -415,6 +418,12 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Arg
   const int wl = threadIdx.x & 63;
   const int f = wl * 4;
   const int cl = wl & 15, q = wl >> 4;
+#if KGX_T2_STAGGER
+  const bool late = __builtin_amdgcn_readfirstlane(wave) >= 4;  // SIMD partners in opposite phase order
+#endif
+#if KGX_T2_PRIO
+  if (__builtin_amdgcn_readfirstlane(wave) >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
   bf16x8_t wfh[2][kSteps], wfm[2][kSteps], wfl[2][kHalf];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -439,7 +448,7 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Arg
       if (st < kHalf)
         wfl[i][st] = __builtin_bit_cast(bf16x8_t, pl);
       else
-        wlo[((2 * wave + i) * kHalf + st - kHalf) * 64 + wl] = pl;
+        wlo[((2 * wave + i) * (kSteps - kHalf) + st - kHalf) * 64 + wl] = pl;
     }
   }
   if (threadIdx.x < kF) sbias[threadIdx.x] = (a.bias && int(threadIdx.x) < a.F_out) ? a.bias[threadIdx.x] : 0.0f;
@@ -520,7 +529,7 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Arg
       for (int i = 0; i < 2; ++i) {
         if (i == 1 && !mf1) break;
         const bf16x8_t wf_lo = st < kHalf ? wfl[i][st < kHalf ? st : 0]
-                                          : __builtin_bit_cast(bf16x8_t, wlo[((2 * wave + i) * kHalf + (st >= kHalf ? st - kHalf : 0)) * 64 + wl]);
+                                          : __builtin_bit_cast(bf16x8_t, wlo[((2 * wave + i) * (kSteps - kHalf) + (st >= kHalf ? st - kHalf : 0)) * 64 + wl]);
         d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[i][st], xl, d[i], 0, 0, 0);
         d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf_lo, xh, d[i], 0, 0, 0);
         d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfm[i][st], xm, d[i], 0, 0, 0);
@@ -558,8 +567,18 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Arg
     // prepare first: tile t+2's gathers are issued as early as possible and have
     // the whole period; measured against MFMA-first and a half / half split of
     // the waves (tools/gpu_jobs/gpu_r3_order.sh), this order was fastest
+#if KGX_T2_STAGGER
+    if (late) {
+      mfma(FT, P);
+      prep();
+    } else {
+      prep();
+      mfma(FT, P);
+    }
+#else
     prep();
     mfma(FT, P);
+#endif
     lds_barrier();
   };
   using P0 = std::integral_constant<int, 0>;

@@ -459,9 +459,9 @@ def _run_wide_rank(rank, hub, dev, x128, x256, out):
                                   gcn_norm=False, halo_chunks=2)
         gin = kd.ShardedGINConv(32, sg, mlp_hidden=[128], aggregator="sum", eps_init=0.5)
         xl = x128[sg.lo: sg.lo + sg.n_local]
-        assert gin._fused(xl.contiguous())
         with torch.no_grad():
             res["gin"] = (gin(xl).cpu().numpy(), gin.conv.get_weights())
+        assert gin._fused(xl.contiguous())  # the MLP exists once built: the route the forward took
         # GCN 256 -> 256: the weighted two-table 256-wide kernels (kgx_spmm_gemm_f256_ex)
         sg2 = kd.ShardedGraph.rmat(N, E, seed=11, device=dev, comm=comm, n_features=256, halo_chunks=2)
         gcn = kd.ShardedGCNConv(256, sg2)

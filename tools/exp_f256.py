@@ -62,6 +62,11 @@ def main(n=10_000_000, e=100_000_000, f=256):
                                                 False, 0))  # n_long = 0: the degree 3-7 launch
         res["fused_tiny_ms"] = timeit(lambda: op(x, g.rowptr, g.rows, tail, None, g.col, None, 0, 0, W, b, True, 1.25,
                                                  False, -1, tpack, tw, 0, n2))
+        y = op(x, g.rowptr, g.rows, g.items, g.split, g.col, None, g.n_slots, 0, W, b, True, 1.25, False, g.n_long,
+               tpack, tw, n_se, n2)
+        bits = y.view(torch.int32).to(torch.int64)
+        res["out_bits"] = int(bits.sum()) + 3 * int(bits[::7].sum())  # variants must match bit for bit
+        del y, bits
         if os.environ.get("KGX_EXP_UNFUSED", "1") == "1":
             h = kops.aggregate(g, x, "sum", epilogue=nat.EPI_GIN, xroot=x, gin_scale=1.25)
             res["unfused_agg_ms"] = timeit(lambda: kops.aggregate(g, x, "sum", epilogue=nat.EPI_GIN, xroot=x,
