@@ -1509,7 +1509,12 @@ class _ShardedWrap(Layer):
             return
         with torch.no_grad():
             sg.tune_exchange(lambda kind, K: self._forward_impl(x_local, None),
-                             sg.exchange_candidates())
+                             sg.exchange_candidates(group_ks=self._group_ks(x_local)))
+
+    def _group_ks(self, x_local: torch.Tensor) -> tuple:
+        """Destination-group chunk counts the tuner also times: only where the
+        layer has a grouped forward (the fused GIN path)."""
+        return ()
 
 
 class ShardedGINConv(_ShardedWrap):
@@ -1532,6 +1537,9 @@ class ShardedGINConv(_ShardedWrap):
         _inference_only(self, self.conv.weights)
         self._maybe_tune(x_local.contiguous())
         return self._forward_impl(x_local, training)
+
+    def _group_ks(self, x_local: torch.Tensor) -> tuple:
+        return (2, 4) if self._fused(x_local) else ()
 
     def _fused(self, x_local: torch.Tensor) -> bool:
         """Whether (1+eps) x_i + aggr -> the MLP's first Dense runs fused into the
@@ -1572,6 +1580,8 @@ class ShardedGINConv(_ShardedWrap):
         W, b = first.kernel, (first.bias if first.use_bias else None)
         pp = sg.exchange_plan(weighted=False)
         halo = sg.halo_buffer(x_local.shape[1], x_local, pp.n_rows)
+        if pp.kind == "group":
+            return self._forward_fused_grouped(x_local, W, b, pp, halo)
         unit = None if (use_merged_halo() or pp.kind == "allgather") else "none"
         g_a, g_b, later, first_wait = sg.merged_passes(pp, unit)
         steps = [st for c in pp.chunks for st in c.steps]
@@ -1603,6 +1613,41 @@ class ShardedGINConv(_ShardedWrap):
         wait_step(len(steps) - 1)  # also orders the side stream's reads of x_local
         if relu and later:
             out = torch.relu_(out)
+        return out
+
+
+    def _forward_fused_grouped(self, x_local, W, b, pp: PushPullPlan, halo: torch.Tensor) -> torch.Tensor:
+        """Destination-group exchange (kind "group", ShardedGraph.group_passes)
+        with the first Dense fused: out[rows with no halo edge] = b + (s x_i +
+        A_own x) W while the exchange is in flight, then per group k, once chunk
+        k has landed, out[group k] = b + (s x_i + A_own x + A_halo halo) W in one
+        two-table launch -- every row written once, so the first Dense's ReLU
+        goes into every launch."""
+        sg, conv = self.sg, self.conv
+        first = conv.mlp.layers[0]
+        g_a, passes = sg.group_passes(pp)
+        steps = [st for c in pp.chunks for st in c.steps]
+        kw = dict(weighted=False, pre_gin=True, gin_scale=float(conv._scale()), relu=first.activation is torch.relu)
+        works = sg.start_halo_exchange(x_local, halo, pp.chunks)
+        handles = []
+        for w, c in zip(works, pp.chunks):
+            handles.extend(w.handles if w is not None else [None] * len(c.steps))
+        waited = set()
+
+        def wait_step(i):
+            for j in range(i + 1):  # steps land in issue order on the comm stream
+                if j not in waited:
+                    waited.add(j)
+                    if handles[j] is not None:
+                        handles[j].wait()
+
+        with kops.sharing_gpu():  # the exchange's packing and RCCL kernels run beside this pass
+            out = sg.backend.aggregate_transform(g_a, x_local, W, bias=b, **kw)
+        for n, (i, g) in enumerate(passes):
+            wait_step(i)
+            with kops.sharing_gpu() if n + 1 < len(passes) else contextlib.nullcontext():
+                sg.backend.aggregate_transform(g, x_local, W, bias=b, out=out, x2=halo, accumulate=False, **kw)
+        wait_step(len(steps) - 1)  # also orders the side stream's reads of x_local
         return out
 
 

@@ -430,6 +430,16 @@ def _conv_worker(rank, world, port, q):
                 assert layer._fused(xl)  # (1+eps) x + aggr -> first Dense (+ReLU) fused into the passes
             with torch.no_grad():
                 outs.append((layer(xl).numpy(), list(layer.conv.get_weights())))
+                if isinstance(layer, kd.ShardedGINConv) and layer.conv.aggregator == "sum":
+                    # destination-group chunks on the fused GIN path: each row written once
+                    saved = (sg.exchange, sg.halo_k, sg.merge_unit)
+                    for kk in (2, 3):
+                        sg.exchange, sg.halo_k = "group", kk
+                        yg = layer(xl).numpy()
+                        assert sg.exchange_plan(weighted=False).kind == "group"
+                        y0 = outs[-1][0]
+                        assert (np.abs(yg - y0) / np.maximum(1, np.abs(y0))).max() <= 1e-5, kk
+                    sg.exchange, sg.halo_k, sg.merge_unit = saved
         q.put((rank, outs))
     finally:
         dist.destroy_process_group()
