@@ -573,17 +573,32 @@ def test_sharded_gatv2_c3_hip(dev):
 
 
 
+class _FnCtx:
+    """The autograd context _ShardedGCNFn uses, for calling it directly."""
+    needs_input_grad = (True, True, True, False)
+
+    def save_for_backward(self, *t):
+        self.saved_tensors = t
+
+
 def _run_train_rank(rank, hub, dev, x, r_grad, out):
     try:
         comm = ThreadComm(hub, rank)
         sg = kd.ShardedGraph.rmat(N, E, seed=12, device=dev, comm=comm, n_features=F_FUSED, halo_chunks=2)
         layer = kd.ShardedGCNConv(64, sg, bias_initializer="glorot_uniform")
-        xl = x[sg.lo: sg.lo + sg.n_local].clone().requires_grad_(True)
-        y = layer(xl)
-        (y * r_grad[sg.lo: sg.lo + sg.n_local]).sum().backward()
+        xl = x[sg.lo: sg.lo + sg.n_local].contiguous()
+        with torch.no_grad():
+            layer(xl)  # builds the weights (rank 0's, broadcast)
+        # the training step's Function driven directly: torch autograd runs CUDA
+        # backward functions on ONE engine thread per device, so two threaded
+        # ranks' .backward() calls on the same GPU would run one after the other
+        # and the first would wait forever in a collective for the second (the
+        # autograd wiring itself is covered by the gloo test, one process per rank)
+        ctx = _FnCtx()
+        y = kd._ShardedGCNFn.forward(ctx, xl, layer.kernel.detach(), layer.bias.detach(), layer)
+        dx, dW, db, _ = kd._ShardedGCNFn.backward(ctx, r_grad[sg.lo: sg.lo + sg.n_local])
         torch.cuda.synchronize()
-        out[rank] = (y.detach().cpu().numpy(), xl.grad.cpu().numpy(), layer.kernel.grad.cpu().numpy(),
-                     layer.bias.grad.cpu().numpy(), layer.get_weights())
+        out[rank] = (y.cpu().numpy(), dx.cpu().numpy(), dW.cpu().numpy(), db.cpu().numpy(), layer.get_weights())
     except BaseException as e:
         out[rank] = e
         hub.barrier.abort()

@@ -39,6 +39,7 @@ def timeit(fn, reps=6):
 
 def main(n=10_000_000, e=100_000_000, f=256):
     dev = torch.device("cuda", 0)
+    torch.manual_seed(0)  # same x / W / b in every process: variants' out_bits compare
     ei = synthetic.rmat_edge_index(n, e, seed=0, device=dev)
     g = G.build_csr(ei[0].contiguous(), ei[1].contiguous(), n, n, n_features=f)
     x = torch.randn(n, f, device=dev)
