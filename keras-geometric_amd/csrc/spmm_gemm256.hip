@@ -486,9 +486,15 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Arg
         pw[r][0] = rw[B][r].x;
         pw[r][1] = rw[B][r].y;
       }
+#if KGX_T2_NOGATHER  // timing only: every gather reads x[0..2] (cache hits)
+      vload<4>(pv[r][0], gsrc256<TWO>(a, (rec[B][r].z & 1)) + f);
+      vload<4>(pv[r][1], gsrc256<TWO>(a, (rec[B][r].w & 1)) + f);
+      if constexpr (GIN) vload<4>(px[r], a.x + row_off(rec[B][r].x & 1, a.ld_x) + f);
+#else
       vload<4>(pv[r][0], gsrc256<TWO>(a, rec[B][r].z) + f);
       vload<4>(pv[r][1], gsrc256<TWO>(a, rec[B][r].w) + f);
       if constexpr (GIN) vload<4>(px[r], a.x + row_off(rec[B][r].x, a.ld_x) + f);
+#endif
     }
   };
   // fold the gathered rows, split them into plane buffer pb; tile_row too
@@ -519,6 +525,7 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Arg
     const bool mf0 = FASTS || 32 * wave < a.F_out, mf1 = FASTS || 32 * wave + 16 < a.F_out;
     if (!mf0) return;
     f32x4 d[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
+#if !KGX_T2_NOMFMA  // timing only: no MFMA phase (zeros stored)
 #pragma unroll
     for (int st = 0; st < kSteps; ++st) {
       const int kk = 64 * q + 8 * st;
@@ -538,6 +545,7 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Arg
         d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[i][st], xh, d[i], 0, 0, 0);
       }
     }
+#endif
     const int rr = tile_row[pb][cl];
     if (!FASTS && rr < 0) return;
 #pragma unroll
