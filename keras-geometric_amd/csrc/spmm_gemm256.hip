@@ -861,7 +861,10 @@ template <typename K>
 unsigned grid256(K k, int64_t tiles) {
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, 0) != hipSuccess || per_cu <= 0) per_cu = 1;
-  const int64_t cap = int64_t(per_cu) * cu_count();
+  int64_t cap = int64_t(per_cu) * cu_count();
+#if KGX_EXP_GRID_CUS  // measurement builds: the grid of a launch on a CU-masked stream (KGX_EXP_CUS CUs)
+  if (const char* e = getenv("KGX_EXP_CUS")) cap = int64_t(per_cu) * atoi(e);
+#endif
   return unsigned(tiles < cap ? tiles : cap);
 }
 
