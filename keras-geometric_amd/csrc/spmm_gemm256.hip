@@ -84,6 +84,7 @@ struct F256Args {
   // address math), so a gather's address is one select of the base
   const float* x2b;
   int32_t n_x1;
+  bool cu_split;  // KGX_FUSED_CU_SPLIT (host side only)
 };
 
 // Source row of column c: x[c], or with TWO x2[c - n_x1].  Root rows (pre_gin's
@@ -858,19 +859,107 @@ __global__ __launch_bounds__(256) void spmm_gemm256_fixup_kernel(F256Args a) {
 }
 
 template <typename K>
-unsigned grid256(K k, int64_t tiles) {
+unsigned grid256(K k, int64_t tiles, int cus = 0) {
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, 0) != hipSuccess || per_cu <= 0) per_cu = 1;
-  int64_t cap = int64_t(per_cu) * cu_count();
+  int64_t cap = int64_t(per_cu) * (cus > 0 ? cus : cu_count());
 #if KGX_EXP_GRID_CUS  // measurement builds: the grid of a launch on a CU-masked stream (KGX_EXP_CUS CUs)
   if (const char* e = getenv("KGX_EXP_CUS")) cap = int64_t(per_cu) * atoi(e);
 #endif
   return unsigned(tiles < cap ? tiles : cap);
 }
 
+// Spatial split of the GPU for one launch (KGX_FUSED_CU_SPLIT; KGX_F256_CU_SPLIT
+// = t, read per launch, default 8; 0 = off): the degree <= 2 tail -- MFMA-bound, its memory phase
+// serialised with its MFMA phase inside every block -- runs on t of every 32
+// CUs, beside the long-row and degree 3..7 launches -- memory-bound, MFMA pipes
+// ~9 % busy -- on the other CUs, each on a CU-masked stream
+// (hipExtStreamCreateWithCUMask) forked from and joined back into the caller's
+// stream, each grid sized to its CU set.  Every row is still reduced by one
+// kernel in the same order: the outputs are bit-identical to the one-stream
+// order (tools/exp_cupart.py, tests/test_gpu_fused256.py).  Measured on C4
+// (profiles/r05/c4_cupart*.json): see DESIGN.md §4.
+struct CuSplit {
+  hipStream_t head = nullptr, tail = nullptr;
+  hipEvent_t fork = nullptr, jh = nullptr, jt = nullptr;
+  int device = -1, per32 = -1, n_head = 0, n_tail = 0;
+};
+
+inline int cu_split_per32() {
+  const char* e = getenv("KGX_F256_CU_SPLIT");
+  const int v = e ? atoi(e) : 8;
+  return v > 0 && v < 32 ? v : 0;
+}
+
+// per (host thread, device, split): streams and events made once, kept for the
+// process (like the library's other side streams)
+inline CuSplit* cu_split(int per32) {
+  thread_local CuSplit cs;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  if (cs.device == dev && cs.per32 == per32) return &cs;
+  const int cus = cu_count();
+  uint32_t mh[8] = {0}, mt[8] = {0};
+  int nh = 0, nt = 0;
+  for (int c = 0; c < cus && c < 256; ++c) {
+    if ((c % 32) < per32) {
+      mt[c / 32] |= 1u << (c % 32);
+      ++nt;
+    } else {
+      mh[c / 32] |= 1u << (c % 32);
+      ++nh;
+    }
+  }
+  if (nh == 0 || nt == 0) return nullptr;
+  CuSplit n;
+  if (hipExtStreamCreateWithCUMask(&n.head, 8, mh) != hipSuccess ||
+      hipExtStreamCreateWithCUMask(&n.tail, 8, mt) != hipSuccess ||
+      hipEventCreateWithFlags(&n.fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&n.jh, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&n.jt, hipEventDisableTiming) != hipSuccess)
+    return nullptr;
+  n.device = dev;
+  n.per32 = per32;
+  n.n_head = nh;
+  n.n_tail = nt;
+  cs = n;  // the previous split's streams (another device or split) stay alive: launches may still use them
+  return &cs;
+}
+
+// joins both CU-masked streams back into the caller's stream on every return
+struct SplitJoin {
+  CuSplit* cs = nullptr;
+  hipStream_t s = nullptr;
+  ~SplitJoin() {
+    if (cs) {
+      (void)hipEventRecord(cs->jh, cs->head);
+      (void)hipEventRecord(cs->jt, cs->tail);
+      (void)hipStreamWaitEvent(s, cs->jh, 0);
+      (void)hipStreamWaitEvent(s, cs->jt, 0);
+    }
+  }
+};
+
 template <int RED, bool WT, bool TWO>
 int launch256(const F256Args& a, hipStream_t s) {
   const int64_t work = a.items ? a.n_work : a.n_rows;
+  hipStream_t sh = s, st = s;  // head (long + degree 3..7) and tail streams
+  int cus_h = 0, cus_t = 0;
+  SplitJoin join;
+  const int per32 = (a.cu_split && a.tpack && a.n_tiny > 0 && work > 0) ? cu_split_per32() : 0;
+  if (per32) {
+    if (CuSplit* cs = cu_split(per32)) {
+      KGX_CHECK_HIP(hipEventRecord(cs->fork, s));
+      KGX_CHECK_HIP(hipStreamWaitEvent(cs->head, cs->fork, 0));
+      KGX_CHECK_HIP(hipStreamWaitEvent(cs->tail, cs->fork, 0));
+      join.cs = cs;
+      join.s = s;
+      sh = cs->head;
+      st = cs->tail;
+      cus_h = cs->n_head;
+      cus_t = cs->n_tail;
+    }
+  }
   // long rows and hub chunks [0, n_long), then the rows of degree 3..7 [n_long, n_work)
   const int64_t n_long = (a.items && a.n_long >= 0 && a.n_long < work) ? a.n_long : work;
   if (n_long > 0) {
@@ -878,7 +967,7 @@ int launch256(const F256Args& a, hipStream_t s) {
     b.n_work = n_long;
     if (!a.items) b.n_rows = n_long;
     auto k = spmm_gemm256_kernel<RED, WT, 4, TWO>;
-    hipLaunchKernelGGL(k, dim3(grid256(k, (n_long + kRows - 1) / kRows)), dim3(kThreads), 0, s, b);
+    hipLaunchKernelGGL(k, dim3(grid256(k, (n_long + kRows - 1) / kRows, cus_h)), dim3(kThreads), 0, sh, b);
     KGX_CHECK_LAUNCH();
   }
   if (work > n_long) {
@@ -886,7 +975,7 @@ int launch256(const F256Args& a, hipStream_t s) {
     b.items = a.items + n_long;
     b.n_work = work - n_long;
     auto k = spmm_gemm256_kernel<RED, WT, KGX_F256_MID_PF, TWO>;
-    hipLaunchKernelGGL(k, dim3(grid256(k, (b.n_work + kRows - 1) / kRows)), dim3(kThreads), 0, s, b);
+    hipLaunchKernelGGL(k, dim3(grid256(k, (b.n_work + kRows - 1) / kRows, cus_h)), dim3(kThreads), 0, sh, b);
     KGX_CHECK_LAUNCH();
   }
   if (a.tpack && a.n_tiny > 0) {
@@ -895,8 +984,16 @@ int launch256(const F256Args& a, hipStream_t s) {
                  ? (fast ? spmm_gemm256_tiny2_kernel<RED, WT, true, true, TWO> : spmm_gemm256_tiny2_kernel<RED, WT, true, false, TWO>)
                  : (fast ? spmm_gemm256_tiny2_kernel<RED, WT, false, true, TWO>
                          : spmm_gemm256_tiny2_kernel<RED, WT, false, false, TWO>);
-    hipLaunchKernelGGL(k, dim3(grid256(k, (a.n_tiny + kRows - 1) / kRows)), dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL(k, dim3(grid256(k, (a.n_tiny + kRows - 1) / kRows, cus_t)), dim3(kThreads), 0, st, a);
     KGX_CHECK_LAUNCH();
+  }
+  if (join.cs) {  // the fix-up reads the long launch's partials: join first
+    CuSplit* cs = join.cs;
+    join.cs = nullptr;
+    KGX_CHECK_HIP(hipEventRecord(cs->jh, cs->head));
+    KGX_CHECK_HIP(hipEventRecord(cs->jt, cs->tail));
+    KGX_CHECK_HIP(hipStreamWaitEvent(s, cs->jh, 0));
+    KGX_CHECK_HIP(hipStreamWaitEvent(s, cs->jt, 0));
   }
   if (a.items && a.n_split > 0) {
     const int64_t blocks = (a.n_split + 3) / 4;
@@ -933,7 +1030,8 @@ extern "C" int kgx_spmm_gemm_f256_ex(int reduce, const int32_t* rowptr, const in
   KGX_REQUIRE(!tiny_pack || (items && n_short_end >= 0 && n_short_end <= n_items && (w == nullptr || tiny_w)),
               KGX_ERR_ARG, "kgx_spmm_gemm_f256: the tiny-row records need the schedule, 0 <= n_short_end <= n_items "
               "(and weights when weighted)");
-  KGX_REQUIRE((flags & ~(KGX_FUSED_PRE_GIN | KGX_FUSED_ACCUMULATE | KGX_FUSED_SHARE_GPU | KGX_FUSED_RELU)) == 0,
+  KGX_REQUIRE((flags & ~(KGX_FUSED_PRE_GIN | KGX_FUSED_ACCUMULATE | KGX_FUSED_SHARE_GPU | KGX_FUSED_RELU |
+                         KGX_FUSED_CU_SPLIT)) == 0,
               KGX_ERR_ARG, "kgx_spmm_gemm_f256: unknown flags 0x%x", flags);
   KGX_REQUIRE(!((flags & KGX_FUSED_RELU) && (flags & KGX_FUSED_ACCUMULATE)), KGX_ERR_ARG,
               "kgx_spmm_gemm_f256: KGX_FUSED_RELU cannot be combined with KGX_FUSED_ACCUMULATE");
@@ -981,6 +1079,7 @@ extern "C" int kgx_spmm_gemm_f256_ex(int reduce, const int32_t* rowptr, const in
   a.accumulate = (flags & KGX_FUSED_ACCUMULATE) != 0;
   a.relu = (flags & KGX_FUSED_RELU) != 0;
   a.gin_scale = gin_scale;
+  a.cu_split = (flags & KGX_FUSED_CU_SPLIT) != 0;
   a.n_x1 = x2 ? int32_t(n_x1) : INT32_MAX;
   // x2 - n_x1 * ld_x as an address (modular): gsrc256 adds row_off(c) for c >= n_x1
   a.x2b = x2 ? reinterpret_cast<const float*>(reinterpret_cast<uintptr_t>(x2) -

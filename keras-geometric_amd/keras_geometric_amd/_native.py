@@ -21,7 +21,7 @@ LIB_PATH = Path(os.environ.get("KGX_LIB", _PKG_ROOT / "lib" / "libkgx.so"))
 KGX_OK, KGX_ERR_ARG, KGX_ERR_HIP, KGX_ERR_INDEX, KGX_ERR_UNSUPPORTED = range(5)
 SUM, MEAN, MAX, MIN, STD = range(5)
 EPI_NONE, EPI_BIAS, EPI_GIN, EPI_RAW, EPI_ACCUM = range(5)
-FUSED_PRE_GIN, FUSED_ACCUMULATE, FUSED_SHARE_GPU, FUSED_RELU = 1, 2, 4, 8
+FUSED_PRE_GIN, FUSED_ACCUMULATE, FUSED_SHARE_GPU, FUSED_RELU, FUSED_CU_SPLIT = 1, 2, 4, 8, 16
 CSR_SELF_LOOPS, CSR_SEGMENT_ONLY, CSR_GCN_NORM = 1, 2, 4
 DENSE_RELU, DENSE_ACCUMULATE = 1, 2
 DENSE_MAX_K, DENSE_MAX_N = 256, 256

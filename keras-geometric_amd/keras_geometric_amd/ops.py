@@ -11,6 +11,7 @@ torch.compile / symbolic tracing sees shapes without running the GPU.
 
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -231,6 +232,27 @@ def _f256_call(reduce, rowptr, rows, n_dst, items, n_items, split, n_split, idx,
     )
 
 
+def _f256_cu_split(n_edges: int, n_tiny: int) -> bool:
+    """Whether a 256-wide launch runs its degree <= 2 tail on 64 CUs beside the
+    rest on the other 192 (KGX_FUSED_CU_SPLIT): when the modelled split time,
+    max(head on 192 CUs, tail on 64) plus the measured 10 % interference, beats
+    the one-stream sum by 3 %.  Per-unit costs from the C4 graph
+    (profiles/r05/c4_cupart*.json: head 15.7 ms / 97M edges on 256 CUs, 17.9 on
+    192; tail 5.63 ms / 7.46M rows on 256, 16.0 on 64).  Large launches only
+    (>= 1M tail rows): the fork / join and the smaller grids cost more than they
+    hide on small ones.  KGX_F256_CU_SPLIT: unset = this model (8 of every 32
+    CUs for the tail), "0" = never, t > 0 = always, with t of every 32 CUs."""
+    env = os.environ.get("KGX_F256_CU_SPLIT")
+    if env is not None:
+        return n_tiny > 0 and env.strip() not in ("", "0")
+    if n_tiny < 1_000_000:
+        return False
+    head_e = max(n_edges - 2 * n_tiny, 0)
+    t_seq = 1.62e-7 * head_e + 7.55e-7 * n_tiny
+    t_split = 1.1 * max(1.85e-7 * head_e, 2.14e-6 * n_tiny)
+    return t_split < 0.97 * t_seq
+
+
 def _partial_width(x: torch.Tensor) -> int:
     """Floats per hub-chunk partial: the 256-wide kernels 256, kgx_spmm_gemm 128 (any F_in <= 128)."""
     return F256 if x.shape[1] == F256 else 128
@@ -253,6 +275,9 @@ def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, b
         partials = torch.empty((n_slots, _partial_width(x)), dtype=torch.float32, device=dev)
     flags = int(pre_gin) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0) | (nat.FUSED_RELU if relu else 0)
     if x.shape[1] == F256:
+        if tpack is not None and items is not None and not _SHARE_GPU and \
+                _f256_cu_split(idx.numel(), n_items - (n_short_end if n_short_end >= 0 else n_items)):
+            flags |= nat.FUSED_CU_SPLIT
         _f256_call(reduce, rowptr, rows, n_dst, items, n_items, split, n_split, idx, w, x, x2, W, bias, flags,
                    gin_scale, out, partials, agg if save_agg else None, dev, tpack, tw, n_short_end, n_long)
         return out, agg
@@ -383,6 +408,9 @@ def spmm_gemm_acc_(
     if items is not None and n_split > 0:
         partials = torch.empty((n_slots, _partial_width(x)), dtype=torch.float32, device=dev)
     if x.shape[1] == F256:
+        if tpack is not None and items is not None and not _SHARE_GPU and \
+                _f256_cu_split(idx.numel(), n_items - (n_short_end if n_short_end >= 0 else n_items)):
+            flags |= nat.FUSED_CU_SPLIT
         _f256_call(reduce, rowptr, rows, n_dst, items, n_items, split, n_split, idx, w, x, x2, W, bias,
                    (nat.FUSED_ACCUMULATE if accumulate else 0) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0) | flags,
                    gin_scale, out, partials, None, dev, tpack, tw, n_short_end, n_long)

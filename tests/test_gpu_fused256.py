@@ -272,3 +272,41 @@ def test_fused256_two_tables_bit_identical(dev, weighted, gin):
         kops.aggregate_transform(g, x_all, W, "sum", out=a1, weighted=weighted)
         kops.aggregate_transform(g, x_own, W, "sum", out=a2, x2=x_halo, weighted=weighted)
         assert torch.equal(a1, a2)
+
+
+@pytest.mark.parametrize("per32", ["3", "8", "16"])
+def test_fused256_cu_split_bit_identical(dev, monkeypatch, per32):
+    """KGX_F256_CU_SPLIT: the degree <= 2 tail on a CU-masked stream beside the
+    long-row and degree 3..7 launches on the other CUs (forked from and joined
+    back into the caller's stream) gives the one-stream bits -- FAST tail (GIN,
+    F_out 256), weighted non-FAST tail (F_out 128, accumulate), two tables, hub
+    fix-up after the join -- and joins before the caller reads the output."""
+    N, H, E = 30000, 8000, 90000
+    rng = np.random.default_rng(23)
+    s, d = rmat_edges(5, scale_for(N + H), N + H, 0, E)
+    d = d % N
+    ei = T(np.stack([s, d]).astype(np.int32)).to(dev)
+    g = G.build_csr(ei[0].contiguous(), ei[1].contiguous(), N + H, N, n_features=F, split_len=16)
+    assert g.n_split > 0 and getattr(g, "_kgx_tiny", (None,))[0] is not None
+    g.w = T(rng.uniform(0.1, 1.0, g.kept).astype(np.float32)).to(dev)
+    x_all = T(rng.standard_normal((N + H, F)).astype(np.float32)).to(dev)
+    x_own, x_halo = x_all[:N].contiguous(), x_all[N:].contiguous()
+    W = T((rng.standard_normal((F, F)) * 0.06).astype(np.float32)).to(dev)
+    W128 = W[:, :128].contiguous()
+    b = T(rng.standard_normal(F).astype(np.float32)).to(dev)
+
+    def run():
+        with torch.no_grad():
+            y1 = kops.aggregate_transform(g, x_all, W, "sum", bias=b, pre_gin=True, gin_scale=1.25)
+            y2 = kops.aggregate_transform(g, x_own, W, "sum", bias=b, weighted=True, x2=x_halo)
+            acc = torch.ones(N, 128, device=dev)
+            kops.aggregate_transform(g, x_all, W128, "sum", out=acc, weighted=True)
+            return y1, y2, acc
+
+    monkeypatch.setenv("KGX_F256_CU_SPLIT", "0")
+    ref = run()
+    monkeypatch.setenv("KGX_F256_CU_SPLIT", per32)
+    for _ in range(2):
+        got = run()
+        for a_, b_ in zip(got, ref):
+            assert torch.equal(a_, b_)

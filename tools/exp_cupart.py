@@ -80,19 +80,28 @@ def main(n=10_000_000, e=100_000_000, f=256):
                                             True, 1.25, False, g.n_long, tpack, tw, n_se, n2))
         res["head_256"] = elapsed(lambda: run_head(256))
         res["tail_256"] = elapsed(lambda: run_tail(256))
-        layouts = {"inter": lambda k: [c for c in range(256) if (c % 8) < k],  # k of every 8 CUs
-                   "contig": lambda k: list(range(32 * k))}                     # the first 32 k CUs
-        for lay, pick in layouts.items():
-            for kt in (2, 3, 4):  # tail on kt / 8 of the CUs
-                tb = set(pick(kt))
+        mid = g.items[g.n_long:n_se].contiguous()
+        lng = g.items[:g.n_long].contiguous()
+
+        def run_long(cus):
+            os.environ["KGX_EXP_CUS"] = str(cus)
+            return op(x, g.rowptr, g.rows, lng, g.split, g.col, None, g.n_slots, 0, W, b, True, 1.25)
+
+        def run_midtail(cus):
+            os.environ["KGX_EXP_CUS"] = str(cus)
+            y = op(x, g.rowptr, g.rows, mid, None, g.col, None, 0, 0, W, b, True, 1.25, False, 0)
+            y2 = op(x, g.rowptr, g.rows, tail, None, g.col, None, 0, 0, W, b, True, 1.25, False, -1, tpack, tw, 0, n2)
+            return y, y2
+
+        main_s = torch.cuda.current_stream()
+        head_rows, long_rows, mid_rows = head[:, 0].long(), lng[:, 0].long(), mid[:, 0].long()
+        for split in ("head|tail", "long|mid+tail"):
+            for nt in (40, 48, 56, 64, 72, 80):
+                tb = {c for c in range(256) if (c % 32) < nt // 8}  # nt // 8 of every 32 CUs
                 hb = [c for c in range(256) if c not in tb]
                 sh, st = masked_stream(hb), masked_stream(sorted(tb))
-                nh, nt = len(hb), len(tb)
-                with torch.cuda.stream(sh):
-                    th = elapsed(lambda: run_head(nh))
-                with torch.cuda.stream(st):
-                    tt = elapsed(lambda: run_tail(nt))
-                main_s = torch.cuda.current_stream()
+                nh = len(hb)
+                fa, fb = (run_head, run_tail) if split == "head|tail" else (run_long, run_midtail)
 
                 def both():
                     ev = torch.cuda.Event()
@@ -100,24 +109,25 @@ def main(n=10_000_000, e=100_000_000, f=256):
                     sh.wait_event(ev)
                     st.wait_event(ev)
                     with torch.cuda.stream(sh):
-                        yh = run_head(nh)
+                        ya = fa(nh)
                     with torch.cuda.stream(st):
-                        yt = run_tail(nt)
+                        yb = fb(nt)
                     eh, et = torch.cuda.Event(), torch.cuda.Event()
                     eh.record(sh)
                     et.record(st)
                     main_s.wait_event(eh)
                     main_s.wait_event(et)
-                    return yh, yt
+                    return ya, yb
 
-                tb_ms = elapsed(both)
-                yh, yt = both()
+                t = elapsed(both)
+                ya, yb = both()
                 torch.cuda.synchronize()
-                same = bool(torch.equal(yt[rows_tail], ref[rows_tail]))
-                head_rows = head[:, 0].long()
-                same = same and bool(torch.equal(yh[head_rows], ref[head_rows]))
-                res[f"{lay}_tail{nt}"] = {"head_ms": round(th, 3), "tail_ms": round(tt, 3), "both_ms": round(tb_ms, 3),
-                                          "bits_equal": same}
+                if split == "head|tail":
+                    same = torch.equal(ya[head_rows], ref[head_rows]) and torch.equal(yb[rows_tail], ref[rows_tail])
+                else:
+                    same = (torch.equal(ya[long_rows], ref[long_rows]) and torch.equal(yb[0][mid_rows], ref[mid_rows])
+                            and torch.equal(yb[1][rows_tail], ref[rows_tail]))
+                res[f"{split}:{nt}"] = {"both_ms": round(t, 3), "bits_equal": bool(same)}
     print(json.dumps({k: round(v, 3) if isinstance(v, float) else v for k, v in res.items()}), flush=True)
 
 
