@@ -406,37 +406,16 @@ template <int RED, bool WEIGHTED, bool GIN, bool FAST, bool TWO>
 __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Args a) {
   using R = RowRed<RED>;
   constexpr int RPW = 2;  // rows per wave per tile
-#ifndef KGX_T2_LO_REG
-#define KGX_T2_LO_REG 4
-#endif
-  constexpr int kHalf = KGX_T2_LO_REG;  // lo-plane k-steps held in registers; the rest in LDS
-  __shared__ u32x4_t wlo[kColBlocks * (kSteps - kHalf) * 64];  // lo plane, k-steps 4..7: 64 KB
-#if KGX_T2_ILV
-  // the two plane buffers as separate objects: the compiler then knows a tile's
-  // plane reads do not alias the next tile's plane writes and may interleave them
-  __shared__ __attribute__((aligned(16))) short tile3a[kPlanes][kRows][kLd], tile3b[kPlanes][kRows][kLd];
-  __shared__ int32_t tile_row_a[kRows], tile_row_b[kRows];
-  __shared__ int32_t row_sink[kWaves][64];  // lanes != 0's copy of a tile_row write (branch-free)
-  auto tile3 = [&](int pb) -> short(*)[kRows][kLd] { return pb ? tile3b : tile3a; };
-  auto tile_row = [&](int pb) -> int32_t* { return pb ? tile_row_b : tile_row_a; };
-#else
-  __shared__ __attribute__((aligned(16))) short tile3_[2][kPlanes][kRows][kLd];  // two tiles of split planes
-  __shared__ int32_t tile_row_[2][kRows];
-  auto tile3 = [&](int pb) -> short(*)[kRows][kLd] { return tile3_[pb]; };
-  auto tile_row = [&](int pb) -> int32_t* { return tile_row_[pb]; };
-#endif
+  constexpr int kHalf = kSteps / 2;
+  __shared__ u32x4_t wlo[kColBlocks * kHalf * 64];  // lo plane, k-steps 4..7: 64 KB
+  __shared__ __attribute__((aligned(16))) short tile3[2][kPlanes][kRows][kLd];  // two tiles of split planes
   __shared__ __attribute__((aligned(16))) float sbias[kF];
+  __shared__ int32_t tile_row[2][kRows];
 
   const int wave = threadIdx.x >> 6;
   const int wl = threadIdx.x & 63;
   const int f = wl * 4;
   const int cl = wl & 15, q = wl >> 4;
-#if KGX_T2_STAGGER
-  const bool late = __builtin_amdgcn_readfirstlane(wave) >= 4;  // SIMD partners in opposite phase order
-#endif
-#if KGX_T2_PRIO
-  if (__builtin_amdgcn_readfirstlane(wave) >= 4) __builtin_amdgcn_s_setprio(1);
-#endif
   bf16x8_t wfh[2][kSteps], wfm[2][kSteps], wfl[2][kHalf];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -461,7 +440,7 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Arg
       if (st < kHalf)
         wfl[i][st] = __builtin_bit_cast(bf16x8_t, pl);
       else
-        wlo[((2 * wave + i) * (kSteps - kHalf) + st - kHalf) * 64 + wl] = pl;
+        wlo[((2 * wave + i) * kHalf + st - kHalf) * 64 + wl] = pl;
     }
   }
   if (threadIdx.x < kF) sbias[threadIdx.x] = (a.bias && int(threadIdx.x) < a.F_out) ? a.bias[threadIdx.x] : 0.0f;
@@ -499,15 +478,9 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Arg
         pw[r][0] = rw[B][r].x;
         pw[r][1] = rw[B][r].y;
       }
-#if KGX_T2_NOGATHER  // timing only: every gather reads x[0..2] (cache hits)
-      vload<4>(pv[r][0], gsrc256<TWO>(a, (rec[B][r].z & 1)) + f);
-      vload<4>(pv[r][1], gsrc256<TWO>(a, (rec[B][r].w & 1)) + f);
-      if constexpr (GIN) vload<4>(px[r], a.x + row_off(rec[B][r].x & 1, a.ld_x) + f);
-#else
       vload<4>(pv[r][0], gsrc256<TWO>(a, rec[B][r].z) + f);
       vload<4>(pv[r][1], gsrc256<TWO>(a, rec[B][r].w) + f);
       if constexpr (GIN) vload<4>(px[r], a.x + row_off(rec[B][r].x, a.ld_x) + f);
-#endif
     }
   };
   // fold the gathered rows, split them into plane buffer pb; tile_row too
@@ -527,18 +500,17 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Arg
         val[k] = rid[r] >= 0 ? v : 0.0f;
       }
       if (!FAST && rid[r] >= 0 && a.agg_out) vstore<4>(a.agg_out + int64_t(rid[r]) * a.ld_agg + f, val);
-      put_row(tile3(pb), RPW * wave + r, f, val);
-      if (wl == 0) tile_row(pb)[RPW * wave + r] = rid[r];
+      put_row(tile3[pb], RPW * wave + r, f, val);
+      if (wl == 0) tile_row[pb][RPW * wave + r] = rid[r];
     }
   };
   // tile in plane buffer pb times W; FASTS = unconditional stores (every row valid)
   auto mfma = [&](auto FT, int pb) {
     constexpr bool FASTS = decltype(FT)::value;
-    const short(*t3)[kRows][kLd] = tile3(pb);
+    const short(*t3)[kRows][kLd] = tile3[pb];
     const bool mf0 = FASTS || 32 * wave < a.F_out, mf1 = FASTS || 32 * wave + 16 < a.F_out;
     if (!mf0) return;
     f32x4 d[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
-#if !KGX_T2_NOMFMA  // timing only: no MFMA phase (zeros stored)
 #pragma unroll
     for (int st = 0; st < kSteps; ++st) {
       const int kk = 64 * q + 8 * st;
@@ -549,7 +521,7 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Arg
       for (int i = 0; i < 2; ++i) {
         if (i == 1 && !mf1) break;
         const bf16x8_t wf_lo = st < kHalf ? wfl[i][st < kHalf ? st : 0]
-                                          : __builtin_bit_cast(bf16x8_t, wlo[((2 * wave + i) * (kSteps - kHalf) + (st >= kHalf ? st - kHalf : 0)) * 64 + wl]);
+                                          : __builtin_bit_cast(bf16x8_t, wlo[((2 * wave + i) * kHalf + (st >= kHalf ? st - kHalf : 0)) * 64 + wl]);
         d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[i][st], xl, d[i], 0, 0, 0);
         d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf_lo, xh, d[i], 0, 0, 0);
         d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfm[i][st], xm, d[i], 0, 0, 0);
@@ -558,8 +530,7 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Arg
         d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[i][st], xh, d[i], 0, 0, 0);
       }
     }
-#endif
-    const int rr = tile_row(pb)[cl];
+    const int rr = tile_row[pb][cl];
     if (!FASTS && rr < 0) return;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -576,166 +547,6 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Arg
       *dst = v;
     }
   };
-#if KGX_T2_ILV && KGX_T2_ILV != 3
-  // A full-tile (FAST) period as one basic block, so the scheduler can place
-  // tile t+1's fold / split / plane writes in the issue slots tile t's MFMAs
-  // leave free: the fold's exact split (split3_pair_rn) is written whatever the
-  // values, and the rare non-finite / huge rows are re-split exactly
-  // (split3_a_lo) after the MFMAs, before the barrier that publishes them.
-  auto period_ilv = [&](auto PT, int64_t base) {
-    constexpr int P = decltype(PT)::value;
-    float vals[RPW][4];
-    bool ok = true;
-#pragma unroll
-    for (int r = 0; r < RPW; ++r) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float acc = R::init();
-        const float m0 = WEIGHTED ? __fmul_rn(pv[r][0][k], pw[r][0]) : pv[r][0][k];
-        const float m1 = WEIGHTED ? __fmul_rn(pv[r][1][k], pw[r][1]) : pv[r][1][k];
-        acc = R::combine(acc, rdeg[r] > 0 ? R::msg(m0) : R::init());
-        acc = R::combine(acc, rdeg[r] > 1 ? R::msg(m1) : R::init());
-        float v = R::finish(acc, rdeg[r]);
-        if constexpr (GIN) v = __fadd_rn(__fmul_rn(a.gin_scale, px[r][k]), v);
-        vals[r][k] = rid[r] >= 0 ? v : 0.0f;  // tile t+1 may be the partial last tile
-      }
-      ok = ok && split_fast_ok(vals[r][0], vals[r][1], vals[r][2], vals[r][3]);
-      uint32_t h0, m0, l0, h1, m1, l1;
-      split3_pair_rn(vals[r][0], vals[r][1], h0, m0, l0);
-      split3_pair_rn(vals[r][2], vals[r][3], h1, m1, l1);
-      const int t = RPW * wave + r;
-      *reinterpret_cast<uint2*>(&tile3(P ^ 1)[0][t][f]) = make_uint2(h0, h1);
-      *reinterpret_cast<uint2*>(&tile3(P ^ 1)[1][t][f]) = make_uint2(m0, m1);
-      *reinterpret_cast<uint2*>(&tile3(P ^ 1)[2][t][f]) = make_uint2(l0, l1);
-      *(wl == 0 ? &tile_row(P ^ 1)[t] : &row_sink[wave][wl]) = rid[r];
-    }
-    issue(std::integral_constant<int, P>{});
-    load_rec(P ^ 1, base + 3 * stride + RPW * wave);
-    mfma(std::true_type{}, P);
-#if KGX_T2_ILV == 2
-#pragma unroll
-    for (int st = 0; st < kSteps; ++st) {
-      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);  // the k-step's plane / lo reads
-#pragma unroll
-      for (int m = 0; m < 12; ++m) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // two VALU in its shadow
-      }
-    }
-#endif
-    if (!__all(ok)) {  // rare (inf / NaN / |v| >= 0x1.ffp127 in a row of this wave): exact planes
-#pragma unroll
-      for (int r = 0; r < RPW; ++r) put_row(tile3(P ^ 1), RPW * wave + r, f, vals[r]);
-    }
-    lds_barrier();
-  };
-#endif
-#if KGX_T2_ILV == 3
-  // The same period as eight pieces, one per k-step of tile t's MFMAs, each
-  // followed by a slice of tile t+1's preparation (fold / split / plane writes of
-  // a row, the gathers of tile t+2, the records of tile t+3) and pinned by a
-  // scheduling fence, so the wave's own VALU work runs between its MFMAs; the
-  // next k-step's operands are read from LDS one piece ahead.
-  auto period_ilv3 = [&](auto PT, int64_t base) {
-    constexpr int P = decltype(PT)::value;
-    const short(*t3)[kRows][kLd] = tile3(P);
-    f32x4 d[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
-    bf16x8_t xf[2][3], lo[2][2];
-    float vals[RPW][4];
-    uint32_t pln[RPW][6];
-    auto rd = [&](auto ST) {  // k-step ST's x planes (and W lo from LDS) into slot ST & 1
-      constexpr int st = decltype(ST)::value;
-      const int kk = 64 * q + 8 * st;
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl) xf[st & 1][pl] = *reinterpret_cast<const bf16x8_t*>(&t3[pl][cl][kk]);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-        lo[st & 1][i] = st < kHalf ? wfl[i][st < kHalf ? st : 0]
-                                   : __builtin_bit_cast(bf16x8_t, wlo[((2 * wave + i) * (kSteps - kHalf) + (st >= kHalf ? st - kHalf : 0)) * 64 + wl]);
-    };
-    auto mm = [&](auto ST) {
-      constexpr int st = decltype(ST)::value;
-      const bf16x8_t xh = xf[st & 1][0], xm = xf[st & 1][1], xl = xf[st & 1][2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[i][st], xl, d[i], 0, 0, 0);
-        d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lo[st & 1][i], xh, d[i], 0, 0, 0);
-        d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfm[i][st], xm, d[i], 0, 0, 0);
-        d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[i][st], xm, d[i], 0, 0, 0);
-        d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfm[i][st], xh, d[i], 0, 0, 0);
-        d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfh[i][st], xh, d[i], 0, 0, 0);
-      }
-    };
-    auto fold_row = [&](int r) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float acc = R::init();
-        const float m0 = WEIGHTED ? __fmul_rn(pv[r][0][k], pw[r][0]) : pv[r][0][k];
-        const float m1 = WEIGHTED ? __fmul_rn(pv[r][1][k], pw[r][1]) : pv[r][1][k];
-        acc = R::combine(acc, rdeg[r] > 0 ? R::msg(m0) : R::init());
-        acc = R::combine(acc, rdeg[r] > 1 ? R::msg(m1) : R::init());
-        float v = R::finish(acc, rdeg[r]);
-        if constexpr (GIN) v = __fadd_rn(__fmul_rn(a.gin_scale, px[r][k]), v);
-        vals[r][k] = rid[r] >= 0 ? v : 0.0f;  // tile t+1 may be the partial last tile
-      }
-    };
-    auto split_row = [&](int r) {
-      split3_pair_rn(vals[r][0], vals[r][1], pln[r][0], pln[r][1], pln[r][2]);
-      split3_pair_rn(vals[r][2], vals[r][3], pln[r][3], pln[r][4], pln[r][5]);
-      if (!__all(split_fast_ok(vals[r][0], vals[r][1], vals[r][2], vals[r][3]))) {  // rare: exact planes
-        short h[4], m_[4], l[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) split3_a_lo(vals[r][k], h[k], m_[k], l[k]);
-        auto pk = [](short x, short y) { return uint32_t(uint16_t(x)) | (uint32_t(uint16_t(y)) << 16); };
-        const bool fine = split_fast_ok(vals[r][0], vals[r][1], vals[r][2], vals[r][3]);
-        pln[r][0] = fine ? pln[r][0] : pk(h[0], h[1]);
-        pln[r][1] = fine ? pln[r][1] : pk(m_[0], m_[1]);
-        pln[r][2] = fine ? pln[r][2] : pk(l[0], l[1]);
-        pln[r][3] = fine ? pln[r][3] : pk(h[2], h[3]);
-        pln[r][4] = fine ? pln[r][4] : pk(m_[2], m_[3]);
-        pln[r][5] = fine ? pln[r][5] : pk(l[2], l[3]);
-      }
-    };
-    auto write_row = [&](int r) {
-      const int t = RPW * wave + r;
-      *reinterpret_cast<uint2*>(&tile3(P ^ 1)[0][t][f]) = make_uint2(pln[r][0], pln[r][3]);
-      *reinterpret_cast<uint2*>(&tile3(P ^ 1)[1][t][f]) = make_uint2(pln[r][1], pln[r][4]);
-      *reinterpret_cast<uint2*>(&tile3(P ^ 1)[2][t][f]) = make_uint2(pln[r][2], pln[r][5]);
-      *(wl == 0 ? &tile_row(P ^ 1)[t] : &row_sink[wave][wl]) = rid[r];
-    };
-    using C0 = std::integral_constant<int, 0>;
-    using C1 = std::integral_constant<int, 1>;
-    using C2 = std::integral_constant<int, 2>;
-    using C3 = std::integral_constant<int, 3>;
-    using C4 = std::integral_constant<int, 4>;
-    using C5 = std::integral_constant<int, 5>;
-    using C6 = std::integral_constant<int, 6>;
-    using C7 = std::integral_constant<int, 7>;
-#define KGX_FENCE() __builtin_amdgcn_sched_barrier(0)
-    rd(C0{});
-    KGX_FENCE();
-    rd(C1{}); mm(C0{}); KGX_FENCE();
-    rd(C2{}); mm(C1{}); fold_row(0); KGX_FENCE();
-    rd(C3{}); mm(C2{}); split_row(0); KGX_FENCE();
-    rd(C4{}); mm(C3{}); write_row(0); fold_row(1); KGX_FENCE();
-    rd(C5{}); mm(C4{}); split_row(1); KGX_FENCE();
-    rd(C6{}); mm(C5{}); write_row(1); KGX_FENCE();
-    rd(C7{}); mm(C6{}); issue(std::integral_constant<int, P>{}); KGX_FENCE();
-    mm(C7{}); load_rec(P ^ 1, base + 3 * stride + RPW * wave); KGX_FENCE();
-#undef KGX_FENCE
-    const int rr = tile_row(P)[cl];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c4 = 32 * wave + 16 * i + 4 * q;
-      float4* dst = reinterpret_cast<float4*>(a.out + int64_t(rr) * a.ld_o + c4);
-      const float4 b4 = *reinterpret_cast<const float4*>(&sbias[c4]);
-      float4 v = make_float4(d[i][0] + b4.x, d[i][1] + b4.y, d[i][2] + b4.z, d[i][3] + b4.w);
-      if (a.relu) v = make_float4(fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f), fmaxf(v.z, 0.0f), fmaxf(v.w, 0.0f));
-      *dst = v;
-    }
-    lds_barrier();
-  };
-#endif
   // period t (parity p): tile t's MFMAs; tile t+1 folded into buffer p^1; tile
   // t+2's gathers issued from record buffer p; tile t+3's records into buffer p^1
   auto period = [&](auto FT, auto PT, int64_t base) {
@@ -748,18 +559,8 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Arg
     // prepare first: tile t+2's gathers are issued as early as possible and have
     // the whole period; measured against MFMA-first and a half / half split of
     // the waves (tools/gpu_jobs/gpu_r3_order.sh), this order was fastest
-#if KGX_T2_STAGGER
-    if (late) {
-      mfma(FT, P);
-      prep();
-    } else {
-      prep();
-      mfma(FT, P);
-    }
-#else
     prep();
     mfma(FT, P);
-#endif
     lds_barrier();
   };
   using P0 = std::integral_constant<int, 0>;
@@ -778,20 +579,10 @@ __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_tiny2_kernel(F256Arg
   int par = 0;
   for (;;) {
     if (base + kRows > n) break;
-#if KGX_T2_ILV == 3
-    if constexpr (FAST) period_ilv3(P0{}, base); else
-#elif KGX_T2_ILV
-    if constexpr (FAST) period_ilv(P0{}, base); else
-#endif
     period(std::integral_constant<bool, FAST>{}, P0{}, base);
     base += stride;
     par = 1;
     if (base + kRows > n) break;
-#if KGX_T2_ILV == 3
-    if constexpr (FAST) period_ilv3(P1{}, base); else
-#elif KGX_T2_ILV
-    if constexpr (FAST) period_ilv(P1{}, base); else
-#endif
     period(std::integral_constant<bool, FAST>{}, P1{}, base);
     base += stride;
     par = 0;
@@ -862,10 +653,7 @@ template <typename K>
 unsigned grid256(K k, int64_t tiles, int cus = 0) {
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, 0) != hipSuccess || per_cu <= 0) per_cu = 1;
-  int64_t cap = int64_t(per_cu) * (cus > 0 ? cus : cu_count());
-#if KGX_EXP_GRID_CUS  // measurement builds: the grid of a launch on a CU-masked stream (KGX_EXP_CUS CUs)
-  if (const char* e = getenv("KGX_EXP_CUS")) cap = int64_t(per_cu) * atoi(e);
-#endif
+  const int64_t cap = int64_t(per_cu) * (cus > 0 ? cus : cu_count());
   return unsigned(tiles < cap ? tiles : cap);
 }
 
