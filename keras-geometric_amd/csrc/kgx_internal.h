@@ -8,6 +8,8 @@
 #include <cstdio>
 
 #include <cstdlib>
+#include <mutex>
+#include <vector>
 
 #include "kgx.h"
 
@@ -122,6 +124,102 @@ struct JoinGuard {
     if (fj) (void)hipStreamWaitEvent(s, fj->join, 0);
   }
 };
+
+// Spatial split of the GPU for one fused launch: two CU-masked streams
+// (hipExtStreamCreateWithCUMask) per (host thread, device, split), "tail" over
+// per32 of every 32 CUs and "head" over the rest; launches on them are forked
+// from and joined back into the caller's stream, each grid sized to its CU set.
+struct CuSplit {
+  hipStream_t head = nullptr, tail = nullptr;
+  hipEvent_t fork = nullptr, jh = nullptr, jt = nullptr;
+  int device = -1, per32 = -1, n_head = 0, n_tail = 0;
+};
+
+
+// Every CU-masked stream and its events are destroyed by an atexit handler,
+// which runs before the HIP runtime's own teardown (it is registered after the
+// runtime initialised): left to the runtime, a process exit under rocprofv3's
+// kernel trace crashed in __cxa_finalize once the masked streams existed.
+inline void cu_split_registry(const CuSplit* add) {
+  static std::mutex mu;
+  static std::vector<CuSplit> all;
+  static bool hooked = false;
+  std::lock_guard<std::mutex> lock(mu);
+  if (add) {
+    all.push_back(*add);
+    if (!hooked) {
+      hooked = true;
+      std::atexit([] { cu_split_registry(nullptr); });
+    }
+    return;
+  }
+  for (const CuSplit& c : all) {  // exit: drain and release
+    (void)hipStreamSynchronize(c.head);
+    (void)hipStreamSynchronize(c.tail);
+    (void)hipStreamDestroy(c.head);
+    (void)hipStreamDestroy(c.tail);
+    (void)hipEventDestroy(c.fork);
+    (void)hipEventDestroy(c.jh);
+    (void)hipEventDestroy(c.jt);
+  }
+  all.clear();
+}
+
+// per (host thread, device, split): streams and events made once and kept for
+// the process, like the library's other side streams (a small per-thread cache:
+// a split is never re-created, so streams are not leaked by alternating splits)
+inline CuSplit* cu_split(int per32) {
+  constexpr int kCache = 8;
+  thread_local CuSplit cache[kCache];
+  thread_local int used = 0;
+  int dev = 0;
+  if (per32 <= 0 || per32 >= 32 || hipGetDevice(&dev) != hipSuccess) return nullptr;
+  for (int i = 0; i < used; ++i)
+    if (cache[i].device == dev && cache[i].per32 == per32) return &cache[i];
+  if (used == kCache) return nullptr;  // more (device, split) pairs than any caller uses: run unsplit
+  const int cus = cu_count();
+  uint32_t mh[8] = {0}, mt[8] = {0};
+  int nh = 0, nt = 0;
+  for (int c = 0; c < cus && c < 256; ++c) {
+    if ((c % 32) < per32) {
+      mt[c / 32] |= 1u << (c % 32);
+      ++nt;
+    } else {
+      mh[c / 32] |= 1u << (c % 32);
+      ++nh;
+    }
+  }
+  if (nh == 0 || nt == 0) return nullptr;
+  CuSplit& n = cache[used];
+  if (hipExtStreamCreateWithCUMask(&n.head, 8, mh) != hipSuccess ||
+      hipExtStreamCreateWithCUMask(&n.tail, 8, mt) != hipSuccess ||
+      hipEventCreateWithFlags(&n.fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&n.jh, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&n.jt, hipEventDisableTiming) != hipSuccess)
+    return nullptr;
+  n.device = dev;
+  n.per32 = per32;
+  n.n_head = nh;
+  n.n_tail = nt;
+  ++used;
+  cu_split_registry(&n);
+  return &n;
+}
+
+// joins both CU-masked streams back into the caller's stream on every return
+struct SplitJoin {
+  CuSplit* cs = nullptr;
+  hipStream_t s = nullptr;
+  ~SplitJoin() {
+    if (cs) {
+      (void)hipEventRecord(cs->jh, cs->head);
+      (void)hipEventRecord(cs->jt, cs->tail);
+      (void)hipStreamWaitEvent(s, cs->jh, 0);
+      (void)hipStreamWaitEvent(s, cs->jt, 0);
+    }
+  }
+};
+
 
 inline int next_pow2(int v) {
   int p = 1;

@@ -861,7 +861,9 @@ __global__ __launch_bounds__(256) void spmm_gemm_fixup_kernel(FusedArgs a) {
 
 // KGX_FUSED_FORK (measurement A/B): 1 = the degree <= 2 tail's tiny-row
 // launches run on a forked side stream beside the main and short-row kernels;
-// 2 = the short-row launch goes to the side stream too (before the tiny ones).
+// 2 = the short-row launch goes to the side stream too (before the tiny ones);
+// 3 = the main kernel and the short + tiny launches on disjoint CU sets (24 / 8
+// of every 32 CUs, CU-masked streams, kgx_internal.h cu_split).
 // Disjoint output rows; the latency-bound tail launches fill the main kernel's
 // gathers instead of starting after it; joined before the hub fix-up.
 inline int fused_fork_mode() {  // read per launch (tests switch it in-process)
@@ -870,19 +872,20 @@ inline int fused_fork_mode() {  // read per launch (tests switch it in-process)
 }
 
 template <int RED, bool W, bool TWO, bool NARROW>
-int launch_short(const FusedArgs& a, hipStream_t s) {
+int launch_short(const FusedArgs& a, hipStream_t s, int cus = 0) {
   int per_cu = 0;
   auto k = spmm_gemm_short_kernel<RED, W, TWO, NARROW>;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, 0) != hipSuccess || per_cu <= 0) per_cu = 2;
   const int64_t need = (a.n_short_end - a.n_long + kShortRows - 1) / kShortRows;
-  const int64_t cap = a.share_gpu ? shared_cap(int64_t(per_cu) * cu_count()) : int64_t(per_cu) * cu_count();
+  const int64_t full = int64_t(per_cu) * (cus > 0 ? cus : cu_count());
+  const int64_t cap = a.share_gpu ? shared_cap(full) : full;
   hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kThreads), 0, s, a);
   KGX_CHECK_LAUNCH();
   return KGX_OK;
 }
 
 template <int RED, bool W, bool TWO, bool NARROW>
-int launch_tiny(const FusedArgs& a, hipStream_t s) {
+int launch_tiny(const FusedArgs& a, hipStream_t s, int cus = 0) {
   const bool extra = a.pre_gin || a.agg_out;
   for (int part = 0; part < 2; ++part) {  // one 1024-thread block per CU; degree-2 head, then the degree <= 1 rest
     FusedArgs b = a;
@@ -896,7 +899,8 @@ int launch_tiny(const FusedArgs& a, hipStream_t s) {
                            : spmm_gemm_tiny_kernel<RED, W, false, 2, TWO, NARROW>);
     const int rows = part ? tiny_rows<1>() : tiny_rows<2>();
     const int64_t need = (b.n_tiny + rows - 1) / rows;
-    const int64_t cap = a.share_gpu ? shared_cap(int64_t(cu_count())) : int64_t(cu_count());
+    const int64_t full = cus > 0 ? cus : cu_count();
+    const int64_t cap = a.share_gpu ? shared_cap(full) : full;
     hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kTinyThreads), 0, s, b);
     KGX_CHECK_LAUNCH();
   }
@@ -910,8 +914,45 @@ int launch(const FusedArgs& a, hipStream_t s) {
   ForkJoin* joined = nullptr;
   const bool has_short = a.items && a.n_long < a.n_short_end;
   const int fork = fused_fork_mode();
+  if (fork == 3 && work > 0 && ((a.tpack && a.n_tiny > 0) || has_short)) {
+    // mode 3: the main kernel on a CU-masked stream over 24 of every 32 CUs, the
+    // short-row and tiny-row launches on another over the other 8 (cu_split)
+    CuSplit* cs = cu_split(8);
+    if (cs) {
+      SplitJoin join;
+      KGX_CHECK_HIP(hipEventRecord(cs->fork, s));
+      KGX_CHECK_HIP(hipStreamWaitEvent(cs->head, cs->fork, 0));
+      KGX_CHECK_HIP(hipStreamWaitEvent(cs->tail, cs->fork, 0));
+      join.cs = cs;
+      join.s = s;
+      int per_cu = 0;
+      auto k = spmm_gemm_kernel<RED, W, TWO, NARROW>;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, 0) != hipSuccess || per_cu <= 0)
+        per_cu = 2;
+      const int64_t need = (work + kGroups - 1) / kGroups;
+      const int64_t full = int64_t(per_cu) * cs->n_head;
+      const int64_t cap = a.share_gpu ? shared_cap(full) : full;
+      hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kThreads), 0, cs->head, a);
+      KGX_CHECK_LAUNCH();
+      if (has_short && launch_short<RED, W, TWO, NARROW>(a, cs->tail, cs->n_tail) != KGX_OK) return KGX_ERR_HIP;
+      if (a.tpack && a.n_tiny > 0 && launch_tiny<RED, W, TWO, NARROW>(a, cs->tail, cs->n_tail) != KGX_OK)
+        return KGX_ERR_HIP;
+      join.cs = nullptr;
+      KGX_CHECK_HIP(hipEventRecord(cs->jh, cs->head));
+      KGX_CHECK_HIP(hipEventRecord(cs->jt, cs->tail));
+      KGX_CHECK_HIP(hipStreamWaitEvent(s, cs->jh, 0));
+      KGX_CHECK_HIP(hipStreamWaitEvent(s, cs->jt, 0));
+      if (a.items && a.n_split > 0) {
+        const int64_t blocks = (a.n_split + 7) / 8;
+        auto fk = spmm_gemm_fixup_kernel<RED, NARROW>;
+        hipLaunchKernelGGL(fk, dim3(unsigned(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s, a);
+        KGX_CHECK_LAUNCH();
+      }
+      return KGX_OK;
+    }
+  }
   const bool short_forked = fork == 2 && has_short;
-  if ((a.tpack && a.n_tiny > 0 && fork >= 1) || short_forked) {
+  if ((a.tpack && a.n_tiny > 0 && fork >= 1 && fork <= 2) || short_forked) {
     ForkJoin& fj = fork_join();
     if (hipEventRecord(fj.fork, s) != hipSuccess || hipStreamWaitEvent(fj.side, fj.fork, 0) != hipSuccess) {
       set_error("kgx_spmm_gemm: stream fork failed");

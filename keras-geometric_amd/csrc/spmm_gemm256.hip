@@ -667,66 +667,11 @@ unsigned grid256(K k, int64_t tiles, int cus = 0) {
 // kernel in the same order: the outputs are bit-identical to the one-stream
 // order (tools/exp_cupart.py, tests/test_gpu_fused256.py).  Measured on C4
 // (profiles/r05/c4_cupart*.json): see DESIGN.md §4.
-struct CuSplit {
-  hipStream_t head = nullptr, tail = nullptr;
-  hipEvent_t fork = nullptr, jh = nullptr, jt = nullptr;
-  int device = -1, per32 = -1, n_head = 0, n_tail = 0;
-};
-
 inline int cu_split_per32() {
   const char* e = getenv("KGX_F256_CU_SPLIT");
   const int v = e ? atoi(e) : 8;
   return v > 0 && v < 32 ? v : 0;
 }
-
-// per (host thread, device, split): streams and events made once, kept for the
-// process (like the library's other side streams)
-inline CuSplit* cu_split(int per32) {
-  thread_local CuSplit cs;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  if (cs.device == dev && cs.per32 == per32) return &cs;
-  const int cus = cu_count();
-  uint32_t mh[8] = {0}, mt[8] = {0};
-  int nh = 0, nt = 0;
-  for (int c = 0; c < cus && c < 256; ++c) {
-    if ((c % 32) < per32) {
-      mt[c / 32] |= 1u << (c % 32);
-      ++nt;
-    } else {
-      mh[c / 32] |= 1u << (c % 32);
-      ++nh;
-    }
-  }
-  if (nh == 0 || nt == 0) return nullptr;
-  CuSplit n;
-  if (hipExtStreamCreateWithCUMask(&n.head, 8, mh) != hipSuccess ||
-      hipExtStreamCreateWithCUMask(&n.tail, 8, mt) != hipSuccess ||
-      hipEventCreateWithFlags(&n.fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&n.jh, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&n.jt, hipEventDisableTiming) != hipSuccess)
-    return nullptr;
-  n.device = dev;
-  n.per32 = per32;
-  n.n_head = nh;
-  n.n_tail = nt;
-  cs = n;  // the previous split's streams (another device or split) stay alive: launches may still use them
-  return &cs;
-}
-
-// joins both CU-masked streams back into the caller's stream on every return
-struct SplitJoin {
-  CuSplit* cs = nullptr;
-  hipStream_t s = nullptr;
-  ~SplitJoin() {
-    if (cs) {
-      (void)hipEventRecord(cs->jh, cs->head);
-      (void)hipEventRecord(cs->jt, cs->tail);
-      (void)hipStreamWaitEvent(s, cs->jh, 0);
-      (void)hipStreamWaitEvent(s, cs->jt, 0);
-    }
-  }
-};
 
 template <int RED, bool WT, bool TWO>
 int launch256(const F256Args& a, hipStream_t s) {
