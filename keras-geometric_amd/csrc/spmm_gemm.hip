@@ -917,7 +917,8 @@ int launch(const FusedArgs& a, hipStream_t s) {
   if (fork == 3 && work > 0 && ((a.tpack && a.n_tiny > 0) || has_short)) {
     // mode 3: the main kernel on a CU-masked stream over 24 of every 32 CUs, the
     // short-row and tiny-row launches on another over the other 8 (cu_split)
-    CuSplit* cs = cu_split(8);
+    const char* e = getenv("KGX_FUSED_CU_SPLIT");  // tail CUs per 32 (measurement A/B)
+    CuSplit* cs = cu_split(e ? atoi(e) : 8);
     if (cs) {
       SplitJoin join;
       KGX_CHECK_HIP(hipEventRecord(cs->fork, s));
