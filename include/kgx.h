@@ -230,12 +230,15 @@ int kgx_dropout_mask(uint64_t seed, float p, const int32_t* keys, int64_t n, int
  * first Dense (gin_conv.py:129-162) or SAGEConv's activation; with ACCUMULATE
  * it applies to the sum (out = max(out + ..., 0)).  kgx_spmm_gemm_f256 rejects
  * RELU | ACCUMULATE. */
-/* KGX_FUSED_CU_SPLIT (kgx_spmm_gemm_f256 / _f256_ex only): run the degree <= 2
- * tail (MFMA-bound) on a CU-masked stream over 8 of every 32 CUs, beside the
- * long-row and degree 3..7 launches (memory-bound) on the other CUs; both
+/* KGX_FUSED_CU_SPLIT: run the schedule's tail launches on a CU-masked stream
+ * over 8 of every 32 CUs, beside the main launches on the other CUs; both
  * streams are forked from and joined back into `stream` (before the hub
  * fix-up).  Outputs are bit-identical to the one-stream order.
- * KGX_F256_CU_SPLIT (environment) = tail CUs per 32, 0 = ignore the flag. */
+ * kgx_spmm_gemm_f256 / _f256_ex: the tail is the degree <= 2 records (MFMA-
+ * bound), the main part the long rows and degree 3..7 (memory-bound);
+ * KGX_F256_CU_SPLIT (environment) = tail CUs per 32, 0 = ignore the flag.
+ * kgx_spmm_gemm*: the tail is the short-row and tiny-record launches, the main
+ * part spmm_gemm_kernel; KGX_FUSED_CU_SPLIT (environment) = tail CUs per 32. */
 enum { KGX_FUSED_PRE_GIN = 1, KGX_FUSED_ACCUMULATE = 2, KGX_FUSED_SHARE_GPU = 4, KGX_FUSED_RELU = 8,
        KGX_FUSED_CU_SPLIT = 16 };
 int kgx_spmm_gemm(int reduce, const int32_t* rowptr, const int32_t* rows, int64_t n_rows,

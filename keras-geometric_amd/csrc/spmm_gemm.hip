@@ -87,6 +87,7 @@ struct FusedArgs {
   // the gather address is one select of the base.  n_x1 = INT32_MAX: one table.
   const float* x2b;
   int32_t n_x1;
+  bool cu_split;  // KGX_FUSED_CU_SPLIT (host side only)
 };
 
 // Source row of column c: x[c], or with TWO x2[c - n_x1] (one 64-bit select per
@@ -913,11 +914,11 @@ int launch(const FusedArgs& a, hipStream_t s) {
   JoinGuard guard;
   ForkJoin* joined = nullptr;
   const bool has_short = a.items && a.n_long < a.n_short_end;
-  const int fork = fused_fork_mode();
+  const int fork = a.cu_split ? 3 : fused_fork_mode();
   if (fork == 3 && work > 0 && ((a.tpack && a.n_tiny > 0) || has_short)) {
     // mode 3: the main kernel on a CU-masked stream over 24 of every 32 CUs, the
     // short-row and tiny-row launches on another over the other 8 (cu_split)
-    const char* e = getenv("KGX_FUSED_CU_SPLIT");  // tail CUs per 32 (measurement A/B)
+    const char* e = getenv("KGX_FUSED_CU_SPLIT");  // tail CUs per 32 (default 8)
     CuSplit* cs = cu_split(e ? atoi(e) : 8);
     if (cs) {
       SplitJoin join;
@@ -1076,7 +1077,8 @@ extern "C" int kgx_spmm_gemm_ex3(int reduce, const int32_t* rowptr, const int32_
   KGX_REQUIRE(F_out > 0 && F_out <= 128 && F_out % 4 == 0, KGX_ERR_UNSUPPORTED,
               "kgx_spmm_gemm: F_out must be a multiple of 4 <= 128 (got %lld)", (long long)F_out);
   KGX_REQUIRE(n_rows >= 0 && n_items >= 0 && n_split >= 0, KGX_ERR_ARG, "kgx_spmm_gemm: negative size");
-  KGX_REQUIRE((flags & ~(KGX_FUSED_PRE_GIN | KGX_FUSED_ACCUMULATE | KGX_FUSED_SHARE_GPU | KGX_FUSED_RELU)) == 0,
+  KGX_REQUIRE((flags & ~(KGX_FUSED_PRE_GIN | KGX_FUSED_ACCUMULATE | KGX_FUSED_SHARE_GPU | KGX_FUSED_RELU |
+                         KGX_FUSED_CU_SPLIT)) == 0,
               KGX_ERR_ARG, "kgx_spmm_gemm: unknown flags 0x%x", flags);
   KGX_REQUIRE(!agg_out || (ld_agg >= F_in && reinterpret_cast<uintptr_t>(agg_out) % 16 == 0 && ld_agg % 4 == 0),
               KGX_ERR_ARG, "kgx_spmm_gemm: agg_out must be 16-byte aligned with ld >= F_in, ld %% 4 == 0");
@@ -1126,6 +1128,7 @@ extern "C" int kgx_spmm_gemm_ex3(int reduce, const int32_t* rowptr, const int32_
   a.accumulate = (flags & KGX_FUSED_ACCUMULATE) != 0;
   a.share_gpu = (flags & KGX_FUSED_SHARE_GPU) != 0;
   a.relu = (flags & KGX_FUSED_RELU) != 0;
+  a.cu_split = (flags & KGX_FUSED_CU_SPLIT) != 0;
   a.gin_scale = gin_scale;
   const bool wt = w != nullptr;
   if (x2) return wt ? launch<KGX_SUM, true, true>(a, stream) : launch<KGX_SUM, false, true>(a, stream);
