@@ -253,6 +253,20 @@ def _f256_cu_split(n_edges: int, n_tiny: int) -> bool:
     return t_split < 0.97 * t_seq
 
 
+def _fused_cu_split(n_edges: int, n_tail_rows: int) -> bool:
+    """Whether a 128-wide fused launch runs its short-row and tiny-record
+    launches on 64 CUs beside spmm_gemm_kernel on the other 192
+    (KGX_FUSED_CU_SPLIT): large schedules with a large tail only -- fitted on
+    the north-star graph (profiles/r05/ns_cusplit*/: 8.62-8.69 against
+    8.92-8.94 ms one-stream; main 8.29 ms on 192 CUs beside the tails' 8.61 on
+    64).  KGX_FUSED_CU_SPLIT: unset = this rule, "0" = never, t > 0 = always,
+    with t of every 32 CUs (only 8 measured well: see DESIGN.md §4)."""
+    env = os.environ.get("KGX_FUSED_CU_SPLIT")
+    if env is not None:
+        return n_tail_rows > 0 and env.strip() not in ("", "0")
+    return n_edges >= 50_000_000 and n_tail_rows >= 2_000_000
+
+
 def _partial_width(x: torch.Tensor) -> int:
     """Floats per hub-chunk partial: the 256-wide kernels 256, kgx_spmm_gemm 128 (any F_in <= 128)."""
     return F256 if x.shape[1] == F256 else 128
@@ -284,6 +298,8 @@ def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, b
     n_long = n_items if n_long < 0 or n_long > n_items else n_long
     n_se, tpack, tw, n_tiny2 = _tiny_abi(items, n_items, n_long, tpack, tw if w is not None else None, n_short_end,
                                          n_tiny2)
+    if items is not None and not _SHARE_GPU and _fused_cu_split(idx.numel(), n_items - n_long):
+        flags |= nat.FUSED_CU_SPLIT
     x2p, n_x1 = _x2_args(x, x2)
     nat.check(
         nat.lib().kgx_spmm_gemm_ex3(
