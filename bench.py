@@ -395,6 +395,7 @@ def main() -> None:
     torch.cuda.synchronize()
 
     kops.EVENT_SINK = []
+    split0 = kops.CU_SPLIT_LAUNCHES
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -405,6 +406,7 @@ def main() -> None:
     elapsed = time.perf_counter() - t0
     events = kops.EVENT_SINK
     kops.EVENT_SINK = None
+    cu_split = kops.CU_SPLIT_LAUNCHES > split0
     # aggregation-kernel time per step (N>1: own-source + halo launches, which overlap)
     kern_ms = sum(s.elapsed_time(e) for s, e in events) / args.steps
     launches = len(events) // args.steps
@@ -527,6 +529,10 @@ def main() -> None:
             # FETCH_SIZE x 2 + WRITE_SIZE: L2 <-> fabric bytes, Infinity-Cache (MALL) hits included
             "traffic_kind": "L2-fabric bytes (TCC FETCH_SIZE/WRITE_SIZE, MALL hits included)" if traffic else None,
             "algorithmic_bytes_per_launch": balg,
+            # KGX_FUSED_CU_SPLIT: the op's launches ran side by side on two CU-masked streams (main
+            # kernel on 192 CUs, tail launches on 64); `achieved` divides by the op's fork-to-join event
+            # time, and rocprof's per-kernel averages of those launches overlap in time
+            "concurrent_launches": "cu-split 192/64" if cu_split else None,
         },
         **({"per_rank": ranks} if ranks is not None else shard_info),
     }
