@@ -256,6 +256,11 @@ def _f256_cu_split(n_edges: int, n_tiny: int) -> bool:
 CU_SPLIT_LAUNCHES = 0  # launches that ran CU-split (KGX_FUSED_CU_SPLIT): bench.py reports it
 
 
+def _count_cu_split() -> None:
+    global CU_SPLIT_LAUNCHES
+    CU_SPLIT_LAUNCHES += 1
+
+
 def _fused_cu_split(n_edges: int, n_tail_rows: int) -> bool:
     """Whether a 128-wide fused launch runs its short-row and tiny-record
     launches on 64 CUs beside spmm_gemm_kernel on the other 192
@@ -295,8 +300,7 @@ def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, b
         if tpack is not None and items is not None and not _SHARE_GPU and \
                 _f256_cu_split(idx.numel(), n_items - (n_short_end if n_short_end >= 0 else n_items)):
             flags |= nat.FUSED_CU_SPLIT
-            global CU_SPLIT_LAUNCHES
-            CU_SPLIT_LAUNCHES += 1
+            _count_cu_split()
         _f256_call(reduce, rowptr, rows, n_dst, items, n_items, split, n_split, idx, w, x, x2, W, bias, flags,
                    gin_scale, out, partials, agg if save_agg else None, dev, tpack, tw, n_short_end, n_long)
         return out, agg
@@ -305,8 +309,7 @@ def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, b
                                          n_tiny2)
     if items is not None and not _SHARE_GPU and _fused_cu_split(idx.numel(), n_items - n_long):
         flags |= nat.FUSED_CU_SPLIT
-        global CU_SPLIT_LAUNCHES
-        CU_SPLIT_LAUNCHES += 1
+        _count_cu_split()
     x2p, n_x1 = _x2_args(x, x2)
     nat.check(
         nat.lib().kgx_spmm_gemm_ex3(
