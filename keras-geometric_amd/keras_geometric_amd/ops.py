@@ -256,6 +256,13 @@ def _f256_cu_split(n_edges: int, n_tiny: int) -> bool:
 CU_SPLIT_LAUNCHES = 0  # launches that ran CU-split (KGX_FUSED_CU_SPLIT): bench.py reports it
 
 
+def _split_allowed() -> bool:
+    """CU-split launches stay off while a launch shares the GPU with an exchange
+    (sharing_gpu: the sharded layers' passes beside RCCL and the packing), unless
+    KGX_CU_SPLIT_SHARED=1 (measurement)."""
+    return not _SHARE_GPU or os.environ.get("KGX_CU_SPLIT_SHARED") == "1"
+
+
 def _count_cu_split() -> None:
     global CU_SPLIT_LAUNCHES
     CU_SPLIT_LAUNCHES += 1
@@ -297,7 +304,7 @@ def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, b
         partials = torch.empty((n_slots, _partial_width(x)), dtype=torch.float32, device=dev)
     flags = int(pre_gin) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0) | (nat.FUSED_RELU if relu else 0)
     if x.shape[1] == F256:
-        if tpack is not None and items is not None and not _SHARE_GPU and \
+        if tpack is not None and items is not None and _split_allowed() and \
                 _f256_cu_split(idx.numel(), n_items - (n_short_end if n_short_end >= 0 else n_items)):
             flags |= nat.FUSED_CU_SPLIT
             _count_cu_split()
@@ -307,7 +314,7 @@ def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, b
     n_long = n_items if n_long < 0 or n_long > n_items else n_long
     n_se, tpack, tw, n_tiny2 = _tiny_abi(items, n_items, n_long, tpack, tw if w is not None else None, n_short_end,
                                          n_tiny2)
-    if items is not None and not _SHARE_GPU and _fused_cu_split(idx.numel(), n_items - n_long):
+    if items is not None and _split_allowed() and _fused_cu_split(idx.numel(), n_items - n_long):
         flags |= nat.FUSED_CU_SPLIT
         _count_cu_split()
     x2p, n_x1 = _x2_args(x, x2)
@@ -434,7 +441,7 @@ def spmm_gemm_acc_(
     if items is not None and n_split > 0:
         partials = torch.empty((n_slots, _partial_width(x)), dtype=torch.float32, device=dev)
     if x.shape[1] == F256:
-        if tpack is not None and items is not None and not _SHARE_GPU and \
+        if tpack is not None and items is not None and _split_allowed() and \
                 _f256_cu_split(idx.numel(), n_items - (n_short_end if n_short_end >= 0 else n_items)):
             flags |= nat.FUSED_CU_SPLIT
         _f256_call(reduce, rowptr, rows, n_dst, items, n_items, split, n_split, idx, w, x, x2, W, bias,
@@ -444,6 +451,9 @@ def spmm_gemm_acc_(
     n_long = n_items if n_long < 0 or n_long > n_items else n_long
     n_se, tpack, tw, n_tiny2 = _tiny_abi(items, n_items, n_long, tpack, tw if w is not None else None, n_short_end,
                                          n_tiny2)
+    if items is not None and _split_allowed() and _fused_cu_split(idx.numel(), n_items - n_long):
+        flags |= nat.FUSED_CU_SPLIT
+        _count_cu_split()
     x2p, n_x1 = _x2_args(x, x2)
     nat.check(
         nat.lib().kgx_spmm_gemm_ex3(
