@@ -909,7 +909,7 @@ class ShardedGraph:
         self.exchange_plan(self.halo_k)
         return candidates[i]
 
-    def merged_passes(self, pp: PushPullPlan, unit: str | None = None):
+    def merged_passes(self, pp: PushPullPlan, unit: str | None = None, light: int = 0):
         """(g_a, g_b, later): the default path's passes with the first exchange
         group folded into the rows it touches (cached on the plan per unit).
 
@@ -926,12 +926,20 @@ class ShardedGraph:
         [(step to wait for, CSR, halo lo, halo hi)] for the remaining groups,
         accumulate-only over the rows each touches.  Each row's sum is own
         edges, then first-group edges, then later groups: a re-association of
-        the one-pass order, tolerance-equal like the rest of this path."""
+        the one-pass order, tolerance-equal like the rest of this path.
+
+        light > 0 (ShardedGCNConv only; KGX_HALO_LIGHT): rows of total degree <=
+        light whose edges reach a later group are taken out of g_a / g_b / the
+        later passes and written once each, with all their edges, by a
+        two-table pass right after the last group they need has landed
+        (ShardedGraph.light_passes) -- the short / tiny-row launches then see
+        each light row once instead of once per pass it is touched by."""
         unit = unit or self.merge_unit or os.environ.get("KGX_HALO_MERGE", "step")
         if pp.merged is None:
             pp.merged = {}
-        if unit in pp.merged:
-            return pp.merged[unit]
+        key = unit if light <= 0 or unit == "none" else (unit, light)
+        if key in pp.merged:
+            return pp.merged[key]
         g_own, _ = self.own_halo_parts()
         n_local = self.n_local
         dev = g_own.col.device
@@ -967,11 +975,68 @@ class ShardedGraph:
         g_b = self.backend.build_graph(cols.to(torch.int32), rows.to(torch.int32), n_local + pp.n_rows, n_local, 128)
         if pp.weighted:
             g_b.w = torch.cat([g_own.w[keep], first.w])[g_b.eid.long()].contiguous()
-        g_b = self.backend.restrict_rows(g_b, in_h)
-        g_a = self.backend.restrict_rows(g_own, ~in_h)
+        defer = torch.zeros(n_local, dtype=torch.bool, device=dev)
+        if light > 0:
+            total = g_own.deg.long().clone()
+            need = torch.full((n_local,), -1, dtype=torch.long, device=dev)
+            for gi, (_, g, _, _) in enumerate(groups):
+                total += g.deg.long()
+                need = torch.where(g.deg > 0, torch.full_like(need, gi), need)
+            defer = (total <= light) & (need >= 1)
+            pp.merged[("light_rows", key)] = (defer, need)
+        g_b = self.backend.restrict_rows(g_b, in_h & ~defer)
+        g_a = self.backend.restrict_rows(g_own, ~in_h & ~defer)
         later = [t for t in groups[1:] if t[1].kept]
-        pp.merged[unit] = (g_a, g_b, later, groups[0][0])
-        return pp.merged[unit]
+        if light > 0:
+            later = [(i, self.backend.restrict_rows(g, ~defer), lo, hi) for (i, g, lo, hi) in later]
+            later = [t for t in later if t[1].kept]
+            pp.merged[("light_groups", key)] = groups
+        pp.merged[key] = (g_a, g_b, later, groups[0][0])
+        return pp.merged[key]
+
+    def light_passes(self, pp: PushPullPlan, unit: str, light: int):
+        """[(wait step, CSR)] for merged_passes(..., light): per later group j,
+        the deferred light rows whose last edge group is j, with their own edges
+        then every group's edges up to j (sources >= n_local index the halo
+        buffer), for one two-table overwriting pass once group j has landed."""
+        key = (unit, light)
+        lk = ("light", key)
+        if lk in pp.merged:
+            return pp.merged[lk]
+        self.merged_passes(pp, unit, light)
+        groups = pp.merged[("light_groups", key)]
+        defer, need = pp.merged[("light_rows", key)]
+        g_own, _ = self.own_halo_parts()
+        n_local = self.n_local
+        dev = g_own.col.device
+        ar = torch.arange(n_local, device=dev)
+        out = []
+        for j in range(1, len(groups)):
+            sel = defer & (need == j)
+            if not bool(sel.any()):
+                continue
+            rows, cols, ws = [], [], []
+            r_own = torch.repeat_interleave(ar, g_own.deg.long(), output_size=g_own.kept)
+            k_own = sel[r_own]
+            rows.append(r_own[k_own])
+            cols.append(g_own.col[k_own].long())
+            if pp.weighted:
+                ws.append(g_own.w[k_own])
+            for gi in range(j + 1):
+                _, g, lo, _ = groups[gi]
+                r_g = torch.repeat_interleave(ar, g.deg.long(), output_size=g.kept)
+                k_g = sel[r_g]
+                rows.append(r_g[k_g])
+                cols.append(g.col[k_g].long() + (n_local + lo))
+                if pp.weighted:
+                    ws.append(g.w[k_g])
+            gl = self.backend.build_graph(torch.cat(cols).to(torch.int32), torch.cat(rows).to(torch.int32),
+                                          n_local + pp.n_rows, n_local, 128)
+            if pp.weighted:
+                gl.w = torch.cat(ws)[gl.eid.long()].contiguous()
+            out.append((groups[j][0], self.backend.restrict_rows(gl, sel)))
+        pp.merged[lk] = out
+        return out
 
     def group_passes(self, pp: PushPullPlan):
         """(g_a, [(wait step, g_k)]) for a destination-group plan (kind "group"):
@@ -1365,7 +1430,10 @@ class ShardedGCNConv(Layer):
         + A_0 halo_0) W in one two-table pass; then out += (A_s halo_s) W per
         later step (pushed partials, later chunks) as each lands."""
         sg = self.sg
-        g_a, g_b, later, first_wait = sg.merged_passes(pp)
+        unit = sg.merge_unit or os.environ.get("KGX_HALO_MERGE", "step")
+        light = halo_light() if pp.kind != "allgather" else 0
+        g_a, g_b, later, first_wait = sg.merged_passes(pp, unit, light)
+        lights = sg.light_passes(pp, unit, light) if light > 0 and g_b is not None and unit != "none" else []
         steps = [st for c in pp.chunks for st in c.steps]
         # the own-only rows' pass (g_a) after the merged pass when two or more exchange
         # groups follow the first: then the first pack runs alone and the first transfer
@@ -1410,13 +1478,34 @@ class ShardedGCNConv(Layer):
                     with kops.sharing_gpu() if later else contextlib.nullcontext():
                         sg.backend.aggregate_transform(g_a, x_local, self.kernel, bias=bias, out=out,
                                                        accumulate=False)
+            pending = list(lights)  # light rows, each written once after the last group it needs
             for n, (i, g, lo, hi) in enumerate(later):
                 wait_step(i)
-                with kops.sharing_gpu() if n + 1 < len(later) else contextlib.nullcontext():
+                last = n + 1 == len(later)
+                with kops.sharing_gpu() if not last else contextlib.nullcontext():
                     sg.backend.aggregate_transform(g, halo[lo: hi], self.kernel, out=out)
+                while pending and pending[0][0] <= i:
+                    _, gl = pending.pop(0)
+                    with kops.sharing_gpu() if not last else contextlib.nullcontext():
+                        sg.backend.aggregate_transform(gl, x_local, self.kernel, bias=bias, out=out, x2=halo,
+                                                       accumulate=False)
+            for i, gl in pending:  # groups with light rows but no accumulate pass left
+                wait_step(i)
+                sg.backend.aggregate_transform(gl, x_local, self.kernel, bias=bias, out=out, x2=halo,
+                                               accumulate=False)
             # every step, used or not: also orders the side stream's reads of x_local
             wait_step(len(steps) - 1)
         return out
+
+
+def halo_light() -> int:
+    """KGX_HALO_LIGHT: rows of total degree <= this many edges are written once,
+    after the last exchange group they need (ShardedGraph.merged_passes);
+    0 = off."""
+    try:
+        return max(0, int(os.environ.get("KGX_HALO_LIGHT", "0")))
+    except ValueError:
+        return 0
 
 
 class _ShardedGCNFn(torch.autograd.Function):

@@ -278,6 +278,20 @@ def _worker(rank, world, chunks, port, q):
                 assert sizes[0] <= 0.25 * pp.n_rows + world, sizes
             finally:
                 del os.environ["KGX_HALO_FIRST"]
+        # light rows (KGX_HALO_LIGHT): rows of total degree <= L that reach a later exchange
+        # group are written once, with all their edges, after the last group they need
+        ys_light = []
+        for light in ("7", "100000"):
+            os.environ["KGX_HALO_LIGHT"] = light
+            try:
+                with torch.no_grad():
+                    ys_light.append(layer(torch.from_numpy(x[lo:hi])).numpy())
+            finally:
+                del os.environ["KGX_HALO_LIGHT"]
+            if chunks > 1:
+                unit = sg.merge_unit or "step"
+                lp = sg.light_passes(sg._pp, unit, int(light))
+                assert lp, light  # some rows were deferred
         # K left open: the first forward times K = 1 / 2 / 4 (collective) and keeps the fastest
         sg2 = kd.ShardedGraph.build(torch.from_numpy(s[keep]), torch.from_numpy(d[keep]), bounds,
                                     backend=OracleBackend(), n_features=F_OUT)
@@ -354,7 +368,7 @@ def _worker(rank, world, chunks, port, q):
         assert torch.equal(y_again, y)
         q.put((rank, gcn.numpy(), mx.numpy(), sg.n_halo, sum(sg.send_counts), y.numpy(), y_pull.numpy(), pp.n_push,
                y_tuned.numpy(), y_unfused.numpy(), y_wide.numpy(), y_unmerged.numpy(), ys_gather[0], ys_gather[1],
-               y_chunk.numpy(), y_pullplan, y_first.numpy(), ys_group[0], ys_group[1]))
+               y_chunk.numpy(), y_pullplan, y_first.numpy(), ys_group[0], ys_group[1], ys_light[0], ys_light[1]))
     finally:
         dist.destroy_process_group()
 
@@ -396,7 +410,7 @@ def test_sharded_equals_unsharded_bitwise(world, chunks):
     # overlapped layer path, push-pull and pull-only halos: own-source part, then
     # one part per halo chunk per row (re-associated sums)
     assert sum(results[r][6] for r in range(world)) > 0  # partial sums were pushed
-    for i in (4, 5, 7, 8, 10, 11, 12, 13, 14, 15, 16, 17):
+    for i in (4, 5, 7, 8, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19):
         y_split = np.concatenate([results[r][i] for r in range(world)])
         err = np.abs(y_split - y) / np.maximum(1, np.abs(y))
         assert err.max() <= 1e-5
