@@ -1501,9 +1501,12 @@ class ShardedGCNConv(Layer):
 def halo_light() -> int:
     """KGX_HALO_LIGHT: rows of total degree <= this many edges are written once,
     after the last exchange group they need (ShardedGraph.merged_passes);
-    0 = off."""
+    0 = off.  Default 7 (the short-row kernel's bound): one-rank simulations of
+    NS weak P = 8, halo K 2 (profiles/r05/sim_light/): compute alone 12.84 ->
+    12.21 ms, at a modelled 400 GB/s 12.99 -> 12.61 ms; 2: 12.92; every row:
+    15.08 (the deferred passes then carry the heavy rows past the last landing)."""
     try:
-        return max(0, int(os.environ.get("KGX_HALO_LIGHT", "0")))
+        return max(0, int(os.environ.get("KGX_HALO_LIGHT", "7")))
     except ValueError:
         return 0
 
