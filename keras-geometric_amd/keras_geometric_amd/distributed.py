@@ -1501,12 +1501,13 @@ class ShardedGCNConv(Layer):
 def halo_light() -> int:
     """KGX_HALO_LIGHT: rows of total degree <= this many edges are written once,
     after the last exchange group they need (ShardedGraph.merged_passes);
-    0 = off.  Default 7 (the short-row kernel's bound): one-rank simulations of
-    NS weak P = 8, halo K 2 (profiles/r05/sim_light/): compute alone 12.84 ->
-    12.21 ms, at a modelled 400 GB/s 12.99 -> 12.61 ms; 2: 12.92; every row:
-    15.08 (the deferred passes then carry the heavy rows past the last landing)."""
+    0 = off.  Default 32, from one-rank simulations of NS weak P = 8, halo K 2,
+    modelled 400 GB/s (profiles/r05/sim_light/, two rounds each): off
+    12.89-12.98 ms, 7: 12.47-12.61, 12: 12.39-12.50, 20: 12.18-12.35, 32:
+    12.12-12.25, 48: 12.21-12.26, 64: 12.45-12.53, every row: 15.08 (the
+    deferred passes then carry the heavy rows past the last landing)."""
     try:
-        return max(0, int(os.environ.get("KGX_HALO_LIGHT", "7")))
+        return max(0, int(os.environ.get("KGX_HALO_LIGHT", "32")))
     except ValueError:
         return 0
 
