@@ -1676,7 +1676,10 @@ class ShardedGINConv(_ShardedWrap):
         if pp.kind == "group":
             return self._forward_fused_grouped(x_local, W, b, pp, halo)
         unit = None if (use_merged_halo() or pp.kind == "allgather") else "none"
-        g_a, g_b, later, first_wait = sg.merged_passes(pp, unit)
+        unit = unit or sg.merge_unit or os.environ.get("KGX_HALO_MERGE", "step")
+        light = halo_light() if pp.kind != "allgather" and unit != "none" else 0
+        g_a, g_b, later, first_wait = sg.merged_passes(pp, unit, light)
+        lights = sg.light_passes(pp, unit, light) if light > 0 and g_b is not None else []
         steps = [st for c in pp.chunks for st in c.steps]
         relu = first.activation is torch.relu
         kw = dict(weighted=False, pre_gin=True, gin_scale=float(conv._scale()), relu=relu and not later)
@@ -1699,10 +1702,21 @@ class ShardedGINConv(_ShardedWrap):
             wait_step(first_wait)
             with kops.sharing_gpu() if later else contextlib.nullcontext():
                 sg.backend.aggregate_transform(g_b, x_local, W, bias=b, out=out, x2=halo, accumulate=False, **kw)
+        kw_light = dict(kw, relu=relu)  # light rows are complete when written: their ReLU goes in
+        pending = list(lights)
         for n, (i, g, lo, hi) in enumerate(later):
             wait_step(i)
-            with kops.sharing_gpu() if n + 1 < len(later) else contextlib.nullcontext():
+            last = n + 1 == len(later)
+            with kops.sharing_gpu() if not last else contextlib.nullcontext():
                 sg.backend.aggregate_transform(g, halo[lo: hi], W, out=out, weighted=False)
+            while pending and pending[0][0] <= i:
+                _, gl = pending.pop(0)
+                with kops.sharing_gpu() if not last else contextlib.nullcontext():
+                    sg.backend.aggregate_transform(gl, x_local, W, bias=b, out=out, x2=halo, accumulate=False,
+                                                   **kw_light)
+        for i, gl in pending:
+            wait_step(i)
+            sg.backend.aggregate_transform(gl, x_local, W, bias=b, out=out, x2=halo, accumulate=False, **kw_light)
         wait_step(len(steps) - 1)  # also orders the side stream's reads of x_local
         if relu and later:
             out = torch.relu_(out)
