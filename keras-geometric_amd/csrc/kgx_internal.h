@@ -181,7 +181,13 @@ inline CuSplit* cu_split(int per32) {
   uint32_t mh[8] = {0}, mt[8] = {0};
   int nh = 0, nt = 0;
   for (int c = 0; c < cus && c < 256; ++c) {
-    if ((c % 32) < per32) {
+    // KGX_CU_SPLIT_INTERLEAVE=1 (measurement): per32 / 4 of every 8 CUs instead of
+    // the first per32 of every 32
+    static const bool inter = [] {
+      const char* e = getenv("KGX_CU_SPLIT_INTERLEAVE");
+      return e && atoi(e) == 1;
+    }();
+    if (inter ? (c % 8) < per32 / 4 : (c % 32) < per32) {
       mt[c / 32] |= 1u << (c % 32);
       ++nt;
     } else {
