@@ -181,9 +181,6 @@ inline CuSplit* cu_split(int per32) {
   uint32_t mh[8] = {0}, mt[8] = {0};
   int nh = 0, nt = 0;
   for (int c = 0; c < cus && c < 256; ++c) {
-    // the first per32 of every 32 mask bits; measured against per32 / 4 of every 8
-    // (same CU count): NS 8.54-8.60 against 11.10-11.14 ms, C4 20.34-20.39 against
-    // 20.24-20.30 (profiles/r05/cu_pattern/)
     if ((c % 32) < per32) {
       mt[c / 32] |= 1u << (c % 32);
       ++nt;
