@@ -1212,8 +1212,12 @@ class ShardedGraph:
         sources, epilogue applied) while the exchange is in flight; the rows
         with them in ONE two-table pass (own then first-step edges, epilogue
         applied) once chunk 0's pulled rows have landed; then out += the later
-        steps' row sums as each lands."""
-        g_a, g_b, later, first_wait = self.merged_passes(pp)
+        steps' row sums as each lands.  Light rows (KGX_HALO_LIGHT) are written
+        once, epilogue applied, after the last step they need."""
+        unit = self.merge_unit or os.environ.get("KGX_HALO_MERGE", "step")
+        light = halo_light() if pp.kind != "allgather" and unit != "none" else 0
+        g_a, g_b, later, first_wait = self.merged_passes(pp, unit, light)
+        lights = self.light_passes(pp, unit, light) if light > 0 and g_b is not None else []
         steps = [st for c in pp.chunks for st in c.steps]
         kw = dict(weighted=weighted, bias=bias, xroot=x_local if fold_gin else None,
                   gin_scale=float(gin_scale) if fold_gin else 1.0)
@@ -1236,9 +1240,16 @@ class ShardedGraph:
             if g_b is not None:
                 wait_step(first_wait)
                 self.backend.aggregate_accumulate(g_b, x_local, out, epilogue=epi, table2=halo, **kw)
+            pending = list(lights)
             for i, g, lo, hi in later:
                 wait_step(i)
                 self.backend.aggregate_accumulate(g, halo[lo: hi], out, weighted=weighted)
+                while pending and pending[0][0] <= i:
+                    _, gl = pending.pop(0)
+                    self.backend.aggregate_accumulate(gl, x_local, out, epilogue=epi, table2=halo, **kw)
+            for i, gl in pending:
+                wait_step(i)
+                self.backend.aggregate_accumulate(gl, x_local, out, epilogue=epi, table2=halo, **kw)
             wait_step(len(steps) - 1)
         return out
 

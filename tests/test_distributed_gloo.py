@@ -236,14 +236,18 @@ def _worker(rank, world, chunks, port, q):
             y = layer(torch.from_numpy(x[lo:hi]))  # push-pull halo (the default)
         pp = sg._pp
         assert pp is not None and pp.n_rows == pp.n_pull + pp.n_push == pp.chunks[-1].hi
-        assert pp.merged is not None and pp.merged["step"][1] is not None  # the first step folded into its rows' pass
+        def merged(unit):  # the plan's cached passes (keyed by unit, with the light-row bound when on)
+            lt = kd.halo_light()
+            return pp.merged[(unit, lt) if lt > 0 else unit]
+
+        assert pp.merged is not None and merged("step")[1] is not None  # the first step folded into its rows' pass
         os.environ["KGX_HALO_MERGE"] = "chunk"  # a chunk's steps (pulled rows + partials) merged together
         try:
             with torch.no_grad():
                 y_chunk = layer(torch.from_numpy(x[lo:hi]))
         finally:
             del os.environ["KGX_HALO_MERGE"]
-        assert pp.merged["chunk"][1] is not None
+        assert merged("chunk")[1] is not None
         # the own-only rows' pass before / after the merged pass (the default picks by the
         # number of later exchange groups): disjoint rows, so the same bits either way
         for order in ("0", "1"):
