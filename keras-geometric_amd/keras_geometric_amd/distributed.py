@@ -1212,10 +1212,14 @@ class ShardedGraph:
         sources, epilogue applied) while the exchange is in flight; the rows
         with them in ONE two-table pass (own then first-step edges, epilogue
         applied) once chunk 0's pulled rows have landed; then out += the later
-        steps' row sums as each lands.  Light rows (KGX_HALO_LIGHT) are written
-        once, epilogue applied, after the last step they need."""
+        steps' row sums as each lands.  Light rows are written once, epilogue
+        applied, after the last step they need -- only when KGX_HALO_LIGHT is set
+        explicitly: on these plain sum / mean passes the C5 simulation (SAGE mean,
+        strong P = 4, 400 GB/s) measured it slower (K 1: 2.57 -> 2.64 ms, K 2:
+        3.20 -> 3.53; profiles/r05/sim_light/c5_*)."""
         unit = self.merge_unit or os.environ.get("KGX_HALO_MERGE", "step")
-        light = halo_light() if pp.kind != "allgather" and unit != "none" else 0
+        light = halo_light() if (pp.kind != "allgather" and unit != "none"
+                                 and os.environ.get("KGX_HALO_LIGHT") is not None) else 0
         g_a, g_b, later, first_wait = self.merged_passes(pp, unit, light)
         lights = self.light_passes(pp, unit, light) if light > 0 and g_b is not None else []
         steps = [st for c in pp.chunks for st in c.steps]
