@@ -456,6 +456,13 @@ def _conv_worker(rank, world, port, q):
                         grouped.append(layer(xl).numpy())  # checked against the oracle like outs[0]
                         assert sg.exchange_plan(weighted=False).kind == "group"
                     sg.exchange, sg.halo_k, sg.merge_unit = saved
+                if isinstance(layer, kd.ShardedSAGEConv) and layer.conv.aggregator == "mean":
+                    # light rows on the plain sum / mean passes (off unless KGX_HALO_LIGHT is set)
+                    os.environ["KGX_HALO_LIGHT"] = "7"
+                    try:
+                        grouped.append(layer(xl).numpy())
+                    finally:
+                        del os.environ["KGX_HALO_LIGHT"]
         q.put((rank, (outs, grouped)))
     finally:
         dist.destroy_process_group()
@@ -513,6 +520,8 @@ def test_sharded_gin_sage_layers():
     for k in range(2):
         got = np.concatenate([res2[r][1][k] for r in range(world)])
         errs.append(float((np.abs(got - refs[0].numpy()) / np.maximum(1, scales[0])).max()))
+    got = np.concatenate([res2[r][1][2] for r in range(world)])  # SAGE mean with light rows
+    errs.append(float((np.abs(got - refs[2].numpy()) / np.maximum(1, np.abs(refs[2].numpy()))).max()))
     assert max(errs) <= 1e-5, errs
 
 
