@@ -1,0 +1,63 @@
+"""Host logic of the CU-split launches (ops._fused_cu_split / ops._f256_cu_split,
+ops._split_allowed) and the ABI flag (KGX_FUSED_CU_SPLIT in include/kgx.h, the
+Python constant).  No GPU: which launches ask for the split, and the overrides."""
+
+import re
+from pathlib import Path
+
+import pytest
+
+from keras_geometric_amd import _native as nat
+from keras_geometric_amd import ops
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def test_flag_matches_header():
+    text = (ROOT / "include" / "kgx.h").read_text()
+    m = re.search(r"KGX_FUSED_CU_SPLIT\s*=\s*(\d+)", text)
+    assert m and int(m.group(1)) == nat.FUSED_CU_SPLIT == 16
+
+
+@pytest.mark.parametrize("env", [None, "0", "8"])
+def test_fused_rule_and_overrides(monkeypatch, env):
+    if env is None:
+        monkeypatch.delenv("KGX_FUSED_CU_SPLIT", raising=False)
+    else:
+        monkeypatch.setenv("KGX_FUSED_CU_SPLIT", env)
+    ns = ops._fused_cu_split(110_000_000, 8_600_000)      # the north star's schedule
+    small = ops._fused_cu_split(11_000_000, 860_000)      # C2
+    if env is None:
+        assert ns and not small
+    elif env == "0":
+        assert not ns and not small
+    else:
+        assert ns and small  # forced
+    assert not ops._fused_cu_split(110_000_000, 0)  # nothing to put on the tail CUs
+
+
+@pytest.mark.parametrize("env", [None, "0", "8"])
+def test_f256_model_and_overrides(monkeypatch, env):
+    if env is None:
+        monkeypatch.delenv("KGX_F256_CU_SPLIT", raising=False)
+    else:
+        monkeypatch.setenv("KGX_F256_CU_SPLIT", env)
+    c4 = ops._f256_cu_split(100_000_000, 7_460_000)       # C4: the tail is a quarter of the time
+    tail_heavy = ops._f256_cu_split(100_000_000, 20_000_000)
+    tiny = ops._f256_cu_split(1_000_000, 70_000)
+    if env is None:
+        assert c4 and not tail_heavy and not tiny
+    elif env == "0":
+        assert not (c4 or tail_heavy or tiny)
+    else:
+        assert c4 and tail_heavy and tiny
+
+
+def test_split_off_while_sharing(monkeypatch):
+    monkeypatch.delenv("KGX_CU_SPLIT_SHARED", raising=False)
+    assert ops._split_allowed()
+    with ops.sharing_gpu():
+        assert not ops._split_allowed()
+        monkeypatch.setenv("KGX_CU_SPLIT_SHARED", "1")
+        assert ops._split_allowed()
+    assert ops._split_allowed()
