@@ -314,7 +314,10 @@ def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, b
     n_long = n_items if n_long < 0 or n_long > n_items else n_long
     n_se, tpack, tw, n_tiny2 = _tiny_abi(items, n_items, n_long, tpack, tw if w is not None else None, n_short_end,
                                          n_tiny2)
-    if items is not None and _split_allowed() and _fused_cu_split(idx.numel(), n_items - n_long):
+    # not for the training forward's saved-aggregate launch: its tail launches also store the
+    # aggregated rows (the EXTRA instantiations), and split it measured slower (NS training step
+    # 23.1 -> 25.0 ms, profiles/r05/train/)
+    if items is not None and not save_agg and _split_allowed() and _fused_cu_split(idx.numel(), n_items - n_long):
         flags |= nat.FUSED_CU_SPLIT
         _count_cu_split()
     x2p, n_x1 = _x2_args(x, x2)
