@@ -304,7 +304,7 @@ def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, b
         partials = torch.empty((n_slots, _partial_width(x)), dtype=torch.float32, device=dev)
     flags = int(pre_gin) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0) | (nat.FUSED_RELU if relu else 0)
     if x.shape[1] == F256:
-        if tpack is not None and items is not None and _split_allowed() and \
+        if tpack is not None and items is not None and not save_agg and _split_allowed() and \
                 _f256_cu_split(idx.numel(), n_items - (n_short_end if n_short_end >= 0 else n_items)):
             flags |= nat.FUSED_CU_SPLIT
             _count_cu_split()
