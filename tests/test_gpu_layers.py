@@ -347,3 +347,42 @@ def test_hip_graph_capture_graph_warmed_by_unfused_op(dev):
         graph.replay()
         torch.cuda.synchronize()
     assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("width", [128, 256])
+def test_hip_graph_capture_cu_split(dev, monkeypatch, width):
+    """The CU-split launch (forced: KGX_FUSED_CU_SPLIT / KGX_F256_CU_SPLIT) inside a
+    HIP-graph capture: the fork onto the CU-masked streams and the join back are
+    event waits, so both streams join the capture; the replay gives the eager
+    (one-stream) bits."""
+    from keras_geometric_amd import graph as G
+
+    N, E = 30000, 300000
+    s, d = rmat_edges(43, scale_for(N), N, 0, E)
+    ei = T(np.stack([s, d]).astype(np.int32)).to(dev)
+    g = G.build_csr(ei[0].contiguous(), ei[1].contiguous(), N, N, self_loops=True, gcn_norm=True, n_features=width)
+    gen = torch.Generator(device=dev).manual_seed(3)
+    x = torch.randn(N, width, device=dev, generator=gen)
+    W = torch.randn(width, width, device=dev, generator=gen) / width ** 0.5
+    b = torch.randn(width, device=dev, generator=gen)
+    with torch.no_grad():
+        monkeypatch.setenv("KGX_FUSED_CU_SPLIT", "0")
+        monkeypatch.setenv("KGX_F256_CU_SPLIT", "0")
+        ref = kops.aggregate_transform(g, x, W, "sum", weighted=True, bias=b)
+        monkeypatch.setenv("KGX_FUSED_CU_SPLIT", "8")
+        monkeypatch.setenv("KGX_F256_CU_SPLIT", "8")
+        n0 = kops.CU_SPLIT_LAUNCHES
+        eager = kops.aggregate_transform(g, x, W, "sum", weighted=True, bias=b)
+        assert kops.CU_SPLIT_LAUNCHES > n0  # the split path ran
+        s_ = torch.cuda.Stream()
+        s_.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s_):
+            kops.aggregate_transform(g, x, W, "sum", weighted=True, bias=b)
+        torch.cuda.current_stream().wait_stream(s_)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = kops.aggregate_transform(g, x, W, "sum", weighted=True, bias=b)
+        graph.replay()
+        torch.cuda.synchronize()
+    assert torch.equal(eager, ref)
+    assert torch.equal(out, ref)
