@@ -953,6 +953,44 @@ int launch(const FusedArgs& a, hipStream_t s) {
       return KGX_OK;
     }
   }
+  if (fork == 4 && work > 0 && ((a.tpack && a.n_tiny > 0) || has_short)) {
+    // mode 4 (measurement): the main kernel first with (den - 1) / den of its
+    // resident grid (KGX_SHARE_DEN), then the short + tiny launches on the forked
+    // side stream, which fill the block slots it leaves on every CU
+    ForkJoin& fj = fork_join();
+    KGX_CHECK_HIP(hipEventRecord(fj.fork, s));
+    KGX_CHECK_HIP(hipStreamWaitEvent(fj.side, fj.fork, 0));
+    struct RecordJoin {  // every return after the fork: record the side stream's join, then wait on it
+      ForkJoin* fj;
+      hipStream_t s;
+      ~RecordJoin() {
+        if (fj) {
+          (void)hipEventRecord(fj->join, fj->side);
+          (void)hipStreamWaitEvent(s, fj->join, 0);
+        }
+      }
+    } rj{&fj, s};
+    int per_cu = 0;
+    auto k = spmm_gemm_kernel<RED, W, TWO, NARROW>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, 0) != hipSuccess || per_cu <= 0)
+      per_cu = 2;
+    const int64_t need = (work + kGroups - 1) / kGroups;
+    const int64_t cap = shared_cap(int64_t(per_cu) * cu_count());
+    hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kThreads), 0, s, a);
+    KGX_CHECK_LAUNCH();
+    if (has_short && launch_short<RED, W, TWO, NARROW>(a, fj.side) != KGX_OK) return KGX_ERR_HIP;
+    if (a.tpack && a.n_tiny > 0 && launch_tiny<RED, W, TWO, NARROW>(a, fj.side) != KGX_OK) return KGX_ERR_HIP;
+    rj.fj = nullptr;
+    KGX_CHECK_HIP(hipEventRecord(fj.join, fj.side));
+    KGX_CHECK_HIP(hipStreamWaitEvent(s, fj.join, 0));
+    if (a.items && a.n_split > 0) {
+      const int64_t blocks = (a.n_split + 7) / 8;
+      auto fk = spmm_gemm_fixup_kernel<RED, NARROW>;
+      hipLaunchKernelGGL(fk, dim3(unsigned(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s, a);
+      KGX_CHECK_LAUNCH();
+    }
+    return KGX_OK;
+  }
   const bool short_forked = fork == 2 && has_short;
   if ((a.tpack && a.n_tiny > 0 && fork >= 1 && fork <= 2) || short_forked) {
     ForkJoin& fj = fork_join();

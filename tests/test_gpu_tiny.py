@@ -124,7 +124,7 @@ def test_tiny_tail_gcn_vs_oracle(dev):
     assert np.isfinite(y.numpy()).all()
 
 
-@pytest.mark.parametrize("fork", ["1", "2", "3"])
+@pytest.mark.parametrize("fork", ["1", "2", "3", "4"])
 def test_fused_fork_bit_identical(dev, fork, monkeypatch):
     """KGX_FUSED_FORK: the tail launches on a forked side stream (1: tiny rows;
     2: short and tiny rows) beside the main kernel give the same bits as the
