@@ -860,13 +860,16 @@ __global__ __launch_bounds__(256) void spmm_gemm_fixup_kernel(FusedArgs a) {
   }
 }
 
-// KGX_FUSED_FORK (measurement A/B): 1 = the degree <= 2 tail's tiny-row
-// launches run on a forked side stream beside the main and short-row kernels;
-// 2 = the short-row launch goes to the side stream too (before the tiny ones);
-// 3 = the main kernel and the short + tiny launches on disjoint CU sets (24 / 8
-// of every 32 CUs, CU-masked streams, kgx_internal.h cu_split).
-// Disjoint output rows; the latency-bound tail launches fill the main kernel's
-// gathers instead of starting after it; joined before the hub fix-up.
+// The CU split (KGX_FUSED_CU_SPLIT flag, or KGX_FUSED_FORK=3 read per launch for
+// measurement): the main kernel and the short + tiny launches on disjoint CU
+// sets (24 / 8 of every 32 CUs, CU-masked streams, kgx_internal.h cu_split).
+// Disjoint output rows; the tail launches' MFMA phases overlap the main
+// kernel's gathers instead of starting after it; joined before the hub
+// fix-up.  Measured and removed (tools/experiments/round5_fork_modes.patch):
+// the tails forked onto an unmasked side stream (tiny only: NS 9.51-9.66 ms;
+// short + tiny: 8.89-8.94), and the main kernel capped to (den - 1) / den of
+// its grid with the tails in the slots left on every CU (8.82-8.86 at den 8;
+// 10.1-10.2 at den 2), against 8.63-8.67 split and 8.87-8.94 one-stream.
 inline int fused_fork_mode() {  // read per launch (tests switch it in-process)
   const char* h = getenv("KGX_FUSED_FORK");
   return h ? atoi(h) : 0;
@@ -911,12 +914,10 @@ int launch_tiny(const FusedArgs& a, hipStream_t s, int cus = 0) {
 template <int RED, bool W, bool TWO = false, bool NARROW = false>
 int launch(const FusedArgs& a, hipStream_t s) {
   const int64_t work = a.items ? a.n_long : a.n_rows;
-  JoinGuard guard;
-  ForkJoin* joined = nullptr;
   const bool has_short = a.items && a.n_long < a.n_short_end;
-  const int fork = a.cu_split ? 3 : fused_fork_mode();
-  if (fork == 3 && work > 0 && ((a.tpack && a.n_tiny > 0) || has_short)) {
-    // mode 3: the main kernel on a CU-masked stream over 24 of every 32 CUs, the
+  const bool split = a.cu_split || fused_fork_mode() == 3;
+  if (split && work > 0 && ((a.tpack && a.n_tiny > 0) || has_short)) {
+    // the main kernel on a CU-masked stream over 24 of every 32 CUs, the
     // short-row and tiny-row launches on another over the other 8 (cu_split)
     const char* e = getenv("KGX_FUSED_CU_SPLIT");  // tail CUs per 32 (default 8)
     CuSplit* cs = cu_split(e ? atoi(e) : 8);
@@ -953,61 +954,6 @@ int launch(const FusedArgs& a, hipStream_t s) {
       return KGX_OK;
     }
   }
-  if (fork == 4 && work > 0 && ((a.tpack && a.n_tiny > 0) || has_short)) {
-    // mode 4 (measurement): the main kernel first with (den - 1) / den of its
-    // resident grid (KGX_SHARE_DEN), then the short + tiny launches on the forked
-    // side stream, which fill the block slots it leaves on every CU
-    ForkJoin& fj = fork_join();
-    KGX_CHECK_HIP(hipEventRecord(fj.fork, s));
-    KGX_CHECK_HIP(hipStreamWaitEvent(fj.side, fj.fork, 0));
-    struct RecordJoin {  // every return after the fork: record the side stream's join, then wait on it
-      ForkJoin* fj;
-      hipStream_t s;
-      ~RecordJoin() {
-        if (fj) {
-          (void)hipEventRecord(fj->join, fj->side);
-          (void)hipStreamWaitEvent(s, fj->join, 0);
-        }
-      }
-    } rj{&fj, s};
-    int per_cu = 0;
-    auto k = spmm_gemm_kernel<RED, W, TWO, NARROW>;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, 0) != hipSuccess || per_cu <= 0)
-      per_cu = 2;
-    const int64_t need = (work + kGroups - 1) / kGroups;
-    const int64_t cap = shared_cap(int64_t(per_cu) * cu_count());
-    hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kThreads), 0, s, a);
-    KGX_CHECK_LAUNCH();
-    if (has_short && launch_short<RED, W, TWO, NARROW>(a, fj.side) != KGX_OK) return KGX_ERR_HIP;
-    if (a.tpack && a.n_tiny > 0 && launch_tiny<RED, W, TWO, NARROW>(a, fj.side) != KGX_OK) return KGX_ERR_HIP;
-    rj.fj = nullptr;
-    KGX_CHECK_HIP(hipEventRecord(fj.join, fj.side));
-    KGX_CHECK_HIP(hipStreamWaitEvent(s, fj.join, 0));
-    if (a.items && a.n_split > 0) {
-      const int64_t blocks = (a.n_split + 7) / 8;
-      auto fk = spmm_gemm_fixup_kernel<RED, NARROW>;
-      hipLaunchKernelGGL(fk, dim3(unsigned(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s, a);
-      KGX_CHECK_LAUNCH();
-    }
-    return KGX_OK;
-  }
-  const bool short_forked = fork == 2 && has_short;
-  if ((a.tpack && a.n_tiny > 0 && fork >= 1 && fork <= 2) || short_forked) {
-    ForkJoin& fj = fork_join();
-    if (hipEventRecord(fj.fork, s) != hipSuccess || hipStreamWaitEvent(fj.side, fj.fork, 0) != hipSuccess) {
-      set_error("kgx_spmm_gemm: stream fork failed");
-      return KGX_ERR_HIP;
-    }
-    if (short_forked && launch_short<RED, W, TWO, NARROW>(a, fj.side) != KGX_OK) return KGX_ERR_HIP;
-    if (a.tpack && a.n_tiny > 0 && launch_tiny<RED, W, TWO, NARROW>(a, fj.side) != KGX_OK) return KGX_ERR_HIP;
-    if (hipEventRecord(fj.join, fj.side) != hipSuccess) {
-      set_error("kgx_spmm_gemm: stream join failed");
-      return KGX_ERR_HIP;
-    }
-    joined = &fj;
-    guard.fj = &fj;
-    guard.s = s;
-  }
   if (work > 0) {
     static int cus = 0;
     if (cus == 0) {
@@ -1028,16 +974,8 @@ int launch(const FusedArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kThreads), 0, s, a);
     KGX_CHECK_LAUNCH();
   }
-  if (has_short && !short_forked && launch_short<RED, W, TWO, NARROW>(a, s) != KGX_OK) return KGX_ERR_HIP;
-  if (joined) {
-    guard.fj = nullptr;  // joined here, with the status checked
-    if (hipStreamWaitEvent(s, joined->join, 0) != hipSuccess) {
-      set_error("kgx_spmm_gemm: stream join failed");
-      return KGX_ERR_HIP;
-    }
-  } else if (a.tpack && a.n_tiny > 0 && launch_tiny<RED, W, TWO, NARROW>(a, s) != KGX_OK) {
-    return KGX_ERR_HIP;
-  }
+  if (has_short && launch_short<RED, W, TWO, NARROW>(a, s) != KGX_OK) return KGX_ERR_HIP;
+  if (a.tpack && a.n_tiny > 0 && launch_tiny<RED, W, TWO, NARROW>(a, s) != KGX_OK) return KGX_ERR_HIP;
   if (a.items && a.n_split > 0) {
     const int64_t blocks = (a.n_split + 7) / 8;
     auto fk = spmm_gemm_fixup_kernel<RED, NARROW>;
