@@ -12,6 +12,7 @@ torch.compile / symbolic tracing sees shapes without running the GPU.
 from __future__ import annotations
 
 import os
+import threading
 from typing import Optional
 
 import torch
@@ -171,17 +172,23 @@ def aggregate_accumulate(g: CSRGraph, table: torch.Tensor, out: torch.Tensor, *,
 
 # Launch hint (results unchanged): while set, fused launches leave 1/8 of the
 # block slots free for a concurrent collective (distributed.py's own-source pass).
-_SHARE_GPU = False
+# Per host thread: ranks driven by threads of one process (tests, rehearsals)
+# each enter and leave their own passes' contexts; a process-wide flag was left
+# set by interleaved exits.
+_SHARE = threading.local()
+
+
+def _share_gpu() -> bool:
+    return getattr(_SHARE, "on", False)
 
 
 class sharing_gpu:
     def __enter__(self):
-        global _SHARE_GPU
-        self._old, _SHARE_GPU = _SHARE_GPU, True
+        self._old = _share_gpu()
+        _SHARE.on = True
 
     def __exit__(self, *exc):
-        global _SHARE_GPU
-        _SHARE_GPU = self._old
+        _SHARE.on = self._old
 
 
 def _tiny_abi(items, n_items, n_long, tpack, tw, n_short_end, n_tiny2):
@@ -260,7 +267,7 @@ def _split_allowed() -> bool:
     """CU-split launches stay off while a launch shares the GPU with an exchange
     (sharing_gpu: the sharded layers' passes beside RCCL and the packing), unless
     KGX_CU_SPLIT_SHARED=1 (measurement)."""
-    return not _SHARE_GPU or os.environ.get("KGX_CU_SPLIT_SHARED") == "1"
+    return not _share_gpu() or os.environ.get("KGX_CU_SPLIT_SHARED") == "1"
 
 
 def _count_cu_split() -> None:
@@ -302,7 +309,7 @@ def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, b
     partials = None
     if items is not None and n_split > 0:
         partials = torch.empty((n_slots, _partial_width(x)), dtype=torch.float32, device=dev)
-    flags = int(pre_gin) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0) | (nat.FUSED_RELU if relu else 0)
+    flags = int(pre_gin) | (nat.FUSED_SHARE_GPU if _share_gpu() else 0) | (nat.FUSED_RELU if relu else 0)
     if x.shape[1] == F256:
         if tpack is not None and items is not None and not save_agg and _split_allowed() and \
                 _f256_cu_split(idx.numel(), n_items - (n_short_end if n_short_end >= 0 else n_items)):
@@ -448,7 +455,7 @@ def spmm_gemm_acc_(
                 _f256_cu_split(idx.numel(), n_items - (n_short_end if n_short_end >= 0 else n_items)):
             flags |= nat.FUSED_CU_SPLIT
         _f256_call(reduce, rowptr, rows, n_dst, items, n_items, split, n_split, idx, w, x, x2, W, bias,
-                   (nat.FUSED_ACCUMULATE if accumulate else 0) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0) | flags,
+                   (nat.FUSED_ACCUMULATE if accumulate else 0) | (nat.FUSED_SHARE_GPU if _share_gpu() else 0) | flags,
                    gin_scale, out, partials, None, dev, tpack, tw, n_short_end, n_long)
         return
     n_long = n_items if n_long < 0 or n_long > n_items else n_long
@@ -463,7 +470,7 @@ def spmm_gemm_acc_(
             reduce, nat.ptr(rowptr), nat.ptr(rows), n_dst, nat.ptr(items), n_items, n_long, n_se, nat.ptr(tpack),
             nat.ptr(tw), n_tiny2, nat.ptr(split), n_split,
             nat.ptr(idx), nat.ptr(w), nat.ptr(x), x.stride(0), x2p, n_x1, x.shape[1], nat.ptr(W), W.shape[1],
-            nat.ptr(bias), (nat.FUSED_ACCUMULATE if accumulate else 0) | (nat.FUSED_SHARE_GPU if _SHARE_GPU else 0) | flags,
+            nat.ptr(bias), (nat.FUSED_ACCUMULATE if accumulate else 0) | (nat.FUSED_SHARE_GPU if _share_gpu() else 0) | flags,
             float(gin_scale), nat.ptr(out), out.stride(0), nat.ptr(partials), None, 0, nat.stream(dev),
         ),
         "kgx_spmm_gemm",

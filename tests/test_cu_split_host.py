@@ -61,3 +61,37 @@ def test_split_off_while_sharing(monkeypatch):
         monkeypatch.setenv("KGX_CU_SPLIT_SHARED", "1")
         assert ops._split_allowed()
     assert ops._split_allowed()
+
+
+def test_sharing_flag_is_per_thread():
+    """Threaded ranks (one process) enter and leave their passes' sharing_gpu
+    contexts in any interleaving: the flag is per host thread, so no thread's
+    exit leaves another's (or the next caller's) launches flagged."""
+    import threading
+
+    a_in, b_in, a_out = threading.Event(), threading.Event(), threading.Event()
+    seen = {}
+
+    def rank_a():
+        with ops.sharing_gpu():
+            a_in.set()
+            b_in.wait(5)
+            seen["a_inside"] = ops._share_gpu()
+        a_out.set()
+        seen["a_after"] = ops._share_gpu()
+
+    def rank_b():
+        a_in.wait(5)
+        with ops.sharing_gpu():
+            b_in.set()
+            a_out.wait(5)  # A leaves while B is still inside
+            seen["b_inside"] = ops._share_gpu()
+        seen["b_after"] = ops._share_gpu()
+
+    ts = [threading.Thread(target=rank_a), threading.Thread(target=rank_b)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(10)
+    assert seen == {"a_inside": True, "a_after": False, "b_inside": True, "b_after": False}
+    assert not ops._share_gpu()
