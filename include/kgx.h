@@ -224,7 +224,8 @@ int kgx_dropout_mask(uint64_t seed, float p, const int32_t* keys, int64_t n, int
  * agg_out (optional, [n, ld_agg >= F_in]): also store PRE(REDUCE(...)), the
  * rows before the transform — what the backward's dW = agg^T dOut needs.
  * ------------------------------------------------------------------------- */
-/* KGX_FUSED_SHARE_GPU: launch 7/8 of the resident grid, leaving block slots
+/* KGX_FUSED_SHARE_GPU: launch (den - 1) / den of the resident grid (den =
+ * KGX_SHARE_DEN, default 16; the 256-wide kernels take the flag and ignore it), leaving block slots
  * for kernels of a concurrent stream (the sharded layer's RCCL exchange).
  * KGX_FUSED_RELU: out = max(bias + ..., 0), the activation of a GIN MLP's
  * first Dense (gin_conv.py:129-162) or SAGEConv's activation; with ACCUMULATE

@@ -80,11 +80,13 @@ unsigned resident_grid(Kern kernel, int64_t groups_needed, int G) {
 }
 
 // A launch that shares the GPU with a concurrent stream (KGX_FUSED_SHARE_GPU)
-// takes (den - 1) / den of its resident grid: den = KGX_SHARE_DEN (default 8).
+// takes (den - 1) / den of its resident grid: den = KGX_SHARE_DEN (default 16:
+// the sharded GCN step with light rows, simulated at 400 GB/s, measured 12.31-
+// 12.36 ms at 8, 12.16-12.18 at 16, 12.12-12.17 at 32, 13.07-13.13 at 64).
 inline int64_t shared_cap(int64_t full) {
   const char* h = getenv("KGX_SHARE_DEN");  // read per launch: measurement sweeps change it in-process
-  const int v = h ? atoi(h) : 8;
-  const int den = v >= 2 ? v : 8;
+  const int v = h ? atoi(h) : 16;
+  const int den = v >= 2 ? v : 16;
   const int64_t c = full * (den - 1) / den;
   return c > 0 ? c : 1;
 }

@@ -74,7 +74,7 @@ struct FusedArgs {
   int64_t ld_agg;
   int pre_gin;      // apply gin_scale * x[row] + aggr before the transform
   int accumulate;   // out += result
-  int share_gpu;    // launch 7/8 of the resident grid
+  int share_gpu;    // launch (den - 1) / den of the resident grid (shared_cap)
   int relu;         // out = max(result, 0), after the accumulate
   float gin_scale;
   int64_t n_short_end;  // items [n_long, n_short_end): spmm_gemm_short_kernel
@@ -968,7 +968,7 @@ int launch(const FusedArgs& a, hipStream_t s) {
       per_cu = 2;
     const int64_t need = (work + kGroups - 1) / kGroups;
     // KGX_FUSED_SHARE_GPU: leave 1/den of the block slots free (share_den(),
-    // default an eighth) so a concurrent collective's kernels (RCCL halo
+    // default a sixteenth) so a concurrent collective's kernels (RCCL halo
     // all-to-all) and the side stream's packing are not starved
     const int64_t cap = a.share_gpu ? shared_cap(int64_t(per_cu) * cus) : int64_t(per_cu) * cus;
     hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kThreads), 0, s, a);
