@@ -925,55 +925,6 @@ int launch_main(const SpmmArgs& a_in, hipStream_t s) {
     }
     return KGX_OK;
   };
-  // KGX_EXACT_CU_SPLIT = t (measurement, default 0): beside the forked hub kernel,
-  // spmm_kernel on a CU-masked stream over 32 - t of every 32 CUs and the
-  // short-row kernel at once on another over the other t (kgx_internal.h
-  // cu_split); every row is still reduced by one lane group in CSR order
-  if constexpr (NT == 1) {
-    static const int exact_split = [] {
-      const char* h = getenv("KGX_EXACT_CU_SPLIT");
-      return h ? atoi(h) : 0;
-    }();
-    const int64_t work_l = a.items ? a.n_long : a.n_rows_long;
-    CuSplit* cs = (exact_split > 0 && a.dyn_rows == 2 && joined && short_on && work_l > 0) ? cu_split(exact_split)
-                                                                                            : nullptr;
-    if (cs) {
-      SplitJoin sj;
-      KGX_CHECK_HIP(hipEventRecord(cs->fork, s));
-      KGX_CHECK_HIP(hipStreamWaitEvent(cs->head, cs->fork, 0));
-      KGX_CHECK_HIP(hipStreamWaitEvent(cs->tail, cs->fork, 0));
-      sj.cs = cs;
-      sj.s = s;
-      auto k = spmm_kernel<VEC, NT, RED, W, false, TWO>;
-      int per_cu = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kBlock, 0) != hipSuccess || per_cu <= 0) per_cu = 4;
-      unsigned grid = resident_grid(k, work_l, a.G);
-      if (int64_t(grid) > int64_t(per_cu) * cs->n_head) grid = unsigned(int64_t(per_cu) * cs->n_head);
-      hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, cs->head, a);
-      KGX_CHECK_LAUNCH();
-      auto ks = spmm_short_kernel<VEC, RED, W, TWO>;
-      int per_cu_s = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_s, ks, kBlock, 0) != hipSuccess || per_cu_s <= 0)
-        per_cu_s = 4;
-      unsigned gs = resident_grid(ks, (n_short + kSR - 1) / kSR, a.G);
-      if (int64_t(gs) > int64_t(per_cu_s) * cs->n_tail) gs = unsigned(int64_t(per_cu_s) * cs->n_tail);
-      hipLaunchKernelGGL(ks, dim3(gs), dim3(kBlock), 0, cs->tail, a);
-      KGX_CHECK_LAUNCH();
-      sj.cs = nullptr;
-      KGX_CHECK_HIP(hipEventRecord(cs->jh, cs->head));
-      KGX_CHECK_HIP(hipEventRecord(cs->jt, cs->tail));
-      KGX_CHECK_HIP(hipStreamWaitEvent(s, cs->jh, 0));
-      KGX_CHECK_HIP(hipStreamWaitEvent(s, cs->jt, 0));
-      guard.fj = nullptr;
-      KGX_CHECK_HIP(hipStreamWaitEvent(s, joined->join, 0));
-      if (a.items && a.n_split > 0) {
-        auto kf = spmm_fixup_kernel<VEC, NT, RED>;
-        hipLaunchKernelGGL(kf, dim3(resident_grid(kf, a.n_split, a.G)), dim3(kBlock), 0, s, a);
-        KGX_CHECK_LAUNCH();
-      }
-      return KGX_OK;
-    }
-  }
   // the short-row kernel first, except beside a forked hub kernel whose rows
   // spmm_kernel's dynamic batches work around (KGX_EXACT_FORK=3)
   const bool short_last = a.dyn_rows == 2 && joined;

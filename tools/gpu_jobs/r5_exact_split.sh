@@ -1,4 +1,4 @@
-# Round 5: EXACT aggregation with the short-row kernel on 8 of every 32 CUs beside spmm_kernel
+# Round 5 (measured, not kept: tools/experiments/round5_exact_cu_split.patch): EXACT aggregation
 # (KGX_EXACT_CU_SPLIT=8, read once per process): the EXACT / bit-identity GPU tests under it, then
 # NS --exact bench lines with and without, interleaved -> gpurun_out/exs
 set -o pipefail
