@@ -163,12 +163,8 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
     // K 256, 8 x 16 KB at K 128; half with two operands, whose sets take
     // twice the registers).  The loads are latency-bound, not bandwidth-bound,
     // below that: 64 KB per CU measured 3 TB/s.
-#ifdef KGX_DENSE_NSETS  // experiment knob
-    constexpr int NSETS_ = KS == 8 ? KGX_DENSE_NSETS : (32 / KS < 2 ? 2 : (32 / KS > 8 ? 8 : 32 / KS));
-#else
     // K 256: three sets (four spilled address registers once the split took fewer VALU but more live values)
     constexpr int NSETS_ = KS == 8 ? 3 : (32 / KS < 2 ? 2 : (32 / KS > 8 ? 8 : 32 / KS));
-#endif
     constexpr int NSETS = TWO ? (NSETS_ / 2 < 2 ? 2 : NSETS_ / 2) : NSETS_;
     const int ptid = tid - 64 * WAVES;
     const int kk = 4 * (ptid % G::F4_PER_ROW);
@@ -218,7 +214,6 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
       }
     };
     auto stage = [&](const f32x4(&p)[NL], const f32x4(&q)[NL], int buf) {
-#ifndef KGX_DENSE_OLD_SPLIT
       // fast path: paired conversions (split3_pair_rn, ~4.5 VALU per element:
       // the producer's split must fit in the issue slots the consumers' MFMAs
       // leave free on its SIMD).  chk = sum of 2|x| over the thread's slots
@@ -244,11 +239,7 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
         *reinterpret_cast<uint2*>(&As[buf][1][row][kk]) = make_uint2(m0, m1);
         *reinterpret_cast<uint2*>(&As[buf][2][row][kk]) = make_uint2(l0, l1);
       }
-#ifdef KGX_DENSE_NO_SLOW  // experiment only: no inf/NaN path (wrong for non-finite inputs)
-      return;
-#endif
       if (__builtin_expect(__builtin_isfinite(chk0 + chk1), 1)) return;
-#endif
 #pragma unroll
       for (int j = 0; j < NL; ++j) {
         const int row = srow0 + j * RSTEP;
@@ -394,18 +385,10 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
       wm[s][j] = m;
       wl[s][j] = lo;
     }
-#ifndef KGX_DENSE_TRANSPOSED
   const float bcol = (a.bias && n_col < a.N) ? a.bias[n_col] : 0.0f;
   // byte offset of this lane's first output element within a tile (row 4 lq, column n_col);
   // out-of-range for columns past N, so their stores are dropped
   const uint32_t out_lane = n_col < a.N ? uint32_t((4 * lq * a.ld_out + n_col) * 4) : 0x80000000u;
-#else
-  // output-transposed form: lane holds row lr, columns col4 .. col4 + 3
-  const int col4 = cg * 16 * WAVES + wave * 16 + 4 * lq;
-  // byte offset of (row lr, column col4) within a tile; a whole 4-column group past N
-  // is out of range (vec_out: N % 4 == 0, so no group straddles N)
-  const uint32_t out_row = col4 < a.N ? uint32_t((lr * a.ld_out + col4) * 4) : 0x80000000u;
-#endif
   if constexpr (LS) {
     if (wave == 0)
       for (int c = l; c < OCOLS; c += 64) Ob[c] = (a.bias && cg * OCOLS + c < a.N) ? a.bias[cg * OCOLS + c] : 0.0f;
@@ -502,18 +485,10 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
         }
         if constexpr (LS && s == KS - 1) asm volatile("" : "+v"(lov[0]), "+v"(lov[1]), "+v"(lb4));
         // small terms first; two independent accumulator chains (row tiles).
-        // Experiment KGX_DENSE_TRANSPOSED: D = W^T x^T, so a lane ends with 4
-        // consecutive output columns of one row (one dwordx4 store per block)
-        // instead of one column of 4 rows (four dword stores); the A and B
-        // fragment layouts of 16x16x32 are mirror images, so the same register /
-        // LDS fragments serve with the operands swapped.  Measured 1-6 % slower
-        // (C4 7.12 vs 7.02 ms, NS 2.24 vs 2.12): the stores' bytes, not their
-        // instruction count, are what the consumers pay for.
-#ifndef KGX_DENSE_TRANSPOSED
+        // (Measured and not kept: D = W^T x^T, a lane holding 4 consecutive
+        // columns of one row for one dwordx4 store per block, 1-6 % slower:
+        // C4 7.12 vs 7.02 ms, NS 2.24 vs 2.12.)
 #define KGX_MF(X, W, ACC_) __builtin_amdgcn_mfma_f32_16x16x32_bf16(X, W, ACC_, 0, 0, 0)
-#else
-#define KGX_MF(X, W, ACC_) __builtin_amdgcn_mfma_f32_16x16x32_bf16(W, X, ACC_, 0, 0, 0)
-#endif
 #pragma unroll
         for (int r = 0; r < 2; ++r) acc[r] = KGX_MF(cur.l[r], wh[s], acc[r]);
 #pragma unroll
@@ -560,7 +535,6 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
       const int bytes = __builtin_amdgcn_readfirstlane(int(rows * a.ld_out * 4));
       const auto rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((uint64_t(hi) << 32) | lo), 0,
                                                         bytes, 0x00020000);
-#ifndef KGX_DENSE_TRANSPOSED
       // lane holds rows 4 lq + j of column lr of each 16x16 block (soffset = the row)
 #pragma unroll
       for (int r = 0; r < 2; ++r)
@@ -573,42 +547,6 @@ __global__ __launch_bounds__(64 * (WAVES + kProducerWaves)) void dense_kernel(De
           if (a.relu) v = fmaxf(v, 0.0f);
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), rs, out_lane, soff, 0);
         }
-#else
-      // lane holds columns col4 + j (j < 4) of row lr of each 16x16 block (soffset = 16 r rows);
-      // the bias is re-read per tile (an L1 hit) rather than held in 4 more registers
-      float b4[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b4[j] = (a.bias && col4 + j < a.N) ? a.bias[col4 + j] : 0.0f;
-#pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        const int soff = int(16 * r * a.ld_out * 4);
-        f32x4 v;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = acc[r][j] + b4[j];
-        if (a.vec_out) {
-          if constexpr (ACC) {
-            const f32x4 o = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, out_row, soff, 0));
-#pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = __fadd_rn(o[j], v[j]);
-          }
-          if (a.relu) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.0f);
-          }
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, out_row, soff, 0);
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const uint32_t off = col4 + j < a.N ? out_row + 4u * j : 0x80000000u;
-            float e = v[j];
-            if constexpr (ACC)
-              e = __fadd_rn(__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, soff, 0)), e);
-            if (a.relu) e = fmaxf(e, 0.0f);
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, e), rs, off, soff, 0);
-          }
-        }
-      }
-#endif
     }
     lds_barrier();  // buffer `buf` free for the producers; the stores stay in flight
   }
@@ -625,14 +563,12 @@ template <int KS, int WAVES>
 int launch(const DenseArgs& a, hipStream_t s) {
   auto k = a.accumulate ? (a.K1 > 0 ? dense_kernel<KS, WAVES, true, true> : dense_kernel<KS, WAVES, true, false>)
                         : (a.K1 > 0 ? dense_kernel<KS, WAVES, false, true> : dense_kernel<KS, WAVES, false, false>);
-#ifndef KGX_DENSE_NO_LS
   // K > 128 only: measured C4 (K 256) 6.91 -> 6.66 ms, C5 (K 200) 0.90 -> 0.86 ms, but the
   // 10M x 128 -> 128 shape 2.13 -> 2.18 ms (half the MFMA time per tile to hide the extra LDS traffic)
   if constexpr (KS == 8) {
     if (!a.accumulate && a.vec_out && !a.pstore && a.debug == 0)
       k = a.K1 > 0 ? dense_kernel<KS, WAVES, false, true, true> : dense_kernel<KS, WAVES, false, false, true>;
   }
-#endif
   static int cus = 0;
   if (cus == 0) {
     int dev = 0;

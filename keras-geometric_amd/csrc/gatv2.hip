@@ -74,12 +74,8 @@ __device__ __forceinline__ float head_reduce(float p, int LH) {
 
 template <int K>
 __global__ __launch_bounds__(kBlock) void gatv2_kernel(GatArgs a) {
-#ifdef KGX_GAT_U
-  constexpr int U = KGX_GAT_U;
-#else
   // edges per online-softmax block: 3 measured best at C3 (K = 4): 1.27 ms vs 1.41 at 8, 1.30 at 4
   constexpr int U = K <= 4 ? 3 : (K == 8 ? 3 : 2);
-#endif
   const int G = a.G;
   const int lane = threadIdx.x & (G - 1);
   const int head = lane >> a.lgLH;
@@ -162,25 +158,6 @@ __global__ __launch_bounds__(kBlock) void gatv2_kernel(GatArgs a) {
       l *= scale;
 #pragma unroll
       for (int k = 0; k < K; ++k) acc[k] *= scale;
-#ifdef KGX_GAT_F32BLOCK
-      // experiment: the U-edge block summed in fp32 (<= U terms), added to the fp64 running sums once
-      float bl = 0.0f, bacc[K];
-#pragma unroll
-      for (int k = 0; k < K; ++k) bacc[k] = 0.0f;
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (u < n) {
-          const float pu = expf(s[u] - m_new);
-          bl += pu;
-          const float pd = pu * dm[u];
-#pragma unroll
-          for (int k = 0; k < K; ++k) bacc[k] = fmaf(pd, hs[u][k], bacc[k]);
-        }
-      }
-      l += double(bl);
-#pragma unroll
-      for (int k = 0; k < K; ++k) acc[k] += double(bacc[k]);
-#else
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (u < n) {
@@ -191,7 +168,6 @@ __global__ __launch_bounds__(kBlock) void gatv2_kernel(GatArgs a) {
           for (int k = 0; k < K; ++k) acc[k] = fma(pd, double(hs[u][k]), acc[k]);
         }
       }
-#endif
       m = m_new;
     }
 

@@ -65,12 +65,8 @@ __device__ __forceinline__ void split3_a_lo(float x, short& hi, short& mid, shor
 // (RNE to bf16 then stays finite: no cancellation in the sum can hide a huge
 // pair).  Otherwise the caller takes split3_a_lo.
 __device__ __forceinline__ bool split_fast_ok(float a, float b, float c, float d) {
-#ifdef KGX_OLD_FAST_CHECK  // measurement A/B only: the round-2 check (misses a huge cancelling pair)
-  return __builtin_isfinite(__fadd_rn(__fadd_rn(a, b), __fadd_rn(c, d)));
-#else
   const float m = fmaxf(fmaxf(fabsf(a), fabsf(b)), fmaxf(fabsf(c), fabsf(d)));
   return __builtin_isfinite(__fadd_rn(__fadd_rn(a, b), __fadd_rn(c, d))) && m < 0x1.ffp127f;
-#endif
 }
 
 // split3_a of a pair, packed (element 0 in the low half): fragments assembled

@@ -197,11 +197,7 @@ template <int VEC, int NT, int RED, bool WEIGHTED, bool DROP = false, bool TWO =
 __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
   using R = Reducer<RED>;
   // gathers in flight per group (NT = 1: 6 measured best at NS, 9.2-9.4 ms vs 9.5 at 8, 9.9 at 12)
-#ifdef KGX_SPMM_U
-  constexpr int U = NT >= 4 ? 2 : (NT == 2 ? 4 : KGX_SPMM_U);
-#else
   constexpr int U = NT >= 4 ? 2 : (NT == 2 ? 4 : 6);
-#endif
   const int G = a.G;
   const int lane = threadIdx.x & (G - 1);
   const int64_t ngroups = (int64_t(gridDim.x) * kBlock) >> a.lgG;
@@ -226,10 +222,7 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
   // take less, and the launch ends together.  Otherwise: static grid-stride.
   const bool dyn = a.dyn != nullptr && a.dyn_rows && !a.items;
   // rows per grab (the KGX_EXACT_FORK experiment, see launch_main)
-#ifndef KGX_DYN_ROWS
-#define KGX_DYN_ROWS 8
-#endif
-  constexpr int kDynRows = KGX_DYN_ROWS;
+  constexpr int kDynRows = 8;
   const int64_t gid = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> a.lgG;
   // dyn_rows == 2 (KGX_EXACT_FORK=3): batch b, one atomic, is rows b, b + NB,
   // b + 2 NB, ... -- one row from each kDynRows-th of the degree-descending
@@ -360,26 +353,11 @@ __global__ __launch_bounds__(kBlock) void spmm_long_kernel(SpmmArgs a) {
 // The gathers and their index / weight loads are inline-asm loads with
 // counted vmcnt waits: the compiler's accounting would wait for the whole
 // queue whenever an index it loaded is used.
-#ifndef KGX_HUB_D
-#define KGX_HUB_D 8
-#endif
-#ifndef KGX_HUB_PRIO
-#define KGX_HUB_PRIO 0
-#endif
-#ifndef KGX_HUB_READER_WAIT
-#define KGX_HUB_READER_WAIT 0
-#endif
-#ifndef KGX_HUB_RPL
-#define KGX_HUB_RPL 2
-#endif
 constexpr int kHubThreads = 1024;
-constexpr int kHubD = KGX_HUB_D;      // rows in flight per producer lane
-constexpr int kHubRPL = KGX_HUB_RPL;  // rows per producer lane per stage
+constexpr int kHubD = 8;      // rows in flight per producer lane
+constexpr int kHubRPL = 2;  // rows per producer lane per stage
 constexpr int kHubSMax = 56;
-#ifndef KGX_HUB_G
-#define KGX_HUB_G 16
-#endif
-constexpr int kHubG = KGX_HUB_G;  // hub column group: 4 x kHubG features
+constexpr int kHubG = 16;  // hub column group: 4 x kHubG features
 
 __device__ __forceinline__ void hub_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -390,9 +368,6 @@ __device__ __forceinline__ void hub_barrier() {
 // barrier (producers overwrite that buffer two barriers later, and the reads
 // are waited for by the fold one iteration later), so no lgkmcnt(0) here.
 __device__ __forceinline__ void hub_barrier_reader() {
-#if KGX_HUB_READER_WAIT
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#endif
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }
@@ -457,9 +432,6 @@ __global__ __launch_bounds__(kHubThreads, 1) void spmm_hub_kernel(SpmmArgs a) {
   const int32_t n_iter = (n_st + 2 + 2 * D - 1) / (2 * D) * (2 * D);
 
   if (wave < CW) {  // ---- consumers
-#if KGX_HUB_PRIO
-    __builtin_amdgcn_s_setprio(3);  // the fold chain is the row's critical path
-#endif
     for (int64_t p = blockIdx.x; p < n_hub_items; p = next_item(p)) {
       KGX_HUB_ROW(p)
       claim_next();
@@ -624,14 +596,8 @@ __global__ __launch_bounds__(kHubThreads, 1) void spmm_hub_kernel(SpmmArgs a) {
 // gathers the first kSPF edges of all of them together (never exec-masked:
 // absent edges read kgx_zero_row and are masked at the fold), the rest in
 // pairs, each row still reduced in its CSR order.
-#ifndef KGX_SPMM_SHORT_R
-#define KGX_SPMM_SHORT_R 4
-#endif
-#ifndef KGX_SPMM_SHORT_PF
-#define KGX_SPMM_SHORT_PF 2
-#endif
-constexpr int kSR = KGX_SPMM_SHORT_R;
-constexpr int kSPF = KGX_SPMM_SHORT_PF;
+constexpr int kSR = 4;
+constexpr int kSPF = 2;
 
 template <int VEC, int RED, bool WEIGHTED, bool TWO = false>
 __global__ __launch_bounds__(kBlock) void spmm_short_kernel(SpmmArgs a) {

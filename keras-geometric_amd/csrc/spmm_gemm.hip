@@ -231,21 +231,13 @@ struct Red {
 template <int RED, bool WEIGHTED, bool TWO, bool NARROW>
 __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedArgs a) {  // TWO: hold 4 waves per SIMD
   using R = Red<RED>;
-#ifdef KGX_FUSED_U
-  constexpr int U = KGX_FUSED_U;
-#else
   // gathers in flight per group: at F_in 128 (GCN, NS) 4 beat 6 and 8 with PF = U
   // (each cost occupancy) and U = 8 with PF = 2 (NS 8.90 -> 9.05-9.15 ms); the
   // narrow unweighted form (SAGE at C5: 50 edges per row on average) takes 6 in
   // 124 VGPRs, occupancy kept (C5 main kernel 7.70 ms at U = 4, 7.37-7.48 at
   // U = 6, 7.77 at U = 8 with PF = 2)
   constexpr int U = (NARROW && !WEIGHTED) ? 6 : 4;
-#endif
-#ifdef KGX_FUSED_PF
-  constexpr int PF = KGX_FUSED_PF;
-#else
   constexpr int PF = 4;  // rows prefetched per group for the next tile (live across the MFMA phase)
-#endif
   __shared__ __attribute__((aligned(16))) short tile3[kFPlanes][kGroups][kFin + 8];  // split planes of the aggregated rows
   __shared__ __attribute__((aligned(16))) float sbias[kFin];  // read at the stores (4 VGPRs fewer than a register copy)
   __shared__ int32_t tile_row[kGroups];
@@ -425,14 +417,8 @@ __global__ __launch_bounds__(kThreads, TWO ? 4 : 1) void spmm_gemm_kernel(FusedA
 // are stored as whole rows (measured 0.98 against 0.99 ms for stores straight
 // from the accumulators).
 static_assert(KGX_SHORT_ROW_MAX == 7, "the short kernel gathers three edges per row up front, then pairs");
-#ifndef KGX_SHORT_RPG
-#define KGX_SHORT_RPG 2
-#endif
-#ifndef KGX_SHORT_PF
-#define KGX_SHORT_PF 3
-#endif
-constexpr int kRPG = KGX_SHORT_RPG;        // rows per group per tile
-constexpr int kSPF = KGX_SHORT_PF;         // edges per row gathered up front (all rows together)
+constexpr int kRPG = 2;        // rows per group per tile
+constexpr int kSPF = 3;         // edges per row gathered up front (all rows together)
 constexpr int kShortRows = kGroups * kRPG;
 
 template <int RED, bool WEIGHTED, bool TWO, bool NARROW>
@@ -627,21 +613,17 @@ __global__ __launch_bounds__(kThreads, 4) void spmm_gemm_short_kernel(FusedArgs 
 constexpr int kTinyThreads = 1024;
 constexpr int kTinyGroups = 16;  // producer row groups
 // rows per group per tile (= 16-row MFMA blocks per tile): two-edge rows / one-edge rows
-#ifndef KGX_TINY_RPG
-#define KGX_TINY_RPG 2
-#endif
-#ifndef KGX_TINY_RPG1
-#define KGX_TINY_RPG1 4
-#endif
+constexpr int kTinyRPG2 = 2;  // two-edge rows
+constexpr int kTinyRPG1 = 4;  // one-edge rows
 template <int NG>
-constexpr int tiny_rows() { return kTinyGroups * (NG == 1 ? KGX_TINY_RPG1 : KGX_TINY_RPG); }
+constexpr int tiny_rows() { return kTinyGroups * (NG == 1 ? kTinyRPG1 : kTinyRPG2); }
 
 // NG: edges gathered per row (2 for the degree-2 head of the tail, 1 for the
 // degree <= 1 rest: the schedule is degree-descending, so each is a range).
 template <int RED, bool WEIGHTED, bool EXTRA, int NG, bool TWO, bool NARROW>  // EXTRA: pre_gin or agg_out (loads / stores under a row mask)
 __global__ __launch_bounds__(kTinyThreads, 1) void spmm_gemm_tiny_kernel(FusedArgs a) {
   using R = Red<RED>;
-  constexpr int kTinyRPG = NG == 1 ? KGX_TINY_RPG1 : KGX_TINY_RPG;  // rows per group per tile
+  constexpr int kTinyRPG = NG == 1 ? kTinyRPG1 : kTinyRPG2;  // rows per group per tile
   constexpr int kTinyRows = kTinyGroups * kTinyRPG;
   __shared__ __attribute__((aligned(16))) short planes[2][kFPlanes][kTinyRows][kFin + 8];
   __shared__ int32_t trow[2][kTinyRows];

@@ -208,12 +208,10 @@ __device__ __forceinline__ void transform_tile(const F256Args& a, const short (*
 // Items [0, n_work): hub-row chunks, long rows and rows of degree 3..7 (the
 // degree <= 2 tail goes to spmm_gemm256_tiny2_kernel when its records exist).
 // PF = edges per row gathered ahead, during the previous tile's MFMAs: 4 for the
-// long rows; KGX_F256_MID_PF for the schedule's rows of degree 3..7 (a second
+// long rows; kMidPF = 6 for the schedule's rows of degree 3..7 (a second
 // launch over items [n_long, n_work)), most of which are then gathered whole a
 // tile ahead.
-#ifndef KGX_F256_MID_PF
-#define KGX_F256_MID_PF 6
-#endif
+constexpr int kMidPF = 6;
 // pre_gin: the rows' own x rows are loaded with the next tile's prefetch
 // instead of after the fold, where their latency was exposed once per tile
 // (C4 layer 21.51-21.53 -> 21.20-21.21 ms interleaved; 8 more VGPRs spilled
@@ -221,11 +219,7 @@ __device__ __forceinline__ void transform_tile(const F256Args& a, const short (*
 template <int RED, bool WEIGHTED, int PF, bool TWO>
 __global__ __launch_bounds__(kThreads, 1) void spmm_gemm256_kernel(F256Args a) {
   using R = RowRed<RED>;
-#ifdef KGX_F256_U
-  constexpr int U = KGX_F256_U;
-#else
   constexpr int U = 4;  // gathers in flight per row in the two-row loop (8 per wave)
-#endif
   __shared__ u32x4_t wlo[kColBlocks * kSteps * 64];  // W lo-plane B-fragments, 128 KB
   __shared__ __attribute__((aligned(16))) short tile3[kPlanes][kRows][kLd];  // the split planes of the tile's rows
   __shared__ __attribute__((aligned(16))) float sbias[kF];
@@ -707,7 +701,7 @@ int launch256(const F256Args& a, hipStream_t s) {
     F256Args b = a;
     b.items = a.items + n_long;
     b.n_work = work - n_long;
-    auto k = spmm_gemm256_kernel<RED, WT, KGX_F256_MID_PF, TWO>;
+    auto k = spmm_gemm256_kernel<RED, WT, kMidPF, TWO>;
     hipLaunchKernelGGL(k, dim3(grid256(k, (b.n_work + kRows - 1) / kRows, cus_h)), dim3(kThreads), 0, sh, b);
     KGX_CHECK_LAUNCH();
   }
