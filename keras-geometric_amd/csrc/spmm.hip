@@ -69,8 +69,8 @@ struct SpmmArgs {
   const float* t2b;
   int32_t n_t1;
   // EXACT mode, dynamic pickup (kgx_spmm_ex2 counters): dyn[0] hands out the hub
-  // kernel's (row, column group) items; with dyn_rows, dyn[1] hands out
-  // spmm_kernel's row batches.  NULL: the static grid-stride schedule.
+  // kernel's (row, column group) items; with dyn_rows = 1, dyn[1] hands out
+  // spmm_kernel's interleaved row batches.  NULL: the static grid-stride schedule.
   int32_t* dyn;
   int dyn_rows;
 };
@@ -216,25 +216,22 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
     fl[t] = fv[t] ? fo[t] : a.F - VEC;  // load offset, always in range
   }
 
-  // EXACT mode with a.dyn: each group takes batches of kDynRows consecutive rows
-  // from a counter (lane 0's atomic, broadcast to the group), so groups whose
-  // blocks started late -- behind the hub kernel running beside this one --
-  // take less, and the launch ends together.  Otherwise: static grid-stride.
+  // EXACT mode beside the forked hub kernel (a.dyn, dyn_rows = 1): each group
+  // takes batches of kDynRows rows from a counter (lane 0's atomic, broadcast to
+  // the group), so groups whose blocks started late -- behind the hub kernel --
+  // take less, and the launch ends together.  Batch b is rows b, b + NB,
+  // b + 2 NB, ... -- one row from each kDynRows-th of the degree-descending
+  // list, so every batch carries about the same work, heaviest batches first.
+  // Otherwise: static grid-stride.
   const bool dyn = a.dyn != nullptr && a.dyn_rows && !a.items;
-  // rows per grab (the KGX_EXACT_FORK experiment, see launch_main)
   constexpr int kDynRows = 8;
   const int64_t gid = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> a.lgG;
-  // dyn_rows == 2 (KGX_EXACT_FORK=3): batch b, one atomic, is rows b, b + NB,
-  // b + 2 NB, ... -- one row from each kDynRows-th of the degree-descending
-  // list, so every batch carries about the same work, heaviest batches first
-  const bool dyn_il = dyn && a.dyn_rows == 2;
   const int64_t NB = (n_work + kDynRows - 1) / kDynRows;
-  int64_t it = gid, batch_end = 0;
+  int64_t it = gid;
   int jj = kDynRows;
-  if (dyn) it = batch_end = 0;
   for (;;) {
     int64_t cur;
-    if (dyn_il) {
+    if (dyn) {
       if (jj >= kDynRows) {
         int64_t b = 0;
         if (lane == 0) b = int64_t(atomicAdd(a.dyn + 1, 1));
@@ -249,20 +246,9 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
         continue;
       }
     } else {
-      if (dyn) {
-        if (it >= batch_end) {
-          int64_t b = 0;
-          if (lane == 0) b = int64_t(atomicAdd(a.dyn + 1, kDynRows));
-          b = __shfl(b, 0, G);  // the group's lane 0 (groups are aligned G-lane slices of the wave)
-          it = b;
-          batch_end = b + kDynRows < n_work ? b + kDynRows : n_work;
-        }
-        if (it >= n_work) break;
-      } else if (it >= n_work) {
-        break;
-      }
+      if (it >= n_work) break;
       cur = it;
-      it = dyn ? it + 1 : it + ngroups;
+      it += ngroups;
     }
     int32_t row, beg, end, slot;
     if (a.items) {
@@ -795,7 +781,6 @@ int launch_main(const SpmmArgs& a_in, hipStream_t s) {
   SpmmArgs a = a_in;
   ForkJoin* joined = nullptr;
   JoinGuard guard;
-  int64_t a_hub_slots = 0;  // KGX_EXACT_FORK=2: spmm_kernel's grid leaves these block slots to the hub kernel
   if constexpr (NT == 1) {
     static const bool hub_off = [] {
       const char* h = getenv("KGX_HUB");
@@ -810,32 +795,22 @@ int launch_main(const SpmmArgs& a_in, hipStream_t s) {
       else if (gh == 8) kh = spmm_hub_kernel<8, RED, W>;
       const int64_t work = a.n_rows * ((a.F + 4 * gh - 1) / (4 * gh));
       const int64_t nb = work < cu_count() ? work : cu_count();  // one resident block per CU
-      // Experiments: KGX_EXACT_FORK=1, the hub kernel forked beside spmm_kernel,
-      // whose rows are then handed out dynamically in contiguous batches of the
-      // degree-descending list -- which concentrate the heaviest rows on single
-      // groups (8 / 32 / 256-row batches: 12.7 / 15.0 / 65 ms against 10.9
-      // static); KGX_EXACT_FORK=2, forked, spmm_kernel keeping its static
-      // grid-stride rows with its grid cut to the block slots the hub blocks
-      // leave (10.29-10.32 against 9.92-10.01 ms: the cut grid runs short of
-      // gathers in flight for the whole launch).
+      // KGX_EXACT_FORK=3 (default): the hub kernel forked beside spmm_kernel,
+      // which runs on its full grid taking interleaved row batches from a
+      // counter (one atomic per kDynRows rows), and the short-row kernel after
+      // it, once the hub kernel's tail is over.  The hub kernel's mass of rows
+      // ends in ~0.3 ms; its largest row then holds two CUs for ~1 ms, which
+      // spmm_kernel's batches fill: NS EXACT aggregation 9.69-9.73 -> 8.96-8.98
+      // ms (profiles/r04/exact_fork3_ab.jsonl).  0: sequential.  Measured and
+      // removed (tools/experiments/round5_exact_fork_modes.patch): contiguous
+      // row batches (12.7-65 ms against 10.9 static) and a grid cut to the
+      // block slots the hub blocks leave (10.29-10.32 against 9.92-10.01 ms).
       static const int fork_mode = [] {
         const char* h = getenv("KGX_EXACT_FORK");
-        return h ? atoi(h) : 3;  // 3: measured 9.69-9.73 -> 8.96-8.98 ms at NS (0: sequential)
+        return h ? atoi(h) : 3;
       }();
-      static const int hub_cus = [] {
-        const char* h = getenv("KGX_EXACT_HUB_CUS");
-        return h ? atoi(h) : 0;
-      }();
-      // KGX_EXACT_FORK=3 (default): forked, spmm_kernel on its full grid taking
-      // interleaved row batches from a counter (one atomic per kDynRows rows),
-      // and the short-row kernel after it, once the hub kernel's tail is over.
-      // The hub kernel's mass of rows ends in ~0.3 ms; its largest row then
-      // holds two CUs for ~1 ms, which spmm_kernel's batches fill: NS EXACT
-      // aggregation 9.69-9.73 -> 8.96-8.98 ms (profiles/r04/exact_fork3_ab.jsonl)
-      const bool fork_on = fork_mode == 1 || fork_mode == 2 || fork_mode == 3;
-      a.dyn_rows = fork_mode == 1 ? 1 : (fork_mode == 3 ? 2 : 0);
-      int64_t hub_blocks = nb;
-      if (fork_mode == 2 && hub_cus > 0 && hub_cus < hub_blocks) hub_blocks = hub_cus;
+      const bool fork_on = fork_mode == 3;
+      a.dyn_rows = fork_on ? 1 : 0;
       if (a.dyn && fork_on) {
         // dynamic pickup: the hub kernel runs on a forked stream BESIDE spmm_kernel
         // (which skips the hub rows and takes its rows from a counter), so the CUs
@@ -846,7 +821,7 @@ int launch_main(const SpmmArgs& a_in, hipStream_t s) {
           set_error("kgx_spmm: stream fork failed");
           return KGX_ERR_HIP;
         }
-        hipLaunchKernelGGL(kh, dim3(unsigned(hub_blocks)), dim3(kHubThreads), 0, fj.side, a);
+        hipLaunchKernelGGL(kh, dim3(unsigned(nb)), dim3(kHubThreads), 0, fj.side, a);
         KGX_CHECK_LAUNCH();
         if (hipEventRecord(fj.join, fj.side) != hipSuccess) {
           set_error("kgx_spmm: stream join failed");
@@ -855,7 +830,6 @@ int launch_main(const SpmmArgs& a_in, hipStream_t s) {
         joined = &fj;
         guard.fj = &fj;
         guard.s = s;
-        if (fork_mode == 2) a_hub_slots = hub_blocks * (kHubThreads / kBlock);  // spmm blocks a hub block displaces
       } else {
         hipLaunchKernelGGL(kh, dim3(unsigned(nb)), dim3(kHubThreads), 0, s, a);
         KGX_CHECK_LAUNCH();
@@ -893,7 +867,7 @@ int launch_main(const SpmmArgs& a_in, hipStream_t s) {
   };
   // the short-row kernel first, except beside a forked hub kernel whose rows
   // spmm_kernel's dynamic batches work around (KGX_EXACT_FORK=3)
-  const bool short_last = a.dyn_rows == 2 && joined;
+  const bool short_last = a.dyn_rows && joined;
   if (!short_last && launch_short() != KGX_OK) return KGX_ERR_HIP;
   const int64_t work_long = a.items ? a.n_long : a.n_rows_long;
   if (work_long > 0) {
@@ -901,12 +875,7 @@ int launch_main(const SpmmArgs& a_in, hipStream_t s) {
     if constexpr (RED == KGX_SUM && !TWO) {
       if (a.drop_key) k = spmm_kernel<VEC, NT, RED, W, true>;
     }
-    unsigned grid = resident_grid(k, work_long, a.G);
-    if (a_hub_slots > 0) {
-      const int64_t g = int64_t(grid) - a_hub_slots;
-      grid = unsigned(g > int64_t(cu_count()) ? g : int64_t(cu_count()));
-    }
-    hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(k, dim3(resident_grid(k, work_long, a.G)), dim3(kBlock), 0, s, a);
     KGX_CHECK_LAUNCH();
   }
   if (short_last && launch_short() != KGX_OK) return KGX_ERR_HIP;
