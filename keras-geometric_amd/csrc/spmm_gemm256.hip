@@ -667,14 +667,6 @@ inline int cu_split_per32() {
   return v > 0 && v < 32 ? v : 0;
 }
 
-// KGX_F256_MID_AFTER (measurement): with the CU split, the degree 3..7 launch
-// runs after the join on the whole GPU instead of after the long rows on the
-// head's CUs.
-inline bool mid_after_join() {
-  const char* e = getenv("KGX_F256_MID_AFTER");
-  return e && atoi(e) != 0;
-}
-
 template <int RED, bool WT, bool TWO>
 int launch256(const F256Args& a, hipStream_t s) {
   const int64_t work = a.items ? a.n_work : a.n_rows;
@@ -705,17 +697,14 @@ int launch256(const F256Args& a, hipStream_t s) {
     hipLaunchKernelGGL(k, dim3(grid256(k, (n_long + kRows - 1) / kRows, cus_h)), dim3(kThreads), 0, sh, b);
     KGX_CHECK_LAUNCH();
   }
-  const bool mid_after = join.cs && mid_after_join();
-  auto launch_mid = [&](hipStream_t sm, int cus) -> int {
+  if (work > n_long) {
     F256Args b = a;
     b.items = a.items + n_long;
     b.n_work = work - n_long;
     auto k = spmm_gemm256_kernel<RED, WT, kMidPF, TWO>;
-    hipLaunchKernelGGL(k, dim3(grid256(k, (b.n_work + kRows - 1) / kRows, cus)), dim3(kThreads), 0, sm, b);
+    hipLaunchKernelGGL(k, dim3(grid256(k, (b.n_work + kRows - 1) / kRows, cus_h)), dim3(kThreads), 0, sh, b);
     KGX_CHECK_LAUNCH();
-    return KGX_OK;
-  };
-  if (work > n_long && !mid_after && launch_mid(sh, cus_h) != KGX_OK) return KGX_ERR_HIP;
+  }
   if (a.tpack && a.n_tiny > 0) {
     const bool fast = a.F_out == kF && !a.accumulate && !a.agg_out;
     auto k = a.pre_gin
@@ -733,7 +722,6 @@ int launch256(const F256Args& a, hipStream_t s) {
     KGX_CHECK_HIP(hipStreamWaitEvent(s, cs->jh, 0));
     KGX_CHECK_HIP(hipStreamWaitEvent(s, cs->jt, 0));
   }
-  if (work > n_long && mid_after && launch_mid(s, 0) != KGX_OK) return KGX_ERR_HIP;
   if (a.items && a.n_split > 0) {
     const int64_t blocks = (a.n_split + 3) / 4;
     hipLaunchKernelGGL(spmm_gemm256_fixup_kernel<RED>, dim3(unsigned(blocks < 4096 ? blocks : 4096)), dim3(256), 0,

@@ -1,4 +1,4 @@
-# Round 5: C4 with the degree 3..7 launch after the CU split's join on the whole GPU
+# Round 5 (measured, not kept: tools/experiments/round5_f256_mid_after.patch): C4 with the degree 3..7 launch after the CU split's join on the whole GPU
 # (KGX_F256_MID_AFTER=1) against after the long rows on the head's 192 CUs: the 256-wide
 # bit-identity tests with it on, then C4 bench lines interleaved -> gpurun_out/mid
 set -o pipefail
