@@ -13,6 +13,8 @@ every call) and reused across steps, as a GNN training loop over a fixed graph d
             ~100M edges of one global R-MAT graph of N x 10M nodes / N x 100M
             edges; source rows owned by other ranks arrive by a halo all-to-all
             over RCCL (xGMI), pipelined under the own-source pass.
+--config ns_strong: the north-star GCNConv, STRONG scaling: the one 10M / 100M
+            graph split by destination range over the N GPUs (N = 1: ns).
 --config c4: GINConv sum, F 256, STRONG scaling: one 10M / 100M graph split by
             destination range over the N GPUs (BASELINE.json configs[3]).
 --config c5: SAGEConv mean, F 100, STRONG scaling: the ogbn-products-shaped
@@ -50,6 +52,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level
 # name: (layer, nodes, edges, F_in, F_out, scaling); weak: nodes/edges per GPU, strong: the whole graph
 CONFIGS = {  # name: (layer, nodes, edges, F_in, F_out, scaling); "tiny" is a control-flow size, not a BASELINE config
     "ns": ("gcn", 10_000_000, 100_000_000, 128, 128, "weak"),
+    # the same 10M / 100M north-star graph split by destination range over the N GPUs
+    "ns_strong": ("gcn", 10_000_000, 100_000_000, 128, 128, "strong"),
     "c2": ("gcn", 1_000_000, 10_000_000, 128, 128, "weak"),
     "tiny": ("gcn", 100_000, 1_000_000, 128, 128, "weak"),
     "c3": ("gat", 1_000_000, 10_000_000, 128, 128, "weak"),
@@ -273,6 +277,7 @@ def shard_summary(sg, kind: str, f_in: int, f_out: int, exact: bool) -> dict:
             "halo_rows_pull_only": sg.n_halo, "halo_rows": n_moved,
             "halo_rows_pushed_partials": pp.n_push if pp is not None else 0,
             "halo_MB_per_layer": n_moved * f_x * 4 / 1e6,
+            "halo_GB_per_layer": n_moved * f_x * 4 / 1e9,
             "halo_chunks": sg.halo_k if sg.halo_k is not None else (len(pp.chunks) if pp else len(sg.chunks)),
             # the tuner's unit, or (tuning skipped: K fixed) the one the merged passes use
             "merge_unit": sg.merge_unit or (os.environ.get("KGX_HALO_MERGE", "step")
@@ -396,6 +401,8 @@ def main() -> None:
 
     kops.EVENT_SINK = []
     split0 = kops.CU_SPLIT_LAUNCHES
+    if world > 1:
+        sg.link_probe = []  # every exchange step's pack-to-landing time (ShardedGraph.link_report)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -443,16 +450,32 @@ def main() -> None:
     else:  # GIN: + the x_i root row of the (1+eps) x_i + aggr epilogue; SAGE mean: plain gather-sum
         balg = b_alg_spmm(n_rows, e_agg, f_in, weighted=False) + (4 * n_rows * f_in if kind == "gin" else 0)
         kernel = ("spmm_kernel", "spmm_short_kernel", "spmm_fixup_kernel")
-    achieved = balg / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
-    mine = {"rank": rank, "e_agg": e_agg, "rows": n_rows, "ms_per_step": elapsed / args.steps * 1e3,
-            "aggregation_ms": kern_ms, "launches_per_step": launches, "roofline_achieved_GBps": achieved,
-            "roofline_frac": achieved / HBM_PEAK_GBS, **shard_info}
+    step_ms = elapsed / args.steps * 1e3
+    if world == 1:  # the op's own event time (one launch, or one fork-to-join of a CU-split op)
+        achieved = balg / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
+    else:
+        # N > 1: a step is a pipeline of passes, packing and transfers that overlap in time, so
+        # the sum of their event times means nothing; a rank's rate is its algorithmic bytes over
+        # its own step time
+        achieved = balg / (step_ms * 1e-3) / 1e9
+    mine = {"rank": rank, "e_agg": e_agg, "rows": n_rows, "ms_per_step": step_ms,
+            "aggregation_ms": kern_ms, "launches_per_step": launches, "algorithmic_bytes": balg,
+            "roofline_achieved_GBps": achieved, "roofline_frac": achieved / HBM_PEAK_GBS, **shard_info}
+    if world > 1:
+        torch.cuda.synchronize()
+        links = sg.link_report(args.steps)
+        mine["links"] = links
+        mine["link_measured_ms_sum"] = sum(r["measured_ms"] for r in links)
+        mine["link_modelled_ms_sum_at_400GBps"] = sum(r["modelled_ms_at_400GBps"] for r in links)
+        sg.link_probe = None
 
     if world > 1:
         ranks = [None] * world
         dist.all_gather_object(ranks, mine)
         elapsed = max(r["ms_per_step"] for r in ranks) * args.steps / 1e3
         e_total = float(sum(r["e_agg"] for r in ranks))
+        slow = max(ranks, key=lambda r: r["ms_per_step"])  # the rank that sets the step
+        achieved, balg = slow["roofline_achieved_GBps"], slow["algorithmic_bytes"]
     else:
         ranks = None
         e_total = float(e_agg)
@@ -529,6 +552,9 @@ def main() -> None:
             # FETCH_SIZE x 2 + WRITE_SIZE: L2 <-> fabric bytes, Infinity-Cache (MALL) hits included
             "traffic_kind": "L2-fabric bytes (TCC FETCH_SIZE/WRITE_SIZE, MALL hits included)" if traffic else None,
             "algorithmic_bytes_per_launch": balg,
+            # N > 1: the slowest rank's B_alg / its ms_per_step (per-rank values in per_rank)
+            "achieved_basis": ("op event time" if world == 1 else
+                               "slowest rank: its SURVEY 8(d) bytes / its ms_per_step (pipelined step)"),
             # KGX_FUSED_CU_SPLIT: the op's launches ran side by side on two CU-masked streams (main
             # kernel on 192 CUs, tail launches on 64); `achieved` divides by the op's fork-to-join event
             # time, and rocprof's per-kernel averages of those launches overlap in time

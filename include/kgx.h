@@ -68,6 +68,17 @@ int kgx_version(void);
 const char* kgx_last_error(void);
 
 /* ---------------------------------------------------------------------------
+ * The CU split (KGX_FUSED_CU_SPLIT launches): validated on gfx950 with 256 CUs
+ * in 8 XCDs only.  kgx_cu_split_layout_ok: 1 when (cus, xccs, arch) is that
+ * layout (pure, no device needed).  kgx_cu_split_supported: 1 when `device`
+ * has it, 0 when its KGX_FUSED_CU_SPLIT launches run unsplit (one note on
+ * stderr), < 0 on error.  A launch whose stream is on another device than the
+ * current one also runs unsplit.
+ * ------------------------------------------------------------------------- */
+int kgx_cu_split_layout_ok(int cus, int xccs, const char* arch);
+int kgx_cu_split_supported(int device);
+
+/* ---------------------------------------------------------------------------
  * Graph preparation: COO int32 [2,E] (generation order, unsorted) -> CSR by
  * destination, STABLE (edges of one destination keep their input order, the
  * self-loop is last), which is the order the reference's segment_sum
@@ -87,8 +98,21 @@ const char* kgx_last_error(void);
  *   rowptr[n_dst+1], col[cap] (source id per CSR slot), eid[cap] (input edge
  *   id per CSR slot; self loop i has id E+i), deg[n_dst] (int32 in-degree),
  *   optional dinv[n_dst] and w[cap] (KGX_CSR_GCN_NORM).
- * info[4] (host) receives: kept edges, max in-degree, #bad indices, 0.
+ * info[4] (host) receives: kept edges, max in-degree, #bad indices, and
+ * (kgx_csr_build2) the rows whose degree the dinv table did not cover.
  * This call synchronises `stream` once (to return info).
+ *
+ * GCN_NORM's dinv: kgx_csr_build computes (deg + 1e-12)^-0.5 correctly
+ * rounded.  kgx_csr_build2 takes it from the caller's device table instead,
+ *   dinv[i] = dinv_table[min(deg[i], 2^24)],   table_len entries,
+ * filled with the reference's own values: utils/main.py:25's
+ * power(deg + 1e-12, -0.5) lowers to torch.pow(Tensor, Tensor), ATen's
+ * vectorised (Sleef) powf, which differs from the correctly-rounded value by
+ * 1 ulp for some degrees.  With that table dinv and w are bit-identical to
+ * the reference's (graph.gcn_dinv_table builds it).  A degree the table does
+ * not cover takes the correctly-rounded value and is counted in info[3]; the
+ * caller then redoes dinv / w with a longer table (kgx_gcn_dinv_table +
+ * kgx_gcn_edge_norm).  dinv_table NULL: kgx_csr_build.
  * ------------------------------------------------------------------------- */
 int kgx_csr_workspace_bytes(int64_t E, int64_t n_dst, int flags, size_t* bytes);
 int kgx_csr_build(const int32_t* src, const int32_t* dst, int64_t E,
@@ -97,6 +121,12 @@ int kgx_csr_build(const int32_t* src, const int32_t* dst, int64_t E,
                   float* dinv, float* w,
                   void* workspace, size_t workspace_bytes,
                   int64_t* info, kgx_stream_t stream);
+int kgx_csr_build2(const int32_t* src, const int32_t* dst, int64_t E,
+                   int64_t n_src, int64_t n_dst, int flags,
+                   int32_t* rowptr, int32_t* col, int32_t* eid, int32_t* deg,
+                   float* dinv, float* w, const float* dinv_table, int64_t table_len,
+                   void* workspace, size_t workspace_bytes,
+                   int64_t* info, kgx_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * GCN normalisation for a CSR whose sources index a different table than its
@@ -104,8 +134,13 @@ int kgx_csr_build(const int32_t* src, const int32_t* dst, int64_t E,
  * nodes).  Same arithmetic as KGX_CSR_GCN_NORM (utils/main.py:20-33):
  *   dinv[i] = (float(min(deg[i], 2^24)) + 1e-12f)^-0.5  (correctly rounded)
  *   w[e]    = dinv_dst[row(e)] * dinv_src[col[e]]       (CSR order)
+ * kgx_gcn_dinv_table: dinv[i] = table[min(deg[i], 2^24)] (the reference's
+ * values, see kgx_csr_build2); the caller's table must cover
+ * min(max(deg), 2^24) (indices past it read the last entry).
  * ------------------------------------------------------------------------- */
 int kgx_gcn_dinv(const int32_t* deg, int64_t n, float* dinv, kgx_stream_t stream);
+int kgx_gcn_dinv_table(const int32_t* deg, int64_t n, const float* table, int64_t table_len,
+                       float* dinv, kgx_stream_t stream);
 int kgx_gcn_edge_norm(const int32_t* rowptr, const int32_t* col, int64_t n_dst,
                       const float* dinv_dst, const float* dinv_src, float* w,
                       kgx_stream_t stream);

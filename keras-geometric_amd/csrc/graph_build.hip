@@ -26,7 +26,7 @@ struct CsrStatus {
   unsigned long long bad;      // out-of-range indices
   unsigned long long max_deg;  // max in-degree
   unsigned long long kept;     // rowptr[n_dst]
-  unsigned long long pad;
+  unsigned long long table_miss;  // rows whose fp32 degree the dinv table does not cover
 };
 
 __global__ void csr_prep_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
@@ -99,24 +99,42 @@ __device__ __forceinline__ float gcn_dinv(int32_t d) {
   return __fdiv_rn(1.0f, sqrt_rn(__fadd_rn(ref_count_f32(d), 1e-12f)));
 }
 
+// dinv from the caller's table of the reference's own values: table[k] =
+// (float(k) + 1e-12f)^-0.5 as ATen's tensor-exponent pow evaluates it
+// (utils/main.py:25 -> keras.ops.power -> torch.pow(Tensor, Tensor); built on
+// the host by graph.gcn_dinv_table).  The index is the fp32 count, which
+// saturates at 2^24 (ref_count_f32).  A degree past the table counts as a miss
+// and takes the correctly-rounded value; the caller then redoes dinv with a
+// longer table (kgx_gcn_dinv_table).
+__device__ __forceinline__ float gcn_dinv_lookup(int32_t d, const float* __restrict__ table, int64_t len,
+                                                 unsigned* miss) {
+  const int64_t k = d < (1 << 24) ? d : (1 << 24);
+  if (k < len) return table[k];
+  *miss += 1;
+  return gcn_dinv(d);
+}
+
 __global__ void csr_deg_kernel(const int32_t* __restrict__ rowptr, int64_t n_dst, int flags,
                                int32_t* __restrict__ deg, float* __restrict__ dinv,
+                               const float* __restrict__ table, int64_t table_len,
                                CsrStatus* __restrict__ st) {
   const int64_t stride = int64_t(gridDim.x) * blockDim.x;
   unsigned long long mx = 0;
+  unsigned miss = 0;
   for (int64_t r = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; r < n_dst; r += stride) {
     const int32_t d = rowptr[r + 1] - rowptr[r];
     deg[r] = d;
     mx = d > (int64_t)mx ? (unsigned long long)d : mx;
-    // (torch's tensor-exponent powf may differ by 1 ulp: DESIGN.md "GCN norm".)
-    if (flags & KGX_CSR_GCN_NORM) dinv[r] = gcn_dinv(d);
+    if (flags & KGX_CSR_GCN_NORM) dinv[r] = table ? gcn_dinv_lookup(d, table, table_len, &miss) : gcn_dinv(d);
   }
   // wave max then one atomic per wave
   for (int o = 32; o > 0; o >>= 1) {
     unsigned long long other = __shfl_xor(mx, o, 64);
     mx = other > mx ? other : mx;
+    miss += __shfl_xor(miss, o, 64);
   }
   if ((threadIdx.x & 63) == 0 && mx) atomicMax(&st->max_deg, mx);
+  if ((threadIdx.x & 63) == 0 && miss) atomicAdd(&st->table_miss, (unsigned long long)miss);
 }
 
 // norm_e = dinv[dst] * dinv[src]  (utils/main.py:29-32; take(dinv,target)*take(dinv,source))
@@ -168,15 +186,43 @@ __global__ void gcn_dinv_kernel(const int32_t* __restrict__ deg, int64_t n, floa
   for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) dinv[i] = gcn_dinv(deg[i]);
 }
 
-// one wave per row, lanes stride over the row's edges (coalesced)
+__global__ void gcn_dinv_table_kernel(const int32_t* __restrict__ deg, int64_t n, const float* __restrict__ table,
+                                      int64_t len, float* __restrict__ dinv) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int32_t d = deg[i];
+    const int64_t k = d < (1 << 24) ? d : (1 << 24);
+    dinv[i] = table[k < len ? k : len - 1];  // the caller covers max(deg) (kgx.h)
+  }
+}
+
+// w_e = dinv_dst[row(e)] * dinv_src[col[e]].  A group of 8 lanes per row
+// (8 rows per wave: most rows of a power-law graph have a few edges); rows of
+// degree > 64 are left to the wave pass below, which strides a whole wave
+// over them, so a hub row does not serialise on 8 lanes.
 __global__ void gcn_edge_norm_kernel(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
                                      int64_t n_dst, const float* __restrict__ dinv_dst,
                                      const float* __restrict__ dinv_src, float* __restrict__ w) {
+  const int sub = threadIdx.x & 7;
+  const int64_t ng = (int64_t(gridDim.x) * blockDim.x) >> 3;
+  for (int64_t r = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 3; r < n_dst; r += ng) {
+    const int32_t b = rowptr[r], e1 = rowptr[r + 1];
+    if (e1 - b > 64) continue;
+    const float dr = dinv_dst[r];
+    for (int32_t e = b + sub; e < e1; e += 8) w[e] = __fmul_rn(dr, dinv_src[col[e]]);
+  }
+}
+
+__global__ void gcn_edge_norm_long_kernel(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                                          int64_t n_dst, const float* __restrict__ dinv_dst,
+                                          const float* __restrict__ dinv_src, float* __restrict__ w) {
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t(gridDim.x) * blockDim.x) >> 6;
   for (int64_t r = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; r < n_dst; r += nw) {
+    const int32_t b = rowptr[r], e1 = rowptr[r + 1];
+    if (e1 - b <= 64) continue;
     const float dr = dinv_dst[r];
-    for (int32_t e = rowptr[r] + lane; e < rowptr[r + 1]; e += 64) w[e] = __fmul_rn(dr, dinv_src[col[e]]);
+    for (int32_t e = b + lane; e < e1; e += 64) w[e] = __fmul_rn(dr, dinv_src[col[e]]);
   }
 }
 
@@ -411,10 +457,11 @@ extern "C" int kgx_csr_workspace_bytes(int64_t E, int64_t n_dst, int flags, size
   return KGX_OK;
 }
 
-extern "C" int kgx_csr_build(const int32_t* src, const int32_t* dst, int64_t E, int64_t n_src,
-                             int64_t n_dst, int flags, int32_t* rowptr, int32_t* col, int32_t* eid,
-                             int32_t* deg, float* dinv, float* w, void* workspace,
-                             size_t workspace_bytes, int64_t* info, kgx_stream_t stream_) {
+extern "C" int kgx_csr_build2(const int32_t* src, const int32_t* dst, int64_t E, int64_t n_src,
+                              int64_t n_dst, int flags, int32_t* rowptr, int32_t* col, int32_t* eid,
+                              int32_t* deg, float* dinv, float* w, const float* dinv_table,
+                              int64_t table_len, void* workspace, size_t workspace_bytes, int64_t* info,
+                              kgx_stream_t stream_) {
   hipStream_t stream = as_stream(stream_);
   const bool loops = flags & KGX_CSR_SELF_LOOPS;
   const bool norm = flags & KGX_CSR_GCN_NORM;
@@ -428,6 +475,7 @@ extern "C" int kgx_csr_build(const int32_t* src, const int32_t* dst, int64_t E, 
   KGX_REQUIRE(rowptr && deg && (total == 0 || (col && eid)), KGX_ERR_ARG, "kgx_csr_build: null output");
   KGX_REQUIRE(E == 0 || (src && dst), KGX_ERR_ARG, "kgx_csr_build: null input");
   KGX_REQUIRE(!norm || (dinv && (total == 0 || w)), KGX_ERR_ARG, "kgx_csr_build: GCN_NORM needs dinv and w");
+  KGX_REQUIRE(!dinv_table || table_len > 0, KGX_ERR_ARG, "kgx_csr_build2: empty dinv table");
   CsrLayout L = csr_layout(workspace, total, n_dst);
   KGX_REQUIRE(workspace && workspace_bytes >= L.total, KGX_ERR_ARG,
               "kgx_csr_build: workspace %zu < %zu bytes", workspace_bytes, L.total);
@@ -453,7 +501,7 @@ extern "C" int kgx_csr_build(const int32_t* src, const int32_t* dst, int64_t E, 
   }
   if (n_dst > 0) {
     hipLaunchKernelGGL(csr_deg_kernel, dim3(grid_for(n_dst, 8192)), dim3(kBlock), 0, stream, rowptr, n_dst,
-                       flags, deg, dinv, L.st);
+                       flags, deg, dinv, dinv_table, table_len, L.st);
     KGX_CHECK_LAUNCH();
   }
   if (norm && total > 0) {
@@ -468,13 +516,21 @@ extern "C" int kgx_csr_build(const int32_t* src, const int32_t* dst, int64_t E, 
     info[0] = int64_t(hs.kept);
     info[1] = int64_t(hs.max_deg);
     info[2] = int64_t(hs.bad);
-    info[3] = 0;
+    info[3] = int64_t(hs.table_miss);
   }
   KGX_REQUIRE(hs.bad == 0, KGX_ERR_INDEX,
               "index out of range in edge_index: %llu edge(s) reference a node outside "
               "[-n, n) (n_src=%lld, n_dst=%lld)",
               hs.bad, (long long)n_src, (long long)n_dst);
   return KGX_OK;
+}
+
+extern "C" int kgx_csr_build(const int32_t* src, const int32_t* dst, int64_t E, int64_t n_src,
+                             int64_t n_dst, int flags, int32_t* rowptr, int32_t* col, int32_t* eid,
+                             int32_t* deg, float* dinv, float* w, void* workspace,
+                             size_t workspace_bytes, int64_t* info, kgx_stream_t stream_) {
+  return kgx_csr_build2(src, dst, E, n_src, n_dst, flags, rowptr, col, eid, deg, dinv, w, nullptr, 0, workspace,
+                        workspace_bytes, info, stream_);
 }
 
 extern "C" int kgx_schedule_workspace_bytes(int64_t n_dst, size_t* bytes) {
@@ -642,13 +698,39 @@ extern "C" int kgx_gcn_dinv(const int32_t* deg, int64_t n, float* dinv, kgx_stre
   return KGX_OK;
 }
 
+extern "C" int kgx_gcn_dinv_table(const int32_t* deg, int64_t n, const float* table, int64_t table_len, float* dinv,
+                                  kgx_stream_t stream_) {
+  KGX_REQUIRE(n >= 0 && (n == 0 || (deg && dinv && table && table_len > 0)), KGX_ERR_ARG,
+              "kgx_gcn_dinv_table: bad arguments");
+  if (n == 0) return KGX_OK;
+  hipLaunchKernelGGL(gcn_dinv_table_kernel, dim3(grid_for(n, 8192)), dim3(kBlock), 0, as_stream(stream_), deg, n,
+                     table, table_len, dinv);
+  KGX_CHECK_LAUNCH();
+  return KGX_OK;
+}
+
 extern "C" int kgx_gcn_edge_norm(const int32_t* rowptr, const int32_t* col, int64_t n_dst, const float* dinv_dst,
                                  const float* dinv_src, float* w, kgx_stream_t stream_) {
   KGX_REQUIRE(n_dst >= 0 && (n_dst == 0 || (rowptr && col && dinv_dst && dinv_src && w)), KGX_ERR_ARG,
               "kgx_gcn_edge_norm: bad arguments");
   if (n_dst == 0) return KGX_OK;
-  hipLaunchKernelGGL(gcn_edge_norm_kernel, dim3(grid_for(n_dst * 64, 8192)), dim3(kBlock), 0, as_stream(stream_),
-                     rowptr, col, n_dst, dinv_dst, dinv_src, w);
+  hipStream_t s = as_stream(stream_);
+  hipLaunchKernelGGL(gcn_edge_norm_kernel, dim3(grid_for(n_dst * 8, 8192)), dim3(kBlock), 0, s, rowptr, col, n_dst,
+                     dinv_dst, dinv_src, w);
+  KGX_CHECK_LAUNCH();
+  hipLaunchKernelGGL(gcn_edge_norm_long_kernel, dim3(grid_for(n_dst * 64, 8192)), dim3(kBlock), 0, s, rowptr, col,
+                     n_dst, dinv_dst, dinv_src, w);
   KGX_CHECK_LAUNCH();
   return KGX_OK;
+}
+
+extern "C" int kgx_cu_split_layout_ok(int cus, int xccs, const char* arch) {
+  return cu_split_layout_ok(cus, xccs, arch) ? 1 : 0;
+}
+
+extern "C" int kgx_cu_split_supported(int device) {
+  int n = 0;
+  KGX_CHECK_HIP(hipGetDeviceCount(&n));
+  KGX_REQUIRE(device >= 0 && device < n, KGX_ERR_ARG, "kgx_cu_split_supported: no device %d", device);
+  return cu_split_device_ok(device) ? 1 : 0;
 }

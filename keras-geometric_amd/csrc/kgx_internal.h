@@ -8,6 +8,7 @@
 #include <cstdio>
 
 #include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <vector>
 
@@ -167,18 +168,59 @@ inline void cu_split_registry(const CuSplit* add) {
   all.clear();
 }
 
+// The layout the CU split was measured and validated on: gfx950
+// with 256 CUs in 8 XCDs (one partition, SPX).  The split's tail set is "the
+// first per32 of every 32 mask bits", which on that layout is one block of CUs
+// per XCD; other splits of the mask measured 30-300 % slower there, so on any
+// other CU count, XCD count or architecture (another partition mode, a
+// harvested part, a larger chip) the launches run unsplit.
+inline bool cu_split_layout_ok(int cus, int xccs, const char* arch) {
+  return cus == 256 && xccs == 8 && arch && std::strncmp(arch, "gfx950", 6) == 0;
+}
+
+// per device, once per process: does it have the validated layout?  A device
+// that does not gets a one-time note on stderr the first time a split is asked for.
+inline bool cu_split_device_ok(int dev) {
+  static std::mutex mu;
+  static signed char known[64];  // 0 unknown, 1 ok, -1 not
+  if (dev < 0 || dev >= 64) return false;
+  std::lock_guard<std::mutex> lock(mu);
+  if (known[dev] == 0) {
+    int cus = 0, xccs = 0;
+    hipDeviceProp_t prop;
+    const bool got = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+                     hipDeviceGetAttribute(&xccs, hipDeviceAttributeNumberOfXccs, dev) == hipSuccess &&
+                     hipGetDeviceProperties(&prop, dev) == hipSuccess;
+    const bool ok = got && cu_split_layout_ok(cus, xccs, prop.gcnArchName);
+    known[dev] = ok ? 1 : -1;
+    if (!ok)
+      std::fprintf(stderr,
+                   "kgx: device %d (%d CUs, %d XCDs, %s) is not the layout the CU split was validated on "
+                   "(gfx950, 256 CUs, 8 XCDs): fused launches run unsplit\n",
+                   dev, cus, xccs, got ? prop.gcnArchName : "?");
+  }
+  return known[dev] > 0;
+}
+
 // per (host thread, device, split): streams and events made once and kept for
 // the process, like the library's other side streams (a small per-thread cache:
-// a split is never re-created, so streams are not leaked by alternating splits)
-inline CuSplit* cu_split(int per32) {
+// a split is never re-created, so streams are not leaked by alternating splits).
+// The device is the caller stream's; a stream on a device other than the
+// current one runs unsplit (the masked streams are created on the current
+// device).  The pair is shared by every caller stream of the thread, so two
+// CU-split launches from different caller streams of one thread are ordered
+// through it: the split assumes one caller stream per host thread (the
+// layers' and bench.py's case; the sharded passes run unsplit).
+inline CuSplit* cu_split(int per32, hipStream_t caller) {
   constexpr int kCache = 8;
   thread_local CuSplit cache[kCache];
   thread_local int used = 0;
-  int dev = 0;
+  int dev = 0, sdev = 0;
   if (per32 <= 0 || per32 >= 32 || hipGetDevice(&dev) != hipSuccess) return nullptr;
+  if (caller && (hipStreamGetDevice(caller, &sdev) != hipSuccess || sdev != dev)) return nullptr;
   for (int i = 0; i < used; ++i)
     if (cache[i].device == dev && cache[i].per32 == per32) return &cache[i];
-  if (used == kCache) return nullptr;  // more (device, split) pairs than any caller uses: run unsplit
+  if (used == kCache || !cu_split_device_ok(dev)) return nullptr;
   const int cus = cu_count();
   uint32_t mh[8] = {0}, mt[8] = {0};
   int nh = 0, nt = 0;
@@ -192,20 +234,28 @@ inline CuSplit* cu_split(int per32) {
     }
   }
   if (nh == 0 || nt == 0) return nullptr;
-  CuSplit& n = cache[used];
-  if (hipExtStreamCreateWithCUMask(&n.head, 8, mh) != hipSuccess ||
-      hipExtStreamCreateWithCUMask(&n.tail, 8, mt) != hipSuccess ||
-      hipEventCreateWithFlags(&n.fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&n.jh, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&n.jt, hipEventDisableTiming) != hipSuccess)
+  CuSplit n;
+  const bool ok = hipExtStreamCreateWithCUMask(&n.head, 8, mh) == hipSuccess &&
+                  hipExtStreamCreateWithCUMask(&n.tail, 8, mt) == hipSuccess &&
+                  hipEventCreateWithFlags(&n.fork, hipEventDisableTiming) == hipSuccess &&
+                  hipEventCreateWithFlags(&n.jh, hipEventDisableTiming) == hipSuccess &&
+                  hipEventCreateWithFlags(&n.jt, hipEventDisableTiming) == hipSuccess;
+  if (!ok) {  // release whatever was made: run unsplit
+    if (n.head) (void)hipStreamDestroy(n.head);
+    if (n.tail) (void)hipStreamDestroy(n.tail);
+    if (n.fork) (void)hipEventDestroy(n.fork);
+    if (n.jh) (void)hipEventDestroy(n.jh);
+    if (n.jt) (void)hipEventDestroy(n.jt);
     return nullptr;
+  }
   n.device = dev;
   n.per32 = per32;
   n.n_head = nh;
   n.n_tail = nt;
+  cache[used] = n;
   ++used;
-  cu_split_registry(&n);
-  return &n;
+  cu_split_registry(&cache[used - 1]);
+  return &cache[used - 1];
 }
 
 // joins both CU-masked streams back into the caller's stream on every return

@@ -902,7 +902,7 @@ int launch(const FusedArgs& a, hipStream_t s) {
     // the main kernel on a CU-masked stream over 24 of every 32 CUs, the
     // short-row and tiny-row launches on another over the other 8 (cu_split)
     const char* e = getenv("KGX_FUSED_CU_SPLIT");  // tail CUs per 32 (default 8)
-    CuSplit* cs = cu_split(e ? atoi(e) : 8);
+    CuSplit* cs = cu_split(e ? atoi(e) : 8, s);
     if (cs) {
       SplitJoin join;
       KGX_CHECK_HIP(hipEventRecord(cs->fork, s));

@@ -675,7 +675,7 @@ int launch256(const F256Args& a, hipStream_t s) {
   SplitJoin join;
   const int per32 = (a.cu_split && a.tpack && a.n_tiny > 0 && work > 0) ? cu_split_per32() : 0;
   if (per32) {
-    if (CuSplit* cs = cu_split(per32)) {
+    if (CuSplit* cs = cu_split(per32, s)) {
       KGX_CHECK_HIP(hipEventRecord(cs->fork, s));
       KGX_CHECK_HIP(hipStreamWaitEvent(cs->head, cs->fork, 0));
       KGX_CHECK_HIP(hipStreamWaitEvent(cs->tail, cs->fork, 0));

@@ -53,9 +53,14 @@ class KgxBackend:
         return G.build_csr(src, dst, n_src, n_dst, n_features=n_features)
 
     def dinv(self, deg: torch.Tensor) -> torch.Tensor:
+        """The reference's dinv (utils/main.py:25) from the ATen-valued table
+        (graph.gcn_dinv_table), bit-identical to the one-GPU build."""
         out = torch.empty(deg.numel(), dtype=torch.float32, device=deg.device)
-        nat.check(nat.lib().kgx_gcn_dinv(nat.ptr(deg), deg.numel(), nat.ptr(out), nat.stream(deg.device)),
-                  "kgx_gcn_dinv")
+        if deg.numel() == 0:
+            return out
+        table = G.gcn_dinv_table(deg.device, int(deg.max()))
+        nat.check(nat.lib().kgx_gcn_dinv_table(nat.ptr(deg), deg.numel(), nat.ptr(table), table.numel(),
+                                               nat.ptr(out), nat.stream(deg.device)), "kgx_gcn_dinv_table")
         return out
 
     def edge_norm(self, g, dinv_dst: torch.Tensor, dinv_src: torch.Tensor) -> torch.Tensor:
@@ -438,6 +443,8 @@ class ShardedGraph:
     tuning_s: float | None = None  # wall time tune_exchange took on this rank
     tuning_skipped: int = 0  # candidates left untimed once KGX_TUNE_BUDGET_S was spent
     self_loops: bool = True  # the shard graph carries utils/main.py:8-16's self loops (GCN, GATv2)
+    link_probe: list | None = None  # a list: time every exchange step's landing (bench.py N > 1; link_report)
+    _probe_stream: object = None
 
     @property
     def lo(self) -> int:
@@ -1141,14 +1148,19 @@ class ShardedGraph:
         wait() orders the then-current stream after that chunk's rows (None:
         the comm ran synchronously and the rows are already ordered)."""
         chunks = self.chunks if chunks is None else chunks
+        probe = []  # (chunk, step, start event, handle, send bytes, receive bytes) when link_probe is on
 
         def run():
             start = getattr(self.comm, "all_to_all_start", None)
             works = []
-            for c in chunks:
+            for k, c in enumerate(chunks):
                 handles = []
-                for st in c.steps or [c]:
+                for j, st in enumerate(c.steps or [c]):
                     send = self._pack(x_local, st)
+                    ev = None
+                    if self.link_probe is not None and start is not None and x_local.is_cuda:
+                        ev = torch.cuda.Event(enable_timing=True)
+                        ev.record()  # the side stream, after this step's packing: the transfer may start
                     if st.kind == "allgather":
                         gstart = getattr(self.comm, "all_gather_start", None) if start is not None else None
                         if gstart is None:
@@ -1160,6 +1172,8 @@ class ShardedGraph:
                         self.comm.all_to_all_single(halo[st.lo: st.hi], send, st.recv_splits, st.send_splits)
                     else:
                         handles.append(start(halo[st.lo: st.hi], send, st.recv_splits, st.send_splits))
+                    if ev is not None and handles[-1] is not None:
+                        probe.append((k, j, ev, handles[-1], send.numel() * 4, (st.hi - st.lo) * halo.shape[1] * 4))
                 works.append(_Works(handles) if start is not None else None)
             return works
 
@@ -1182,7 +1196,40 @@ class ShardedGraph:
             self.packs_done.record()
         if any(w is None for w in works):  # synchronous comm: order the halo rows before later work
             cur.wait_stream(self._side)
+        if probe:  # the landing of every step, seen from a stream that waits for nothing else
+            if self._probe_stream is None:
+                self._probe_stream = torch.cuda.Stream(device=x_local.device)
+            self._probe_stream.wait_stream(self._side)
+            with torch.cuda.stream(self._probe_stream):
+                for k, j, ev0, h, sb, rb in probe:
+                    h.wait()
+                    ev1 = torch.cuda.Event(enable_timing=True)
+                    ev1.record()
+                    self.link_probe.append({"chunk": k, "step": j, "start": ev0, "land": ev1,
+                                            "send_bytes": sb, "recv_bytes": rb})
         return works
+
+    def link_report(self, steps: int, link_gbps: float = 400.0) -> list:
+        """Per exchange step (chunk, step), averaged over `steps` layer calls of
+        the link_probe log (call after a synchronize): the bytes this rank sent
+        and received, the measured time from the end of its packing to its
+        landing (the transfer, plus any wait behind the previous steps on the
+        comm stream), and the time a modelled link of `link_gbps` would take for
+        the received bytes (tools/shard_sim.py's model)."""
+        acc = {}
+        for r in self.link_probe or []:
+            a = acc.setdefault((r["chunk"], r["step"]), {"chunk": r["chunk"], "step": r["step"], "n": 0, "ms": 0.0,
+                                                        "send_bytes": r["send_bytes"], "recv_bytes": r["recv_bytes"]})
+            a["n"] += 1
+            a["ms"] += r["start"].elapsed_time(r["land"])
+        out = []
+        for key in sorted(acc):
+            a = acc[key]
+            out.append({"chunk": a["chunk"], "step": a["step"], "send_MB": a["send_bytes"] / 1e6,
+                        "recv_MB": a["recv_bytes"] / 1e6, "measured_ms": a["ms"] / max(a["n"], 1),
+                        "modelled_ms_at_%dGBps" % int(link_gbps): a["recv_bytes"] / (link_gbps * 1e6),
+                        "calls": a["n"]})
+        return out
 
     def propagate_overlapped(self, x_local: torch.Tensor, reduce: str = "sum", *, gin_scale: float | None = None,
                              weighted: bool = False, bias: torch.Tensor | None = None) -> torch.Tensor:

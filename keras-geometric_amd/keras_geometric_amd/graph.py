@@ -83,6 +83,48 @@ class CSRGraph:
         return self.items, self.n_items, self.split, self.n_split, self.n_slots
 
 
+# ---------------------------------------------------------------------------
+# GCN dinv as the reference evaluates it
+# ---------------------------------------------------------------------------
+_DINV_TABLES: dict = {}
+_DINV_SLICE = 16384  # < ATen's GRAIN_SIZE (one thread) and a multiple of every vector width
+
+
+def _dinv_values(lo: int, hi: int) -> torch.Tensor:
+    """float32 [hi - lo]: (k + 1e-12)^-0.5 for k in [lo, hi) exactly as the
+    reference computes dinv (utils/main.py:25: keras.ops.power(keras.ops.add(
+    degrees, 1e-12), -0.5) -> torch.pow(Tensor, 0-dim Tensor) on ATen's CPU
+    kernel).  ATen evaluates that with its vectorised (Sleef) powf, which is
+    not correctly rounded for some degrees; scalar leftovers of a vector loop
+    would use libm's powf instead, so the values are made in aligned slices
+    that run on one thread and end on a whole vector: every entry takes the
+    vectorised path, the one ATen takes for all but the last few elements of
+    each thread's chunk of the reference's degree vector."""
+    out = []
+    exp = torch.tensor(-0.5, dtype=torch.float32)
+    for a in range(lo - lo % _DINV_SLICE, hi, _DINV_SLICE):
+        k = torch.arange(a, a + _DINV_SLICE, dtype=torch.float32)
+        out.append(torch.pow(torch.add(k, torch.tensor(1e-12, dtype=torch.float32)), exp))
+    vals = torch.cat(out)
+    off = lo - (lo - lo % _DINV_SLICE)
+    return vals[off: off + hi - lo]
+
+
+def gcn_dinv_table(device: torch.device, max_degree: int = 0) -> torch.Tensor:
+    """Device table dinv_table[k] = the reference's dinv of a node of fp32 degree
+    k, covering k <= min(max_degree, 2^24) (grown in powers of two and cached
+    per device).  kgx_csr_build2 / kgx_gcn_dinv_table index it."""
+    need = min(max(int(max_degree), 0), 1 << 24) + 1
+    key = str(torch.device(device))
+    t = _DINV_TABLES.get(key)
+    if t is None or t.numel() < need:
+        n = max(4096, 1 << (need - 1).bit_length())
+        n = min(n, (1 << 24) + 1)
+        t = _dinv_values(0, n).to(device)
+        _DINV_TABLES[key] = t
+    return t
+
+
 def build_csr(
     src: torch.Tensor,
     dst: torch.Tensor,
@@ -122,16 +164,25 @@ def build_csr(
     nat.check(L.kgx_csr_workspace_bytes(E, n_dst, flags, ctypes.byref(nbytes)), "kgx_csr_workspace_bytes")
     ws = torch.empty(max(nbytes.value, 1), dtype=torch.uint8, device=dev)
     info = (ctypes.c_int64 * 4)()
+    table = gcn_dinv_table(dev) if gcn_norm else None
     nat.check(
-        L.kgx_csr_build(
+        L.kgx_csr_build2(
             nat.ptr(src), nat.ptr(dst), E, n_src, n_dst, flags,
             nat.ptr(rowptr), nat.ptr(col), nat.ptr(eid), nat.ptr(deg), nat.ptr(dinv), nat.ptr(w),
+            nat.ptr(table), table.numel() if table is not None else 0,
             nat.ptr(ws), nbytes.value, info, nat.stream(dev),
         ),
-        "kgx_csr_build",
+        "kgx_csr_build2",
     )
     del ws
     kept, max_deg = int(info[0]), int(info[1])
+    if gcn_norm and int(info[3]):  # degrees past the table: grow it, redo dinv and w
+        table = gcn_dinv_table(dev, max_deg)
+        st = nat.stream(dev)
+        nat.check(L.kgx_gcn_dinv_table(nat.ptr(deg), n_dst, nat.ptr(table), table.numel(), nat.ptr(dinv), st),
+                  "kgx_gcn_dinv_table")
+        nat.check(L.kgx_gcn_edge_norm(nat.ptr(rowptr), nat.ptr(col), n_dst, nat.ptr(dinv), nat.ptr(dinv),
+                                      nat.ptr(w), st), "kgx_gcn_edge_norm")
     g = CSRGraph(
         n_src=n_src, n_dst=n_dst, n_input_edges=E, kept=kept, max_degree=max_deg, flags=flags,
         rowptr=rowptr, col=col[:kept], eid=eid[:kept], deg=deg[:n_dst],

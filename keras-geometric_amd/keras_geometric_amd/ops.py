@@ -249,9 +249,9 @@ def _f256_cu_split(n_edges: int, n_tiny: int) -> bool:
     (>= 1M tail rows): the fork / join and the smaller grids cost more than they
     hide on small ones.  KGX_F256_CU_SPLIT: unset = this model (8 of every 32
     CUs for the tail), "0" = never, t > 0 = always, with t of every 32 CUs."""
-    env = os.environ.get("KGX_F256_CU_SPLIT")
-    if env is not None:
-        return n_tiny > 0 and env.strip() not in ("", "0")
+    per32 = _per32_override("KGX_F256_CU_SPLIT")
+    if per32 is not None:
+        return n_tiny > 0 and per32 > 0
     if n_tiny < 1_000_000:
         return False
     head_e = max(n_edges - 2 * n_tiny, 0)
@@ -263,11 +263,46 @@ def _f256_cu_split(n_edges: int, n_tiny: int) -> bool:
 CU_SPLIT_LAUNCHES = 0  # launches that ran CU-split (KGX_FUSED_CU_SPLIT): bench.py reports it
 
 
-def _split_allowed() -> bool:
+def _per32_override(name: str):
+    """A KGX_*_CU_SPLIT override parsed as the library parses it: None when
+    unset, else the tail CUs per 32 -- an integer in 1..31, anything else 0
+    (the library then runs unsplit)."""
+    env = os.environ.get(name)
+    if env is None:
+        return None
+    try:
+        v = int(env.strip())
+    except ValueError:
+        return 0
+    return v if 0 < v < 32 else 0
+
+
+_DEVICE_SPLIT_OK: dict = {}
+
+
+def _device_split_ok(dev: torch.device | None) -> bool:
+    """The device has the layout the CU split was validated on (kgx_cu_split_supported:
+    gfx950, 256 CUs, 8 XCDs); else its launches run unsplit and are not counted."""
+    if dev is None:
+        return True
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    ok = _DEVICE_SPLIT_OK.get(idx)
+    if ok is None:
+        ok = _DEVICE_SPLIT_OK[idx] = nat.lib().kgx_cu_split_supported(int(idx)) == 1
+    return ok
+
+
+def _split_allowed(dev: torch.device | None = None) -> bool:
     """CU-split launches stay off while a launch shares the GPU with an exchange
     (sharing_gpu: the sharded layers' passes beside RCCL and the packing), unless
-    KGX_CU_SPLIT_SHARED=1 (measurement)."""
-    return not _share_gpu() or os.environ.get("KGX_CU_SPLIT_SHARED") == "1"
+    KGX_CU_SPLIT_SHARED=1 (measurement); off on a device whose layout is not the
+    validated one, and for a tensor on another device than the current one (the
+    library would run it unsplit)."""
+    if _share_gpu() and os.environ.get("KGX_CU_SPLIT_SHARED") != "1":
+        return False
+    if dev is not None and dev.type == "cuda" and dev.index is not None and dev.index != torch.cuda.current_device():
+        return False
+    return _device_split_ok(dev)
 
 
 def _count_cu_split() -> None:
@@ -283,9 +318,9 @@ def _fused_cu_split(n_edges: int, n_tail_rows: int) -> bool:
     8.92-8.94 ms one-stream; main 8.29 ms on 192 CUs beside the tails' 8.61 on
     64).  KGX_FUSED_CU_SPLIT: unset = this rule, "0" = never, t > 0 = always,
     with t of every 32 CUs (only 8 measured well: see DESIGN.md §4)."""
-    env = os.environ.get("KGX_FUSED_CU_SPLIT")
-    if env is not None:
-        return n_tail_rows > 0 and env.strip() not in ("", "0")
+    per32 = _per32_override("KGX_FUSED_CU_SPLIT")
+    if per32 is not None:
+        return n_tail_rows > 0 and per32 > 0
     return n_edges >= 50_000_000 and n_tail_rows >= 2_000_000
 
 
@@ -311,7 +346,7 @@ def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, b
         partials = torch.empty((n_slots, _partial_width(x)), dtype=torch.float32, device=dev)
     flags = int(pre_gin) | (nat.FUSED_SHARE_GPU if _share_gpu() else 0) | (nat.FUSED_RELU if relu else 0)
     if x.shape[1] == F256:
-        if tpack is not None and items is not None and not save_agg and _split_allowed() and \
+        if tpack is not None and items is not None and not save_agg and _split_allowed(dev) and \
                 _f256_cu_split(idx.numel(), n_items - (n_short_end if n_short_end >= 0 else n_items)):
             flags |= nat.FUSED_CU_SPLIT
             _count_cu_split()
@@ -324,7 +359,7 @@ def _spmm_gemm_impl(x, rowptr, rows, items, split, idx, w, n_slots, reduce, W, b
     # not for the training forward's saved-aggregate launch: its tail launches also store the
     # aggregated rows (the EXTRA instantiations), and split it measured slower (NS training step
     # 23.1 -> 25.0 ms, profiles/r05/train/)
-    if items is not None and not save_agg and _split_allowed() and _fused_cu_split(idx.numel(), n_items - n_long):
+    if items is not None and not save_agg and _split_allowed(dev) and _fused_cu_split(idx.numel(), n_items - n_long):
         flags |= nat.FUSED_CU_SPLIT
         _count_cu_split()
     x2p, n_x1 = _x2_args(x, x2)
@@ -451,9 +486,10 @@ def spmm_gemm_acc_(
     if items is not None and n_split > 0:
         partials = torch.empty((n_slots, _partial_width(x)), dtype=torch.float32, device=dev)
     if x.shape[1] == F256:
-        if tpack is not None and items is not None and _split_allowed() and \
+        if tpack is not None and items is not None and _split_allowed(dev) and \
                 _f256_cu_split(idx.numel(), n_items - (n_short_end if n_short_end >= 0 else n_items)):
             flags |= nat.FUSED_CU_SPLIT
+            _count_cu_split()
         _f256_call(reduce, rowptr, rows, n_dst, items, n_items, split, n_split, idx, w, x, x2, W, bias,
                    (nat.FUSED_ACCUMULATE if accumulate else 0) | (nat.FUSED_SHARE_GPU if _share_gpu() else 0) | flags,
                    gin_scale, out, partials, None, dev, tpack, tw, n_short_end, n_long)
@@ -461,7 +497,7 @@ def spmm_gemm_acc_(
     n_long = n_items if n_long < 0 or n_long > n_items else n_long
     n_se, tpack, tw, n_tiny2 = _tiny_abi(items, n_items, n_long, tpack, tw if w is not None else None, n_short_end,
                                          n_tiny2)
-    if items is not None and _split_allowed() and _fused_cu_split(idx.numel(), n_items - n_long):
+    if items is not None and _split_allowed(dev) and _fused_cu_split(idx.numel(), n_items - n_long):
         flags |= nat.FUSED_CU_SPLIT
         _count_cu_split()
     x2p, n_x1 = _x2_args(x, x2)

@@ -95,3 +95,43 @@ def test_sharing_flag_is_per_thread():
         t.join(10)
     assert seen == {"a_inside": True, "a_after": False, "b_inside": True, "b_after": False}
     assert not ops._share_gpu()
+
+
+@pytest.mark.parametrize("cus,xccs,arch,ok", [
+    (256, 8, b"gfx950:sramecc+:xnack-", True),  # MI355X, SPX: the validated layout
+    (256, 8, b"gfx950", True),
+    (32, 1, b"gfx950:sramecc+:xnack-", False),  # CPX partition: one XCD per device
+    (128, 4, b"gfx950", False),  # DPX
+    (240, 8, b"gfx950", False),  # a harvested part
+    (304, 8, b"gfx942:sramecc+:xnack-", False),  # MI300X
+    (256, 8, b"gfx942", False),
+    (256, 8, None, False),
+])
+def test_cu_split_layout_decision(cus, xccs, arch, ok):
+    """The library's fallback decision (kgx_cu_split_layout_ok, kgx_internal.h
+    cu_split_layout_ok): split only on the layout it was validated on."""
+    assert nat.lib().kgx_cu_split_layout_ok(cus, xccs, arch) == int(ok)
+
+
+@pytest.mark.parametrize("val,per32", [("8", 8), (" 16 ", 16), ("0", 0), ("32", 0), ("40", 0), ("-3", 0),
+                                       ("abc", 0), ("", 0)])
+def test_override_parsed_like_the_library(monkeypatch, val, per32):
+    """KGX_FUSED_CU_SPLIT / KGX_F256_CU_SPLIT: the Python rule asks for (and counts)
+    a split only for values the library runs split (1..31)."""
+    monkeypatch.setenv("KGX_FUSED_CU_SPLIT", val)
+    monkeypatch.setenv("KGX_F256_CU_SPLIT", val)
+    assert ops._per32_override("KGX_FUSED_CU_SPLIT") == per32
+    assert ops._fused_cu_split(110_000_000, 8_600_000) == (per32 > 0)
+    assert ops._f256_cu_split(100_000_000, 7_460_000) == (per32 > 0)
+
+
+def test_split_off_on_unvalidated_device(monkeypatch):
+    import torch
+
+    monkeypatch.delenv("KGX_CU_SPLIT_SHARED", raising=False)
+    monkeypatch.setattr(ops, "_DEVICE_SPLIT_OK", {0: False, 1: True})
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: 0)
+    assert not ops._split_allowed(torch.device("cuda", 0))
+    assert not ops._split_allowed(torch.device("cuda", 1))  # not the current device: the library runs it unsplit
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: 1)
+    assert ops._split_allowed(torch.device("cuda", 1))

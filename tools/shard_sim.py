@@ -34,6 +34,22 @@ from keras_geometric_amd import distributed as kd  # noqa: E402
 from keras_geometric_amd import ops as kops  # noqa: E402
 
 
+TIMELINE: list | None = None  # (what, start event, end event, bytes) when --timeline
+
+
+def _mark():
+    if TIMELINE is None:
+        return None
+    ev = torch.cuda.Event(enable_timing=True)
+    ev.record()
+    return ev
+
+
+def _note(what, t0, t1, nbytes=0):
+    if TIMELINE is not None and t0 is not None:
+        TIMELINE.append((what, t0, t1, nbytes))
+
+
 class _EventWork:
     def __init__(self, ev):
         self.ev = ev
@@ -100,10 +116,12 @@ class LoopbackComm(kd.TorchComm):
         self.link.wait_event(ready)
         with torch.cuda.stream(self.link):
             ms = out.numel() * out.element_size() / (self.link_gbps * 1e6)
+            t0 = _mark()
             if ms > 0:
                 torch.cuda._sleep(int(ms * self.cycles_per_ms))
             if self._land(out):
                 self.all_to_all_single(out, inp, out_splits, in_splits)
+            _note("link", t0, _mark(), out.numel() * out.element_size())
             inp.record_stream(self.link)
             out.record_stream(self.link)
             ev = torch.cuda.Event()
@@ -145,6 +163,8 @@ class LoopbackComm(kd.TorchComm):
 
 CONFIGS = {  # name: (layer, nodes, edges, features, scaling) -- bench.py's configs
     "ns": ("gcn", 10_000_000, 100_000_000, 128, "weak"),
+    # the north-star 10M / 100M graph split over the world (bench.py --config ns_strong)
+    "ns_strong": ("gcn", 10_000_000, 100_000_000, 128, "strong"),
     "c4": ("gin", 10_000_000, 100_000_000, 256, "strong"),
     "c5": ("sage", 2_449_029, 123_718_280, 100, "strong"),
 }
@@ -171,6 +191,10 @@ def main():
     ap.add_argument("--edges", type=int, default=None)
     ap.add_argument("--link-gbps", type=float, default=0.0,
                     help="model the exchange: per-GPU receive rate in GB/s (0: no link time)")
+    ap.add_argument("--timeline", action="store_true",
+                    help="print one more line per run: every kgx op, packing copy and modelled transfer of the "
+                         "last timed step as [start, end] ms from the step's start (which stream: 'link' = the "
+                         "modelled transfer; ops in issue order)")
     ap.add_argument("--free-exchange", action="store_true",
                     help="received buffers land once (a loopback device copy), later exchanges copy nothing: "
                          "with --link-gbps 0 the step is the rank's compute alone; with a link rate the "
@@ -228,6 +252,53 @@ def main():
                 for _ in range(2):
                     layer(x)
                 torch.cuda.synchronize()
+                if args.timeline:  # one extra, separately recorded step
+                    global TIMELINE
+                    TIMELINE = []
+                    kops.EVENT_SINK = []
+                    ref = torch.cuda.Event(enable_timing=True)
+                    ref.record()
+                    gr = kops.gather_rows
+
+                    def timed_gather(table, rows):
+                        t0 = _mark()
+                        out = gr(table, rows)
+                        _note("pack rows", t0, _mark(), 2 * out.numel() * 4)
+                        return out
+
+                    kops.gather_rows = timed_gather
+                    be = sg.backend
+                    saved = {}
+                    for name in ("aggregate_transform", "aggregate", "aggregate_accumulate"):
+                        fn = getattr(be, name)
+                        saved[name] = fn
+
+                        def wrapped(g, *a, _fn=fn, _name=name, **kw):
+                            t0 = _mark()
+                            out = _fn(g, *a, **kw)
+                            what = f"{_name}{'(2 tables)' if kw.get('x2') is not None else ''}" \
+                                   f"{'' if kw.get('accumulate', True) or _name != 'aggregate_transform' else ' overwrite'}"
+                            _note(f"{what} items={g.n_items} edges={g.kept}", t0, _mark())
+                            return out
+
+                        setattr(be, name, wrapped)
+                    kops.EVENT_SINK = None
+                    try:
+                        layer(x)
+                        end = torch.cuda.Event(enable_timing=True)
+                        end.record()
+                        torch.cuda.synchronize()
+                    finally:
+                        kops.gather_rows = gr
+                        for name, fn in saved.items():
+                            setattr(be, name, fn)
+                    items = TIMELINE
+                    TIMELINE = None
+                    tl = sorted(([w, round(ref.elapsed_time(a), 3), round(ref.elapsed_time(b), 3), nb]
+                                 for w, a, b, nb in items), key=lambda r: r[1])
+                    print(json.dumps({"timeline": tl, "step_ms": round(ref.elapsed_time(end), 3),
+                                      "share_den": int(den), "chunks": K, "link_gbps": args.link_gbps}),
+                          flush=True)
                 kops.EVENT_SINK = []
                 t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 t0.record()
