@@ -297,6 +297,9 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cold", action="store_true", help="skip the cold-graph layer timing")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--train", action="store_true",
+                    help="a step is one training step: forward keeping the aggregate P, then backward "
+                         "(dx over the transposed graph, dW = P^T dOut, db); GCN, one GPU")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -307,6 +310,8 @@ def main() -> None:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.train and (world > 1 or CONFIGS[args.config][0] != "gcn" or args.exact):
+        raise SystemExit("--train: the GCN configs on one GPU (the fused forward + backward)")
     # stdout discipline: the one JSON line goes to the original stdout; anything
     # a library prints (gloo/RCCL banners, warnings) lands on stderr
     result_fd = os.dup(1) if rank == 0 else None
@@ -366,6 +371,16 @@ def main() -> None:
         def step():  # the forward (inference) pass: no autograd state kept
             with torch.no_grad():
                 return layer([x, ei])
+
+        if args.train:
+            x.requires_grad_(True)
+            kgx.graph.transpose(g)  # the backward's graph, built once per graph like the forward CSR
+            gout = torch.randn(n_rows, f_out, device=dev)
+
+            def step():  # one training step: forward (P kept), backward (dx, dW, db)
+                x.grad = None
+                layer.zero_grad(set_to_none=True)
+                layer([x, ei]).backward(gout)
     else:
         from keras_geometric_amd.distributed import heartbeat
 
@@ -425,7 +440,28 @@ def main() -> None:
                                                                                      two_table=world > 1)
     # SAGEConv's neighbour map in the aggregation's store (1 GPU; the sharded layer keeps kgx_dense)
     fused_sage = kind == "sage" and world == 1 and not args.exact and kops.fused_sage_supported(f_in, f_out)
-    if kind == "gcn":
+    train_parts = None
+    if kind == "gcn" and args.train:
+        # a training step's algorithmic bytes: the forward + writing P
+        # [N, F_in]; dx = (A^T dOut) W^T, the same fused op over the transposed graph (E' edges, rows
+        # of dOut gathered, N rows of dx written); dW = P^T dOut and db = colsum(dOut): P and dOut
+        # read once
+        b_fwd = b_alg_spmm(n_rows, e_agg, f_in, weighted=True, f_out=f_out) + 4 * n_rows * f_in
+        b_dx = b_alg_spmm(n_rows, e_agg, f_out, weighted=True, f_out=f_in)
+        b_dw = 4 * n_rows * (f_in + f_out) + 4 * f_out * (f_in + 1)
+        balg = b_fwd + b_dx + b_dw
+        kernel = ("spmm_gemm_kernel", "spmm_gemm_short_kernel", "spmm_gemm_tiny_kernel", "spmm_gemm_fixup_kernel")
+        ev_ms = [s.elapsed_time(e) for s, e in events]
+        per = len(ev_ms) // args.steps if args.steps else 0
+        fwd_ms = sum(ev_ms[i] for i in range(0, len(ev_ms), per)) / args.steps if per else None
+        dx_ms = sum(ev_ms[i] for i in range(1, len(ev_ms), per)) / args.steps if per >= 2 else None
+        train_parts = {"forward_keep_P": {"bytes": b_fwd, "ms": fwd_ms},
+                       "dx_transposed": {"bytes": b_dx, "ms": dx_ms},
+                       "dW_db": {"bytes": b_dw, "ms": (elapsed / args.steps * 1e3 - fwd_ms - dx_ms)
+                                 if fwd_ms is not None and dx_ms is not None else None}}
+        for v in train_parts.values():
+            v["GBps"] = v["bytes"] / (v["ms"] * 1e-3) / 1e9 if v["ms"] else None
+    elif kind == "gcn":
         # SURVEY.md §8d per rank; at N>1 the accumulating halo-chunk passes' re-reads
         # of the rows they add to are implementation overhead, not algorithmic bytes
         balg = b_alg_spmm(n_rows, e_agg, f_in if fused else f_out, weighted=True, f_out=f_out)
@@ -451,7 +487,9 @@ def main() -> None:
         balg = b_alg_spmm(n_rows, e_agg, f_in, weighted=False) + (4 * n_rows * f_in if kind == "gin" else 0)
         kernel = ("spmm_kernel", "spmm_short_kernel", "spmm_fixup_kernel")
     step_ms = elapsed / args.steps * 1e3
-    if world == 1:  # the op's own event time (one launch, or one fork-to-join of a CU-split op)
+    if train_parts is not None:  # a training step: its kernels run back to back on one stream
+        achieved = balg / (step_ms * 1e-3) / 1e9
+    elif world == 1:  # the op's own event time (one launch, or one fork-to-join of a CU-split op)
         achieved = balg / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
     else:
         # N > 1: a step is a pipeline of passes, packing and transfers that overlap in time, so
@@ -483,8 +521,9 @@ def main() -> None:
     ms_per_step = elapsed / args.steps * 1e3
     value = e_total * args.steps / elapsed
     traffic, traffic_src = (None, None)
-    if world == 1:
+    if world == 1 and train_parts is None:
         traffic, traffic_src = pmc_traffic(args.config, kernel)
+    if world == 1 and not args.train:
         if not args.no_cold:
             # cold layer: CSR + (GCN) norm + schedule + forward from a fresh edge_index,
             # what the reference pays on every call (utils/main.py:8-33 per call)
@@ -553,7 +592,8 @@ def main() -> None:
             "traffic_kind": "L2-fabric bytes (TCC FETCH_SIZE/WRITE_SIZE, MALL hits included)" if traffic else None,
             "algorithmic_bytes_per_launch": balg,
             # N > 1: the slowest rank's B_alg / its ms_per_step (per-rank values in per_rank)
-            "achieved_basis": ("op event time" if world == 1 else
+            "achieved_basis": ("training step: forward (P kept) + dx + dW + db bytes / ms_per_step"
+                               if train_parts is not None else "op event time" if world == 1 else
                                "slowest rank: its SURVEY 8(d) bytes / its ms_per_step (pipelined step)"),
             # KGX_FUSED_CU_SPLIT: the op's launches ran side by side on two CU-masked streams (main
             # kernel on 192 CUs, tail launches on 64); `achieved` divides by the op's fork-to-join event
@@ -562,13 +602,17 @@ def main() -> None:
         },
         **({"per_rank": ranks} if ranks is not None else shard_info),
     }
+    if train_parts is not None:
+        result["metric"] = "aggregated edges/sec + achieved HBM GB/s, GCNConv fwd+bwd (training step)"
+        result["training_step"] = train_parts
     if world > 1:  # self-diagnosing multi-GPU line: the process group as the library reports it
         result["distributed"] = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
                                  "rccl_version": _rccl_version() if dist.get_backend() == "nccl" else None,
                                  "exchange": shard_info.get("exchange"), "halo_chunks": shard_info.get("halo_chunks"),
                                  "merge_unit": shard_info.get("merge_unit"),
                                  "tuning_s": max((r.get("exchange_tuning_total_s") or 0.0) for r in ranks)}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and kind == "gcn" and args.config != "tiny":
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and kind == "gcn" and args.config != "tiny" \
+            and not args.train:
         log("timing the CPU baseline (oracle, C2-sized sample)")
         del x, layer, ei
         kgx.clear_cache()

@@ -364,6 +364,25 @@ int kgx_spmm_gemm_f256_ex(int reduce, const int32_t* rowptr, const int32_t* rows
                           int64_t ld_agg, kgx_stream_t stream);
 
 /* ---------------------------------------------------------------------------
+ * Weight and bias gradients of a layer out = P W + b (the fused layers'
+ * training step, kgx_dense's backward):
+ *   dW[k, m] = sum_n P[n, k] D[n, m]  (K x M, row stride ld_dw)
+ *   db[m]    = sum_n D[n, m]          (NULL: not computed)
+ * in one pass over P [N, K] and D = dOut [N, M] (row strides ldp, ldd, unit
+ * column stride).  bf16x3-split MFMA products (f32-accurate), the node sum
+ * split over row ranges and the partials added in a fixed order
+ * (deterministic).  A row range holding an inf / NaN is recomputed in plain
+ * f32 (IEEE propagation).  Workspace: kgx_gemm_tn_workspace_bytes.
+ * Replaces: the reference autograd's matmul / sum backward of
+ * gcn_conv.py:233-272 (x_j W, + bias) and of keras Dense (gin_conv.py:129-162,
+ * sage_conv.py:404-433).
+ * ------------------------------------------------------------------------- */
+int kgx_gemm_tn_workspace_bytes(int64_t N, int64_t K, int64_t M, size_t* bytes);
+int kgx_gemm_tn(int64_t N, const float* P, int64_t ldp, int64_t K, const float* D, int64_t ldd, int64_t M,
+                float* dW, int64_t ld_dw, float* db, void* workspace, size_t workspace_bytes,
+                kgx_stream_t stream);
+
+/* ---------------------------------------------------------------------------
  * Backward of the segment max / min reduction (autograd of kgx_spmm MAX/MIN).
  * torch's scatter_reduce amax/amin backward, under the reference's isinf
  * guard (aggregators.py:99-112, 151-167): grad_out[i,f] is shared evenly by

@@ -1,0 +1,270 @@
+// Weight and bias gradients of the fused layers' training step (the backward
+// of kgx_spmm_gemm's `out = bias + P W`, DESIGN.md §4 "Backward"):
+//
+//   dW[k, m] = sum_n P[n, k] D[n, m]      (P^T D, the sum over all N nodes)
+//   db[m]    = sum_n D[n, m]              (column sums of D = dOut)
+//
+// in ONE pass over P and D.  The torch path it replaces (ops._gemm_tn_tall: a
+// split-K batched fp32 GEMM, then D.sum(0) as a second pass) read D twice and
+// ran the fp32 GEMM at ~2 TB/s (NS: 5.2 ms of a 24.5 ms training step).
+//
+// Layout: the reduction runs over the node dimension n, which is the stored
+// row index of both operands, so the MFMA's K dimension is n.  For
+// v_mfma_f32_16x16x32_bf16, lane l supplies A[l % 16][8 (l / 16) + t] and
+// B[8 (l / 16) + t][l % 16], t = 0..7: eight consecutive NODES of one column.
+// Each of those eight loads is one dword per lane; across the wave it reads
+// four rows x 64 contiguous bytes, so the operands come straight from HBM in
+// MFMA order, with no LDS transpose.  Products are the bf16x3 split
+// (kgx_bf16x3.h: six bf16 products per f32 product, f32-accurate).
+//
+// Block: 256 threads, a 128 x 128 tile of dW; wave w owns rows k in
+// [64 (w >> 1), +64) and columns m in [64 (w & 1), +64): 16 MFMA tiles, 64
+// accumulator registers.  Grid: x = contiguous row ranges (split-K, ~2 blocks
+// per CU), y = dW tiles.  Each block writes its partial tile (and partial db)
+// to the workspace; gemm_tn_finish sums the partials in block order, so the
+// result is deterministic.
+//
+// Non-finite inputs: a block that loads an inf or NaN recomputes its partial
+// with plain f32 multiply-adds (IEEE propagation), the slow path.
+
+#include "kgx_bf16x3.h"
+#include "kgx_internal.h"
+
+namespace kgx {
+namespace {
+
+typedef short kgx_bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float kgx_f32x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t kgx_u32x4_t __attribute__((ext_vector_type(4)));
+
+constexpr int kTile = 128;          // dW tile edge per block
+constexpr int kTn = 256;            // threads per block (4 waves)
+constexpr int kStep = 32;           // nodes per MFMA K step
+constexpr int kPart = kTile * kTile + kTile;  // floats per partial: tile + db
+
+struct TnArgs {
+  const float* P;
+  const float* D;
+  float* part;
+  int64_t N, ldp, ldd, K, M;
+  int64_t steps;   // ceil(N / kStep)
+  int tiles_m;     // dW tiles along m
+  int with_db;
+};
+
+struct Planes {
+  kgx_bf16x8_t hi, mid, lo;
+};
+
+// eight f32 values -> three bf16x8 planes (pairs through split3_pair_rn)
+__device__ __forceinline__ Planes split8(const float (&v)[8]) {
+  kgx_u32x4_t h, m, l;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    uint32_t a, b, c;
+    split3_pair_rn(v[2 * p], v[2 * p + 1], a, b, c);
+    h[p] = a;
+    m[p] = b;
+    l[p] = c;
+  }
+  Planes r;
+  r.hi = __builtin_bit_cast(kgx_bf16x8_t, h);
+  r.mid = __builtin_bit_cast(kgx_bf16x8_t, m);
+  r.lo = __builtin_bit_cast(kgx_bf16x8_t, l);
+  return r;
+}
+
+__device__ __forceinline__ kgx_f32x4_t mfma6(const Planes& a, const Planes& b, kgx_f32x4_t acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.hi, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.mid, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.mid, b.hi, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.lo, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.lo, b.hi, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.mid, b.mid, acc, 0, 0, 0);
+  return acc;
+}
+
+__global__ __launch_bounds__(kTn, 2) void gemm_tn_kernel(TnArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = lane & 15, g = lane >> 4;
+  const int tile = blockIdx.y;
+  const int64_t k0 = int64_t(tile / a.tiles_m) * kTile + (wave >> 1) * 64;
+  const int64_t m0 = int64_t(tile % a.tiles_m) * kTile + (wave & 1) * 64;
+  const int64_t s_lo = a.steps * blockIdx.x / gridDim.x, s_hi = a.steps * (blockIdx.x + 1) / gridDim.x;
+  const bool do_db = a.with_db && k0 == 0;  // the waves of the first k half of the first tile row
+
+  // this lane's columns (clamped for the loads; masked to 0 after)
+  int64_t kc[4], mc[4];
+  bool kin[4], min_[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t k = k0 + 16 * i + c, m = m0 + 16 * i + c;
+    kin[i] = k < a.K;
+    min_[i] = m < a.M;
+    kc[i] = kin[i] ? k : a.K - 1;
+    mc[i] = min_[i] ? m : a.M - 1;
+  }
+  const bool wave_live = k0 < a.K && m0 < a.M;
+
+  kgx_f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = kgx_f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float dbs[4] = {0.f, 0.f, 0.f, 0.f};
+  int bad = 0;
+
+  for (int64_t s = s_lo; s < s_hi; ++s) {
+    const int64_t n0 = s * kStep + 8 * g;
+    float pa[4][8], db_[4][8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int64_t n = n0 + t;
+      const bool nin = n < a.N;
+      const int64_t nr = nin ? n : a.N - 1;
+      const float* prow = a.P + nr * a.ldp;
+      const float* drow = a.D + nr * a.ldd;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = prow[kc[i]], d = drow[mc[i]];
+        pa[i][t] = (nin && kin[i]) ? p : 0.0f;
+        db_[i][t] = (nin && min_[i]) ? d : 0.0f;
+      }
+    }
+    if (wave_live) {
+      // finite and split-safe (|x| < 0x1.ffp127, kgx_bf16x3.h) for every value iff the sum of |x| is
+      // below that (an inf / NaN propagates; a sum of huge finite values sends the block to the
+      // slow path too, which is only slower)
+      float sa = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) sa += fabsf(pa[i][t]) + fabsf(db_[i][t]);
+      bad |= sa < 0x1.ffp127f ? 0 : 1;
+      Planes B[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) B[j] = split8(db_[j]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const Planes A = split8(pa[i]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma6(A, B[j], acc[i][j]);
+      }
+      if (do_db) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int t = 0; t < 8; ++t) dbs[j] = __fadd_rn(dbs[j], db_[j][t]);
+      }
+    }
+  }
+
+  float* part = a.part + (int64_t(blockIdx.x) * gridDim.y + tile) * kPart;
+  const int kl0 = (wave >> 1) * 64, ml0 = (wave & 1) * 64;
+  if (__syncthreads_or(bad)) {
+    // slow path: this block's rows in plain f32, one thread per (k, m) pair in turn
+    for (int o = threadIdx.x; o < kTile * kTile; o += kTn) {
+      const int64_t k = int64_t(tile / a.tiles_m) * kTile + o / kTile;
+      const int64_t m = int64_t(tile % a.tiles_m) * kTile + o % kTile;
+      float s = 0.0f;
+      if (k < a.K && m < a.M)
+        for (int64_t n = s_lo * kStep; n < s_hi * kStep && n < a.N; ++n)
+          s = __fadd_rn(s, __fmul_rn(a.P[n * a.ldp + k], a.D[n * a.ldd + m]));
+      part[o] = s;
+    }
+    if (a.with_db && tile / a.tiles_m == 0)
+      for (int o = threadIdx.x; o < kTile; o += kTn) {
+        const int64_t m = int64_t(tile % a.tiles_m) * kTile + o;
+        float s = 0.0f;
+        if (m < a.M)
+          for (int64_t n = s_lo * kStep; n < s_hi * kStep && n < a.N; ++n) s = __fadd_rn(s, a.D[n * a.ldd + m]);
+        part[kTile * kTile + o] = s;
+      }
+    return;
+  }
+  // accumulator (i, j): rows kl0 + 16 i + 4 g + r, column ml0 + 16 j + c
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) part[(kl0 + 16 * i + 4 * g + r) * kTile + ml0 + 16 * j + c] = acc[i][j][r];
+  if (do_db) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v = dbs[j];
+      v = __fadd_rn(v, __shfl_xor(v, 16, 64));
+      v = __fadd_rn(v, __shfl_xor(v, 32, 64));
+      if (g == 0) part[kTile * kTile + ml0 + 16 * j + c] = v;
+    }
+  }
+}
+
+// dW[k, m] = sum over blocks b (in order) of part[b][tile(k, m)][k % 128][m % 128]; db likewise
+__global__ void gemm_tn_finish_kernel(const float* __restrict__ part, int nb, int tiles, int tiles_m, int64_t K,
+                                      int64_t M, float* __restrict__ dW, int64_t ld_dw, float* __restrict__ db) {
+  const int64_t o = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t n_w = K * M;
+  if (o < n_w) {
+    const int64_t k = o / M, m = o % M;
+    const int tile = int(k / kTile) * tiles_m + int(m / kTile);
+    const int64_t off = (k % kTile) * kTile + (m % kTile);
+    float s = 0.0f;
+    for (int b = 0; b < nb; ++b) s = __fadd_rn(s, part[(int64_t(b) * tiles + tile) * kPart + off]);
+    dW[k * ld_dw + m] = s;
+  } else if (db && o < n_w + M) {
+    const int64_t m = o - n_w;
+    const int tile = int(m / kTile);  // tile row 0
+    float s = 0.0f;
+    for (int b = 0; b < nb; ++b) s = __fadd_rn(s, part[(int64_t(b) * tiles + tile) * kPart + kTile * kTile + m % kTile]);
+    db[m] = s;
+  }
+}
+
+int gemm_tn_blocks(int64_t N) {
+  const int64_t steps = (N + kStep - 1) / kStep;
+  const int64_t want = int64_t(2) * cu_count();
+  return int(steps < want ? (steps > 0 ? steps : 1) : want);
+}
+
+}  // namespace
+}  // namespace kgx
+
+using namespace kgx;
+
+extern "C" int kgx_gemm_tn_workspace_bytes(int64_t N, int64_t K, int64_t M, size_t* bytes) {
+  KGX_REQUIRE(bytes && N >= 0 && K > 0 && M > 0, KGX_ERR_ARG, "kgx_gemm_tn_workspace_bytes: bad arguments");
+  const int64_t tiles = ((K + kTile - 1) / kTile) * ((M + kTile - 1) / kTile);
+  *bytes = size_t(gemm_tn_blocks(N)) * size_t(tiles) * kPart * sizeof(float);
+  return KGX_OK;
+}
+
+extern "C" int kgx_gemm_tn(int64_t N, const float* P, int64_t ldp, int64_t K, const float* D, int64_t ldd, int64_t M,
+                           float* dW, int64_t ld_dw, float* db, void* workspace, size_t workspace_bytes,
+                           kgx_stream_t stream_) {
+  KGX_REQUIRE(N >= 0 && K > 0 && M > 0 && ldp >= K && ldd >= M && ld_dw >= M, KGX_ERR_ARG,
+              "kgx_gemm_tn: bad shapes (N=%lld K=%lld M=%lld ldp=%lld ldd=%lld ld_dw=%lld)", (long long)N,
+              (long long)K, (long long)M, (long long)ldp, (long long)ldd, (long long)ld_dw);
+  KGX_REQUIRE(dW && (N == 0 || (P && D)), KGX_ERR_ARG, "kgx_gemm_tn: null pointer");
+  size_t need = 0;
+  (void)kgx_gemm_tn_workspace_bytes(N, K, M, &need);
+  KGX_REQUIRE(workspace && workspace_bytes >= need, KGX_ERR_ARG, "kgx_gemm_tn: workspace %zu < %zu bytes",
+              workspace_bytes, need);
+  hipStream_t s = as_stream(stream_);
+  const int tiles_m = int((M + kTile - 1) / kTile);
+  const int tiles = int((K + kTile - 1) / kTile) * tiles_m;
+  const int nb = gemm_tn_blocks(N);
+  if (N > 0) {
+    TnArgs a{P, D, static_cast<float*>(workspace), N, ldp, ldd, K, M, (N + kStep - 1) / kStep, tiles_m, db ? 1 : 0};
+    hipLaunchKernelGGL(gemm_tn_kernel, dim3(nb, tiles), dim3(kTn), 0, s, a);
+    KGX_CHECK_LAUNCH();
+  } else {
+    KGX_CHECK_HIP(hipMemsetAsync(workspace, 0, need, s));
+  }
+  const int64_t outs = K * M + (db ? M : 0);
+  hipLaunchKernelGGL(gemm_tn_finish_kernel, dim3(unsigned((outs + 255) / 256)), dim3(256), 0, s,
+                     static_cast<const float*>(workspace), nb, tiles, tiles_m, K, M, dW, ld_dw, db);
+  KGX_CHECK_LAUNCH();
+  return KGX_OK;
+}

@@ -206,8 +206,9 @@ def _inference_only(layer: Layer, weights) -> None:
     under no_grad, so an output would carry no gradient to the weights."""
     if torch.is_grad_enabled() and any(p.requires_grad for p in weights):
         raise NotImplementedError(
-            f"{type(layer).__name__} is inference-only: call it under torch.no_grad() (or freeze its weights); "
-            "training runs on the single-GPU layers and on ShardedGCNConv")
+            f"{type(layer).__name__} is inference-only here: call it under torch.no_grad() (or freeze its "
+            "weights); training runs on the single-GPU layers, ShardedGCNConv, and ShardedGINConv / "
+            "ShardedSAGEConv with a sum or mean aggregator")
 
 
 # where progress and heartbeat lines go (stderr; tests substitute a buffer)
@@ -1647,6 +1648,44 @@ class _ShardedGCNFn(torch.autograd.Function):
         return dx, dW, db, None
 
 
+class _ShardedAggFn(torch.autograd.Function):
+    """AGG_j x_j over a shard, sum or mean of the plain message x_j, with
+    gradients: the neighbour reduction of GINConv and SAGEConv on the
+    reference's model.fit path (tests/performance/test_large_graphs.py:341-357;
+    gin_conv.py:216-225, sage_conv.py:404-439), whose node update then trains
+    through torch autograd on the shard's own rows.
+
+    forward:  table = [x_local | pulled halo x] (halo_exchange); agg = the shard
+              CSR's row sums in each row's global input order (ShardedGraph.
+              propagate), mean = sum / max(fp32 in-degree, 1e-8)
+              (aggregators.py:56-85).
+    backward: mean: dagg / count; G = A_shard^T dagg over the shard's sources
+              (graph.transpose: own rows and halo rows); the halo rows' G goes
+              back to their owners (reverse_halo_exchange, the forward
+              all-to-all with the splits swapped) and is added to their own G."""
+
+    @staticmethod
+    def forward(ctx, x_local, sg, reduce):
+        with torch.no_grad():
+            agg = sg.propagate(x_local.contiguous(), reduce)
+        ctx.sg, ctx.reduce = sg, reduce
+        return agg
+
+    @staticmethod
+    def backward(ctx, dagg):
+        sg = ctx.sg
+        d = dagg.contiguous()
+        if ctx.reduce == "mean":
+            count = torch.clamp(sg.graph.deg[: sg.n_local].to(torch.float32), min=1e-8)
+            d = d / count.unsqueeze(1)
+        g_src = sg.backend.aggregate_transposed(sg.graph, d.contiguous(), weighted=False)
+        return sg.reverse_halo_exchange(g_src), None, None
+
+
+def _training(weights, x_local: torch.Tensor) -> bool:
+    return torch.is_grad_enabled() and (x_local.requires_grad or any(p.requires_grad for p in weights))
+
+
 def use_merged_halo() -> bool:
     """The default GCN path merges the first halo step into its rows' pass
     (KGX_HALO_MERGED=0: the round-2 own pass + accumulating chunk passes)."""
@@ -1672,7 +1711,19 @@ class _ShardedWrap(Layer):
         with torch.no_grad():
             for p in self.conv.weights:
                 self.sg.comm.broadcast(p.data, src=0)
+        if self.sg.world > 1:
+            # training: a weight's gradient from this rank's rows is a partial sum; every
+            # rank gets the sum over all ranks (as ShardedGCNConv's dW / db), so the same
+            # optimizer step keeps the broadcast weights identical everywhere
+            for p in self.conv.weights:
+                if p.requires_grad:
+                    p.register_hook(self._all_reduce_grad)
         self.built = True
+
+    def _all_reduce_grad(self, grad: torch.Tensor) -> torch.Tensor:
+        g = grad.detach().clone().contiguous()
+        self.sg.comm.all_reduce(g)
+        return g
 
     def _pipelined(self) -> bool:
         """Whether the forward takes the pipelined (exchange-overlapped) sum / mean path."""
@@ -1714,7 +1765,15 @@ class ShardedGINConv(_ShardedWrap):
 
     def forward(self, x_local: torch.Tensor, training=None) -> torch.Tensor:
         self._ensure_built(x_local)
-        _inference_only(self, self.conv.weights)
+        conv = self.conv
+        if _training(conv.weights, x_local) and conv.aggregator in ("sum", "mean"):
+            # training (sum / mean): the aggregation through _ShardedAggFn, (1+eps) x_i +
+            # aggr and the MLP through torch autograd (gin_conv.py:216-225)
+            agg = _ShardedAggFn.apply(x_local, self.sg, conv.aggregator)
+            scale = (1 + conv.eps) if conv.train_eps else torch.tensor(float(conv._scale()), dtype=torch.float32,
+                                                                        device=x_local.device)
+            return conv.mlp(scale * x_local + agg, training=training)
+        _inference_only(self, conv.weights)
         self._maybe_tune(x_local.contiguous())
         return self._forward_impl(x_local, training)
 
@@ -1861,7 +1920,16 @@ class ShardedSAGEConv(_ShardedWrap):
 
     def forward(self, x_local: torch.Tensor, training=None) -> torch.Tensor:
         self._ensure_built(x_local)
-        _inference_only(self, self.conv.weights)
+        conv = self.conv
+        if _training(conv.weights, x_local) and conv.actual_aggregator in ("sum", "mean"):
+            if training and conv.dropout_rate > 0:
+                raise NotImplementedError("ShardedSAGEConv: training with message dropout runs on the single-GPU "
+                                          "SAGEConv (sage_conv.py:280-298 masks every message)")
+            # training (sum / mean): the aggregation through _ShardedAggFn, lin_neigh(aggr) +
+            # lin_self(x) + b, activation and L2 norm through torch autograd (sage_conv.py:404-439)
+            agg = _ShardedAggFn.apply(x_local, self.sg, conv.actual_aggregator)
+            return conv.update_nodes(x_local, agg)
+        _inference_only(self, conv.weights)
         self._maybe_tune(x_local.contiguous())
         return self._forward_impl(x_local, training)
 

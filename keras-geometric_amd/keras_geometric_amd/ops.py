@@ -11,6 +11,7 @@ torch.compile / symbolic tracing sees shapes without running the GPU.
 
 from __future__ import annotations
 
+import ctypes
 import os
 import threading
 from typing import Optional
@@ -882,20 +883,29 @@ def _aggregate_transform_raw(g, x, W, red, weighted, bias, pre_gin, gin_scale, e
     ))
 
 
-def _gemm_tn_tall(P: torch.Tensor, D: torch.Tensor, chunks: int = 512) -> torch.Tensor:
-    """P^T @ D for tall-skinny P [K, m], D [K, n] (K = number of nodes): split-K
-    as a batched GEMM over row chunks plus one sum, so every CU gets work
-    (a single GEMM with M = N = 128 and K = 10M runs on a handful of tiles)."""
-    K = P.shape[0]
-    if K < 8 * chunks:
-        return P.t() @ D
-    kc = K // chunks
-    main = kc * chunks
-    out = torch.bmm(P[:main].view(chunks, kc, P.shape[1]).transpose(1, 2), D[:main].view(chunks, kc, D.shape[1]))
-    out = out.sum(0)
-    if main < K:
-        out = out + P[main:].t() @ D[main:]
-    return out
+def gemm_tn(P: torch.Tensor, D: torch.Tensor, with_db: bool = False):
+    """(P^T D, column sums of D or None) in one pass over P and D (kgx_gemm_tn:
+    the bf16x3-split MFMA product over the node dimension, split-K over row
+    ranges with partials summed in block order) -- the weight and bias
+    gradients of a layer out = P W + b.  Device tensors only (the product path
+    has no CPU fallback)."""
+    P = P if P.stride(-1) == 1 else P.contiguous()
+    D = D if D.stride(-1) == 1 else D.contiguous()
+    dev = nat.require_device(P, D)
+    if P.dtype != torch.float32 or D.dtype != torch.float32 or P.dim() != 2 or D.dim() != 2 or P.shape[0] != D.shape[0]:
+        raise ValueError(f"gemm_tn: float32 [N, K] and [N, M] expected (got {tuple(P.shape)}, {tuple(D.shape)})")
+    N, K, M = P.shape[0], P.shape[1], D.shape[1]
+    dW = torch.empty((K, M), dtype=torch.float32, device=dev)
+    db = torch.empty(M, dtype=torch.float32, device=dev) if with_db else None
+    if K == 0 or M == 0:
+        return dW, (db.zero_() if db is not None else None)
+    L = nat.lib()
+    nbytes = ctypes.c_size_t(0)
+    nat.check(L.kgx_gemm_tn_workspace_bytes(N, K, M, ctypes.byref(nbytes)), "kgx_gemm_tn_workspace_bytes")
+    ws = torch.empty(max(nbytes.value, 4), dtype=torch.uint8, device=dev)
+    nat.check(L.kgx_gemm_tn(N, nat.ptr(P), P.stride(0), K, nat.ptr(D), D.stride(0), M, nat.ptr(dW), M, nat.ptr(db),
+                            nat.ptr(ws), nbytes.value, nat.stream(dev)), "kgx_gemm_tn")
+    return dW, db
 
 
 class _AggregateTransformFn(torch.autograd.Function):
@@ -926,9 +936,9 @@ class _AggregateTransformFn(torch.autograd.Function):
         x, W, P = ctx.saved_tensors
         grad_out = grad_out.contiguous()
         g_x = g_W = g_b = None
-        if ctx.needs_input_grad[1]:
-            g_W = _gemm_tn_tall(P, grad_out)
-        if ctx.needs_input_grad[2]:
+        if ctx.needs_input_grad[1]:  # dW = P^T dOut and db = colsum(dOut) in one pass (kgx_gemm_tn)
+            g_W, g_b = gemm_tn(P, grad_out, with_db=ctx.needs_input_grad[2])
+        elif ctx.needs_input_grad[2]:
             g_b = grad_out.sum(0)
         if ctx.needs_input_grad[0]:
             f_out, f_in = W.shape[1], W.shape[0]
@@ -1170,13 +1180,13 @@ class _DenseFn(torch.autograd.Function):
         g = [None] * 6
         if ctx.needs_input_grad[0]:
             g[0] = _matmul_t(dz, W0)
-        if ctx.needs_input_grad[1]:
-            g[1] = _gemm_tn_tall(x0, dz)
+        if ctx.needs_input_grad[1]:  # dW0 = x0^T dz (+ db = colsum(dz) in the same pass, kgx_gemm_tn)
+            g[1], g[4] = gemm_tn(x0, dz, with_db=ctx.needs_input_grad[4])
         if x1 is not None and ctx.needs_input_grad[2]:
             g[2] = _matmul_t(dz, W1)
         if x1 is not None and ctx.needs_input_grad[3]:
-            g[3] = _gemm_tn_tall(x1, dz)
-        if ctx.needs_input_grad[4]:
+            g[3], _ = gemm_tn(x1, dz)
+        if ctx.needs_input_grad[4] and g[4] is None:
             g[4] = dz.sum(0)
         return tuple(g)
 

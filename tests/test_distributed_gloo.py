@@ -903,3 +903,89 @@ def test_chunk_slice_bounds():
                 if first is not None and K > 1:
                     assert cuts[0][1] == int(count * first)
     assert kd.chunk_slice(10, 1, 4) == (2, 5)
+
+
+def _train_gin_sage_worker(rank, world, port, q):
+    """ShardedGINConv (sum, trainable eps) and ShardedSAGEConv (mean, L2 norm) with
+    gradients: _ShardedAggFn over the pulled halo table, the node update through
+    torch autograd, weight gradients all-reduced by the layers' hooks."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        s, d, x, _, _ = _graph()
+        bounds = kd.equal_bounds(N, world)
+        lo, hi = bounds[rank], bounds[rank + 1]
+        keep = (d >= lo) & (d < hi)
+        sg = kd.ShardedGraph.build(torch.from_numpy(s[keep]), torch.from_numpy(d[keep]), bounds,
+                                   backend=OracleBackend(), n_features=F_IN, self_loops=False, gcn_norm=False,
+                                   halo_chunks=2)
+        r = torch.from_numpy(np.random.default_rng(5).standard_normal((N, F_OUT)).astype(np.float32))[lo:hi]
+        out = []
+        for layer in (kd.ShardedGINConv(F_OUT, sg, mlp_hidden=[12], aggregator="sum", eps_init=0.25, train_eps=True),
+                      kd.ShardedGINConv(F_OUT, sg, aggregator="mean"),
+                      kd.ShardedSAGEConv(F_OUT, sg, aggregator="mean", normalize=True),
+                      kd.ShardedSAGEConv(F_OUT, sg, aggregator="sum")):
+            xl = torch.from_numpy(x[lo:hi]).clone()
+            layer._ensure_built(xl)
+            xg = xl.clone().requires_grad_(True)
+            y = layer(xg)
+            (y * r).sum().backward()
+            weights = [p.detach().numpy().copy() for p in layer.conv.weights]
+            grads = [p.grad.numpy().copy() for p in layer.conv.weights]
+            out.append((y.detach().numpy(), xg.grad.numpy(), weights, grads))
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_sharded_gin_sage_backward():
+    """Sharded GINConv (sum with trainable eps; mean) and SAGEConv (mean + L2
+    norm; sum) training steps at world 2 against torch autograd through the
+    oracle's whole-graph forwards (gin_conv.py:216-225, sage_conv.py:404-439):
+    output and dX within 1e-5 of max(1, |ref|); every weight gradient (eps
+    included) all-reduced -- the same on both ranks -- and within sqrt(N) * 1e-5
+    of the reference's (sums over all rows)."""
+    if torch.cuda.is_initialized():
+        pytest.skip("never start processes from a process that has initialised the GPU")
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_train_gin_sage_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    s, d, x, _, _ = _graph()
+    EI = torch.from_numpy(np.stack([s, d]))
+    rr = torch.from_numpy(np.random.default_rng(5).standard_normal((N, F_OUT)).astype(np.float32))
+
+    def close(got, ref, tol):
+        err = np.abs(got - ref) / np.maximum(1.0, np.abs(ref))
+        assert err.max() <= tol, err.max()
+
+    for i in range(4):
+        y0, _, w0, g0 = res[0][i]
+        for r in range(1, world):
+            for a, b in zip(w0, res[r][i][2]):  # broadcast weights
+                np.testing.assert_array_equal(a, b)
+            for a, b in zip(g0, res[r][i][3]):  # all-reduced gradients
+                np.testing.assert_array_equal(a, b)
+        X = torch.from_numpy(x).clone().requires_grad_(True)
+        w = [torch.from_numpy(a).clone().requires_grad_(True) for a in w0]
+        if i == 0:  # weights: eps, hidden kernel, bias, output kernel, bias
+            ref = R.gin_forward(X, EI, [(w[1], w[2], "relu"), (w[3], w[4], None)], "sum", eps_tensor=w[0])
+        elif i == 1:
+            ref = R.gin_forward(X, EI, [(w[0], w[1], None)], "mean")
+        elif i == 2:  # SAGE weights: bias, lin_neigh, lin_self
+            ref = R.sage_forward(X, EI, w[1], w[2], w[0], "mean", normalize=True)
+        else:
+            ref = R.sage_forward(X, EI, w[1], w[2], w[0], "sum")
+        (ref * rr).sum().backward()
+        close(np.concatenate([res[r][i][0] for r in range(world)]), ref.detach().numpy(), 1e-5)
+        close(np.concatenate([res[r][i][1] for r in range(world)]), X.grad.numpy(), 1e-5)
+        for got, wt in zip(g0, w):
+            close(got, wt.grad.numpy(), 1e-5 * np.sqrt(N))
