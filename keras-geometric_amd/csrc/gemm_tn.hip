@@ -12,15 +12,18 @@
 // row index of both operands, so the MFMA's K dimension is n.  For
 // v_mfma_f32_16x16x32_bf16, lane l supplies A[l % 16][8 (l / 16) + t] and
 // B[8 (l / 16) + t][l % 16], t = 0..7: eight consecutive NODES of one column.
-// Each of those eight loads is one dword per lane; across the wave it reads
-// four rows x 64 contiguous bytes, so the operands come straight from HBM in
-// MFMA order, with no LDS transpose.  Products are the bf16x3 split
+// A lane loads float4 pieces of eight rows (four columns each); element e of
+// every lane's pieces is the operand of MFMA e, whose 16 output rows are then
+// every fourth column -- so the operands come straight from HBM in 1-KB
+// coalesced loads, with no LDS transpose, and the stores unscramble the
+// columns.  Products are the bf16x3 split
 // (kgx_bf16x3.h: six bf16 products per f32 product, f32-accurate).
 //
 // Block: 256 threads, a 128 x 128 tile of dW; wave w owns rows k in
 // [64 (w >> 1), +64) and columns m in [64 (w & 1), +64): 16 MFMA tiles, 64
-// accumulator registers.  Grid: x = contiguous row ranges (split-K, ~2 blocks
-// per CU), y = dW tiles.  Each block writes its partial tile (and partial db)
+// accumulator registers, plus three steps' operand values (this step's, and
+// the next two steps' loads in flight): one wave per SIMD.  Grid: x = contiguous
+// row ranges (split-K, one block per CU), y = dW tiles.  Each block writes its partial tile (and partial db)
 // to the workspace; gemm_tn_finish sums the partials in block order, so the
 // result is deterministic.
 //
@@ -39,7 +42,7 @@ typedef uint32_t kgx_u32x4_t __attribute__((ext_vector_type(4)));
 
 constexpr int kTile = 128;          // dW tile edge per block
 constexpr int kTn = 256;            // threads per block (4 waves)
-constexpr int kStep = 32;           // nodes per MFMA K step
+constexpr int kStep = 32;           // nodes per MFMA K step (8 per lane group)
 constexpr int kPart = kTile * kTile + kTile;  // floats per partial: tile + db
 
 struct TnArgs {
@@ -84,7 +87,45 @@ __device__ __forceinline__ kgx_f32x4_t mfma6(const Planes& a, const Planes& b, k
   return acc;
 }
 
-__global__ __launch_bounds__(kTn, 2) void gemm_tn_kernel(TnArgs a) {
+// One step's operand values per lane: for nodes n = 32 s + 8 g + t (t = 0..7),
+// P[n][k0 + 4 c .. +3] and D[n][m0 + 4 c .. +3] as float4 -- 16 dwordx4 loads
+// per lane, each instruction reading four rows x 256 contiguous bytes.  Buffer
+// loads through a per-step descriptor: rows past N fall outside its record
+// count and column groups past K / M get an out-of-range offset, so both read
+// as 0 with no branch -- every load is unconditional and the next step's
+// loads stay in flight across this step's MFMAs.
+//
+// Element e of lane c's float4 is column 4 c + e: MFMA e of a k (or m) block
+// takes element e of every lane, so its 16 output rows are the columns
+// k0 + 4 c + e, c = 0..15 (a strided set; the store unscrambles it).
+typedef float kgx_f32x4v_t __attribute__((ext_vector_type(4)));
+
+struct StepVals {
+  kgx_f32x4v_t p[8], d[8];
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t step_rsrc(const float* base, int64_t ld, int64_t s, int64_t N) {
+  const int64_t r0 = s * kStep;
+  int64_t rows = N - r0;
+  rows = rows > kStep ? kStep : (rows < 0 ? 0 : rows);
+  const uint64_t addr = reinterpret_cast<uint64_t>(base) + uint64_t(r0 * ld * 4);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(addr));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(addr >> 32));
+  const int bytes = __builtin_amdgcn_readfirstlane(int(rows * ld * 4));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((uint64_t(hi) << 32) | lo), 0, bytes, 0x00020000);
+}
+
+__device__ __forceinline__ void load_step(StepVals& v, const TnArgs& a, int64_t s, uint32_t po, uint32_t dof) {
+  const auto rp = step_rsrc(a.P, a.ldp, s, a.N);
+  const auto rd = step_rsrc(a.D, a.ldd, s, a.N);
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    v.p[t] = __builtin_bit_cast(kgx_f32x4v_t, __builtin_amdgcn_raw_buffer_load_b128(rp, po, int(t * a.ldp * 4), 0));
+    v.d[t] = __builtin_bit_cast(kgx_f32x4v_t, __builtin_amdgcn_raw_buffer_load_b128(rd, dof, int(t * a.ldd * 4), 0));
+  }
+}
+
+__global__ __launch_bounds__(kTn, 1) void gemm_tn_kernel(TnArgs a) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c = lane & 15, g = lane >> 4;
@@ -94,17 +135,11 @@ __global__ __launch_bounds__(kTn, 2) void gemm_tn_kernel(TnArgs a) {
   const int64_t s_lo = a.steps * blockIdx.x / gridDim.x, s_hi = a.steps * (blockIdx.x + 1) / gridDim.x;
   const bool do_db = a.with_db && k0 == 0;  // the waves of the first k half of the first tile row
 
-  // this lane's columns (clamped for the loads; masked to 0 after)
-  int64_t kc[4], mc[4];
-  bool kin[4], min_[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int64_t k = k0 + 16 * i + c, m = m0 + 16 * i + c;
-    kin[i] = k < a.K;
-    min_[i] = m < a.M;
-    kc[i] = kin[i] ? k : a.K - 1;
-    mc[i] = min_[i] ? m : a.M - 1;
-  }
+  // this lane's byte offsets within a step (row 8 g, columns 4 c .. 4 c + 3 of the wave's
+  // 64); column groups past K / M get an offset past every record count (K, M % 4 == 0)
+  const int64_t kq = k0 + 4 * c, mq = m0 + 4 * c;
+  const uint32_t po = kq < a.K ? uint32_t((8 * g * a.ldp + kq) * 4) : 0x80000000u;
+  const uint32_t dof = mq < a.M ? uint32_t((8 * g * a.ldd + mq) * 4) : 0x80000000u;
   const bool wave_live = k0 < a.K && m0 < a.M;
 
   kgx_f32x4_t acc[4][4];
@@ -115,49 +150,59 @@ __global__ __launch_bounds__(kTn, 2) void gemm_tn_kernel(TnArgs a) {
   float dbs[4] = {0.f, 0.f, 0.f, 0.f};
   int bad = 0;
 
-  for (int64_t s = s_lo; s < s_hi; ++s) {
-    const int64_t n0 = s * kStep + 8 * g;
-    float pa[4][8], db_[4][8];
+  auto compute = [&](const StepVals& v) {
+    if (!wave_live) return;
+    // finite and split-safe (|x| < 0x1.ffp127, kgx_bf16x3.h) for every value iff the sum of |x| is
+    // below that (an inf / NaN propagates; a sum of huge finite values sends the block to the slow
+    // path too, which is only slower)
+    float sa = 0.0f;
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const int64_t n = n0 + t;
-      const bool nin = n < a.N;
-      const int64_t nr = nin ? n : a.N - 1;
-      const float* prow = a.P + nr * a.ldp;
-      const float* drow = a.D + nr * a.ldd;
+    for (int t = 0; t < 8; ++t)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float p = prow[kc[i]], d = drow[mc[i]];
-        pa[i][t] = (nin && kin[i]) ? p : 0.0f;
-        db_[i][t] = (nin && min_[i]) ? d : 0.0f;
-      }
+      for (int e = 0; e < 4; ++e) sa += fabsf(v.p[t][e]) + fabsf(v.d[t][e]);
+    bad |= sa < 0x1.ffp127f ? 0 : 1;
+    Planes B[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float col[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) col[t] = v.d[t][j];
+      B[j] = split8(col);
     }
-    if (wave_live) {
-      // finite and split-safe (|x| < 0x1.ffp127, kgx_bf16x3.h) for every value iff the sum of |x| is
-      // below that (an inf / NaN propagates; a sum of huge finite values sends the block to the
-      // slow path too, which is only slower)
-      float sa = 0.0f;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i) {
+      float col[8];
 #pragma unroll
-        for (int t = 0; t < 8; ++t) sa += fabsf(pa[i][t]) + fabsf(db_[i][t]);
-      bad |= sa < 0x1.ffp127f ? 0 : 1;
-      Planes B[4];
+      for (int t = 0; t < 8; ++t) col[t] = v.p[t][i];
+      const Planes A = split8(col);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) B[j] = split8(db_[j]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const Planes A = split8(pa[i]);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma6(A, B[j], acc[i][j]);
-      }
-      if (do_db) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int t = 0; t < 8; ++t) dbs[j] = __fadd_rn(dbs[j], db_[j][t]);
-      }
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma6(A, B[j], acc[i][j]);
     }
+    if (do_db) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) dbs[j] = __fadd_rn(dbs[j], v.d[t][j]);
+    }
+  };
+
+  // Three register sets in turn: step s's values are consumed while the loads of steps s + 1
+  // and s + 2 are in flight (32 KB per wave, 128 KB per CU).  Every load is unconditional (a step
+  // past the block's range is valid memory or reads 0), so the count of loads issued after a
+  // set's loads is the same on every path and the compiler's waits before its use stay partial
+  // (vmcnt(32)).
+  StepVals v0, v1, v2;
+  load_step(v0, a, s_lo, po, dof);
+  load_step(v1, a, s_lo + 1, po, dof);
+  for (int64_t s = s_lo; s < s_hi; s += 3) {
+    load_step(v2, a, s + 2, po, dof);
+    compute(v0);
+    if (s + 1 >= s_hi) break;
+    load_step(v0, a, s + 3, po, dof);
+    compute(v1);
+    if (s + 2 >= s_hi) break;
+    load_step(v1, a, s + 4, po, dof);
+    compute(v2);
   }
 
   float* part = a.part + (int64_t(blockIdx.x) * gridDim.y + tile) * kPart;
@@ -183,20 +228,21 @@ __global__ __launch_bounds__(kTn, 2) void gemm_tn_kernel(TnArgs a) {
       }
     return;
   }
-  // accumulator (i, j): rows kl0 + 16 i + 4 g + r, column ml0 + 16 j + c
+  // accumulator (i, j), element r: MFMA row 4 g + r = column k0 + 4 (4 g + r) + i of P, MFMA
+  // column c = column m0 + 4 c + j of D
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) part[(kl0 + 16 * i + 4 * g + r) * kTile + ml0 + 16 * j + c] = acc[i][j][r];
+      for (int r = 0; r < 4; ++r) part[(kl0 + 4 * (4 * g + r) + i) * kTile + ml0 + 4 * c + j] = acc[i][j][r];
   if (do_db) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float v = dbs[j];
       v = __fadd_rn(v, __shfl_xor(v, 16, 64));
       v = __fadd_rn(v, __shfl_xor(v, 32, 64));
-      if (g == 0) part[kTile * kTile + ml0 + 16 * j + c] = v;
+      if (g == 0) part[kTile * kTile + ml0 + 4 * c + j] = v;
     }
   }
 }
@@ -224,7 +270,7 @@ __global__ void gemm_tn_finish_kernel(const float* __restrict__ part, int nb, in
 
 int gemm_tn_blocks(int64_t N) {
   const int64_t steps = (N + kStep - 1) / kStep;
-  const int64_t want = int64_t(2) * cu_count();
+  const int64_t want = cu_count();
   return int(steps < want ? (steps > 0 ? steps : 1) : want);
 }
 

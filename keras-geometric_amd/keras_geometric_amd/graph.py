@@ -16,6 +16,7 @@ import os
 from collections import OrderedDict
 from dataclasses import dataclass, field
 
+import numpy as np
 import torch
 
 from . import _native as nat
@@ -399,9 +400,28 @@ _CACHE: "OrderedDict[tuple, tuple[torch.Tensor, CSRGraph]]" = OrderedDict()
 _CACHE_SIZE = int(os.environ.get("KGX_GRAPH_CACHE", "8"))
 
 
+def host_array_key(a) -> tuple | None:
+    """Key of a host (numpy) edge_index.  The reference casts edge_index once
+    and caches the cast by id() (message_passing.py:256-268); here the key is
+    the id, the data address, shape, strides and dtype, plus a fingerprint of
+    4096 evenly spaced elements, so an array modified in place in the sampled
+    positions is not served stale (the reference would).  The cache entry
+    holds a reference to the array, so its id cannot be reused while cached.
+    None for anything that is not an ndarray (a list becomes a new array on
+    every call: nothing to key on)."""
+    if not isinstance(a, np.ndarray):
+        return None
+    n = a.size
+    pick = np.linspace(0, n - 1, min(n, 4096)).astype(np.int64) if n else np.zeros(0, np.int64)
+    sample = np.ascontiguousarray(a.flat[pick])
+    return ("host", id(a), a.__array_interface__["data"][0], a.shape, a.strides, a.dtype.str,
+            hash(sample.tobytes()))
+
+
 def cache_key(edge_index: torch.Tensor, *extra) -> tuple | None:
     if not isinstance(edge_index, torch.Tensor):
-        return None
+        hk = host_array_key(edge_index)
+        return (*hk, *extra) if hk is not None else None
     return (
         edge_index.data_ptr(), edge_index._version, tuple(edge_index.shape), tuple(edge_index.stride()),
         edge_index.dtype, str(edge_index.device), *extra,
@@ -424,3 +444,6 @@ def cached(key: tuple | None, anchor, builder) -> CSRGraph:
 
 def clear_cache() -> None:
     _CACHE.clear()
+    from .layers import _edges
+
+    _edges._HOST_CAST.clear()

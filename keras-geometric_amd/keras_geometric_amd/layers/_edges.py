@@ -2,6 +2,8 @@
 
 from __future__ import annotations
 
+from collections import OrderedDict
+
 import numpy as np
 import torch
 
@@ -9,10 +11,33 @@ from .. import graph as G
 from .base import default_device
 
 
+_HOST_CAST: "OrderedDict[tuple, tuple]" = OrderedDict()  # host edge_index -> (the array, its device copy)
+_HOST_CAST_SIZE = 4
+
+
 def edge_index_tensor(edge_index, device: torch.device | None, *, allow_transpose: bool) -> torch.Tensor:
     """Cast to int32 [2,E] on `device` (reference: ops.cast(edge_index,"int32"),
     message_passing.py:265 / gcn_conv.py:307; [E,2] transposed for the layers
-    that accept it, gcn_conv.py:309-318, sage_conv.py:384-393)."""
+    that accept it, gcn_conv.py:309-318, sage_conv.py:384-393).  A numpy
+    edge_index's device copy is cached like the reference's cast
+    (message_passing.py:256-268; graph.host_array_key), so a reference-style
+    caller passing the same array every step pays the host-to-device copy once."""
+    hk = G.host_array_key(edge_index)
+    if hk is not None:
+        key = (*hk, str(device), allow_transpose)
+        hit = _HOST_CAST.get(key)
+        if hit is not None:
+            _HOST_CAST.move_to_end(key)
+            return hit[1]
+        ei = _edge_index_tensor(edge_index, device, allow_transpose=allow_transpose)
+        _HOST_CAST[key] = (edge_index, ei)
+        while len(_HOST_CAST) > _HOST_CAST_SIZE:
+            _HOST_CAST.popitem(last=False)
+        return ei
+    return _edge_index_tensor(edge_index, device, allow_transpose=allow_transpose)
+
+
+def _edge_index_tensor(edge_index, device: torch.device | None, *, allow_transpose: bool) -> torch.Tensor:
     if isinstance(edge_index, torch.Tensor):
         ei = edge_index
         if ei.device.type != "cuda":

@@ -936,8 +936,20 @@ class _AggregateTransformFn(torch.autograd.Function):
         x, W, P = ctx.saved_tensors
         grad_out = grad_out.contiguous()
         g_x = g_W = g_b = None
+        side = None
         if ctx.needs_input_grad[1]:  # dW = P^T dOut and db = colsum(dOut) in one pass (kgx_gemm_tn)
-            g_W, g_b = gemm_tn(P, grad_out, with_db=ctx.needs_input_grad[2])
+            if ctx.needs_input_grad[0] and grad_out.is_cuda and _tn_overlap():
+                # on a side stream, beside the dx pass below: the dx op is gather-bound with its
+                # matrix cores mostly idle, kgx_gemm_tn streams P and dOut once through them
+                side = _side_stream(grad_out.device)
+                cur = torch.cuda.current_stream(grad_out.device)
+                side.wait_stream(cur)
+                with torch.cuda.stream(side):
+                    g_W, g_b = gemm_tn(P, grad_out, with_db=ctx.needs_input_grad[2])
+                P.record_stream(side)
+                grad_out.record_stream(side)
+            else:
+                g_W, g_b = gemm_tn(P, grad_out, with_db=ctx.needs_input_grad[2])
         elif ctx.needs_input_grad[2]:
             g_b = grad_out.sum(0)
         if ctx.needs_input_grad[0]:
@@ -956,7 +968,31 @@ class _AggregateTransformFn(torch.autograd.Function):
                 g_x = _reduce_backward(ctx.g, ctx.red, ctx.weighted, False, x, dP, ctx.exact, ctx.x_rows)
                 if ctx.pre_gin:
                     g_x = g_x + dP * ctx.gin_scale
+        if side is not None:  # join: dW / db are ready before anything later on this stream
+            cur = torch.cuda.current_stream(grad_out.device)
+            cur.wait_stream(side)
+            for t in (g_W, g_b):
+                if t is not None:
+                    t.record_stream(cur)
         return g_x, g_W, g_b, None, None, None, None, None, None
+
+
+_SIDE_STREAMS: dict = {}
+
+
+def _side_stream(dev: torch.device) -> torch.cuda.Stream:
+    """One side stream per device for backward work that runs beside the main pass."""
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    s = _SIDE_STREAMS.get(key)
+    if s is None:
+        s = _SIDE_STREAMS[key] = torch.cuda.Stream(device=dev)
+    return s
+
+
+def _tn_overlap() -> bool:
+    """KGX_TN_OVERLAP (default 1): the fused layers' dW / db pass (kgx_gemm_tn) runs on a side
+    stream beside the dx pass of the same backward; 0 runs it first on the current stream."""
+    return os.environ.get("KGX_TN_OVERLAP", "1") not in ("0", "", "false", "False")
 
 
 def aggregate_transform(

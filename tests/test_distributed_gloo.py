@@ -250,7 +250,7 @@ def _worker(rank, world, chunks, port, q):
         assert merged("chunk")[1] is not None
         # the own-only rows' pass before / after the merged pass (the default picks by the
         # number of later exchange groups): disjoint rows, so the same bits either way
-        for order in ("0", "1"):
+        for order in ("0", "1", "3"):  # 3: first, after the first step's packing (an event on the GPU)
             os.environ["KGX_HALO_A_LATE"] = order
             try:
                 with torch.no_grad():

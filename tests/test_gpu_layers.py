@@ -386,3 +386,30 @@ def test_hip_graph_capture_cu_split(dev, monkeypatch, width):
         torch.cuda.synchronize()
     assert torch.equal(eager, ref)
     assert torch.equal(out, ref)
+
+
+def test_numpy_edge_index_cached(dev):
+    """A reference-style caller passing the same numpy edge_index every step
+    (the reference caches its int32 cast by id(), message_passing.py:256-268):
+    the device copy and the CSR are built once; an in-place change to the
+    array (caught by the sampled fingerprint) or a new array rebuilds."""
+    from keras_geometric_amd import graph as G
+    from keras_geometric_amd.layers import _edges
+
+    G.clear_cache()
+    rng = np.random.default_rng(0)
+    n, e = 3000, 20000
+    ei = rng.integers(0, n, (2, e)).astype(np.int64)
+    x = torch.randn(n, 16, device=dev)
+    layer = kgx.GCNConv(8)
+    with torch.no_grad():
+        y1 = layer([x, ei])
+        g1 = next(reversed(G._CACHE.values()))[1]
+        y2 = layer([x, ei])
+        assert len(G._CACHE) == 1 and len(_edges._HOST_CAST) == 1
+        assert next(reversed(G._CACHE.values()))[1] is g1 and torch.equal(y1, y2)
+        ei[:] = ei[:, ::-1].copy()  # in place: a different graph in the same buffer
+        y3 = layer([x, ei])
+        assert next(reversed(G._CACHE.values()))[1] is not g1
+        ref = layer([x, torch.from_numpy(ei.copy()).to(dev)])
+        assert torch.equal(y3, ref)

@@ -182,7 +182,8 @@ def main():
     ap.add_argument("--merged", default="1", help="KGX_HALO_MERGED values to run (0: round-2 own pass + chunk passes)")
     ap.add_argument("--merge-unit", default="step", help="KGX_HALO_MERGE values: step, chunk")
     ap.add_argument("--a-late", default="auto",
-                    help="KGX_HALO_A_LATE values (1: own-only rows after the merged pass; auto: the layer's rule)")
+                    help="KGX_HALO_A_LATE values (1: own-only rows after the merged pass; 3: first, after the first "
+                         "step's packing; auto: the layer's rule)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--share-den", default="8",
                     help="KGX_SHARE_DEN values timed on each built shard (the overlapped passes leave 1/den of "
@@ -227,7 +228,7 @@ def main():
         os.environ["KGX_HALO_PUSH"] = push
         os.environ["KGX_HALO_MERGED"] = merged
         os.environ["KGX_HALO_MERGE"] = unit
-        if a_late in ("0", "1"):
+        if a_late in ("0", "1", "2", "3"):
             os.environ["KGX_HALO_A_LATE"] = a_late
         else:
             os.environ.pop("KGX_HALO_A_LATE", None)
@@ -297,7 +298,9 @@ def main():
                     tl = sorted(([w, round(ref.elapsed_time(a), 3), round(ref.elapsed_time(b), 3), nb]
                                  for w, a, b, nb in items), key=lambda r: r[1])
                     print(json.dumps({"timeline": tl, "step_ms": round(ref.elapsed_time(end), 3),
-                                      "share_den": int(den), "chunks": K, "link_gbps": args.link_gbps}),
+                                      "share_den": int(den), "chunks": K, "link_gbps": args.link_gbps,
+                                      "a_late": a_late, "config": args.config, "world": P,
+                                      "env": {k: v for k, v in os.environ.items() if k.startswith("KGX_")}}),
                           flush=True)
                 kops.EVENT_SINK = []
                 t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
