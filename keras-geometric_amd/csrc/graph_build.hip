@@ -82,13 +82,51 @@ __global__ void csr_rowptr_kernel(const uint32_t* __restrict__ keys, int64_t tot
   }
 }
 
+// col[e] = srcn[eid[e]] (the source of every CSR slot) and, with NORM, the GCN
+// edge norm w[e] = dinv[dst(e)] * dinv[col[e]] (utils/main.py:29-32,
+// take(dinv, target) * take(dinv, source)) in the same pass.  The srcn and
+// dinv[col] reads are random: each thread takes kColIlp slots per iteration
+// (coalesced across the block) and issues all their loads before the first
+// use, so a wave has that many random reads in flight instead of one.
+constexpr int kColIlp = 8;
+
+template <bool NORM>
 __global__ void csr_col_kernel(const int32_t* __restrict__ eid, const int32_t* __restrict__ srcn,
-                               const int32_t* __restrict__ rowptr, int64_t n_dst,
-                               int32_t* __restrict__ col) {
+                               const uint32_t* __restrict__ keys_sorted, const int32_t* __restrict__ rowptr,
+                               int64_t n_dst, const float* __restrict__ dinv, int32_t* __restrict__ col,
+                               float* __restrict__ w) {
   const int64_t kept = rowptr[n_dst];
-  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
-  for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < kept; e += stride)
-    col[e] = srcn[eid[e]];
+  if (kept <= 0) return;
+  const int64_t chunk = int64_t(blockDim.x) * kColIlp;
+  for (int64_t base = int64_t(blockIdx.x) * chunk; base < kept; base += int64_t(gridDim.x) * chunk) {
+    int32_t ev[kColIlp], c[kColIlp];
+#pragma unroll
+    for (int j = 0; j < kColIlp; ++j) {
+      const int64_t e = base + int64_t(j) * blockDim.x + threadIdx.x;
+      ev[j] = eid[e < kept ? e : kept - 1];
+    }
+#pragma unroll
+    for (int j = 0; j < kColIlp; ++j) c[j] = srcn[ev[j]];
+    if constexpr (NORM) {
+      float dd[kColIlp], ds[kColIlp];
+#pragma unroll
+      for (int j = 0; j < kColIlp; ++j) {
+        const int64_t e = base + int64_t(j) * blockDim.x + threadIdx.x;
+        dd[j] = dinv[keys_sorted[e < kept ? e : kept - 1]];
+        ds[j] = dinv[c[j]];
+      }
+#pragma unroll
+      for (int j = 0; j < kColIlp; ++j) {
+        const int64_t e = base + int64_t(j) * blockDim.x + threadIdx.x;
+        if (e < kept) w[e] = __fmul_rn(dd[j], ds[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kColIlp; ++j) {
+      const int64_t e = base + int64_t(j) * blockDim.x + threadIdx.x;
+      if (e < kept) col[e] = c[j];
+    }
+  }
 }
 
 // Integer in-degree; fp32 degree as the reference computes it: a sequential
@@ -135,16 +173,6 @@ __global__ void csr_deg_kernel(const int32_t* __restrict__ rowptr, int64_t n_dst
   }
   if ((threadIdx.x & 63) == 0 && mx) atomicMax(&st->max_deg, mx);
   if ((threadIdx.x & 63) == 0 && miss) atomicAdd(&st->table_miss, (unsigned long long)miss);
-}
-
-// norm_e = dinv[dst] * dinv[src]  (utils/main.py:29-32; take(dinv,target)*take(dinv,source))
-__global__ void csr_norm_kernel(const uint32_t* __restrict__ keys_sorted, const int32_t* __restrict__ col,
-                                const int32_t* __restrict__ rowptr, int64_t n_dst,
-                                const float* __restrict__ dinv, float* __restrict__ w) {
-  const int64_t kept = rowptr[n_dst];
-  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
-  for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < kept; e += stride)
-    w[e] = __fmul_rn(dinv[keys_sorted[e]], dinv[col[e]]);
 }
 
 size_t sort_temp_bytes(int64_t n, int end_bit) {
@@ -216,13 +244,21 @@ __global__ void gcn_edge_norm_kernel(const int32_t* __restrict__ rowptr, const i
 __global__ void gcn_edge_norm_long_kernel(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
                                           int64_t n_dst, const float* __restrict__ dinv_dst,
                                           const float* __restrict__ dinv_src, float* __restrict__ w) {
+  // each wave scans 64 rows at a time (one per lane) and takes the rows of degree > 64 one
+  // after another with all its lanes
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t(gridDim.x) * blockDim.x) >> 6;
-  for (int64_t r = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; r < n_dst; r += nw) {
-    const int32_t b = rowptr[r], e1 = rowptr[r + 1];
-    if (e1 - b <= 64) continue;
-    const float dr = dinv_dst[r];
-    for (int32_t e = b + lane; e < e1; e += 64) w[e] = __fmul_rn(dr, dinv_src[col[e]]);
+  for (int64_t r0 = ((int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6) * 64; r0 < n_dst; r0 += nw * 64) {
+    const int64_t r = r0 + lane;
+    const int32_t b = r < n_dst ? rowptr[r] : 0, e1 = r < n_dst ? rowptr[r + 1] : 0;
+    unsigned long long long_rows = __ballot(e1 - b > 64);
+    while (long_rows) {
+      const int k = __ffsll(long_rows) - 1;
+      long_rows &= long_rows - 1;
+      const int32_t bk = __shfl(b, k, 64), ek = __shfl(e1, k, 64);
+      const float dr = dinv_dst[r0 + k];
+      for (int32_t e = bk + lane; e < ek; e += 64) w[e] = __fmul_rn(dr, dinv_src[col[e]]);
+    }
   }
 }
 
@@ -494,19 +530,19 @@ extern "C" int kgx_csr_build2(const int32_t* src, const int32_t* dst, int64_t E,
   hipLaunchKernelGGL(csr_rowptr_kernel, dim3(grid_for(n_dst + 1, 8192)), dim3(kBlock), 0, stream,
                      L.keys_sorted, total, n_dst, rowptr, L.st);
   KGX_CHECK_LAUNCH();
-  if (total > 0) {
-    hipLaunchKernelGGL(csr_col_kernel, dim3(grid_for(total, 8192)), dim3(kBlock), 0, stream, eid, L.srcn,
-                       rowptr, n_dst, col);
-    KGX_CHECK_LAUNCH();
-  }
-  if (n_dst > 0) {
+  if (n_dst > 0) {  // degrees (and dinv) first: the col pass below computes the norms with it
     hipLaunchKernelGGL(csr_deg_kernel, dim3(grid_for(n_dst, 8192)), dim3(kBlock), 0, stream, rowptr, n_dst,
                        flags, deg, dinv, dinv_table, table_len, L.st);
     KGX_CHECK_LAUNCH();
   }
-  if (norm && total > 0) {
-    hipLaunchKernelGGL(csr_norm_kernel, dim3(grid_for(total, 8192)), dim3(kBlock), 0, stream,
-                       L.keys_sorted, col, rowptr, n_dst, dinv, w);
+  if (total > 0) {
+    const dim3 grid(grid_for(total / kColIlp + 1, 8192));
+    if (norm)
+      hipLaunchKernelGGL(csr_col_kernel<true>, grid, dim3(kBlock), 0, stream, eid, L.srcn, L.keys_sorted, rowptr,
+                         n_dst, dinv, col, w);
+    else
+      hipLaunchKernelGGL(csr_col_kernel<false>, grid, dim3(kBlock), 0, stream, eid, L.srcn, L.keys_sorted, rowptr,
+                         n_dst, dinv, col, w);
     KGX_CHECK_LAUNCH();
   }
   CsrStatus hs;
@@ -718,7 +754,7 @@ extern "C" int kgx_gcn_edge_norm(const int32_t* rowptr, const int32_t* col, int6
   hipLaunchKernelGGL(gcn_edge_norm_kernel, dim3(grid_for(n_dst * 8, 8192)), dim3(kBlock), 0, s, rowptr, col, n_dst,
                      dinv_dst, dinv_src, w);
   KGX_CHECK_LAUNCH();
-  hipLaunchKernelGGL(gcn_edge_norm_long_kernel, dim3(grid_for(n_dst * 64, 8192)), dim3(kBlock), 0, s, rowptr, col,
+  hipLaunchKernelGGL(gcn_edge_norm_long_kernel, dim3(grid_for(n_dst, 8192)), dim3(kBlock), 0, s, rowptr, col,
                      n_dst, dinv_dst, dinv_src, w);
   KGX_CHECK_LAUNCH();
   return KGX_OK;

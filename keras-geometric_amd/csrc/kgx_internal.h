@@ -81,13 +81,14 @@ unsigned resident_grid(Kern kernel, int64_t groups_needed, int G) {
 }
 
 // A launch that shares the GPU with a concurrent stream (KGX_FUSED_SHARE_GPU)
-// takes (den - 1) / den of its resident grid: den = KGX_SHARE_DEN (default 16:
-// the sharded GCN step with light rows, simulated at 400 GB/s, measured 12.31-
-// 12.36 ms at 8, 12.16-12.18 at 16, 12.12-12.17 at 32, 13.07-13.13 at 64).
+// takes (den - 1) / den of its resident grid: den = KGX_SHARE_DEN (default 32:
+// the sharded GCN step with light rows and pruned pulls, simulated at 400 GB/s
+// on three boxes, measured 11.72-11.79 ms at 32 against 11.80-11.84 at 16; 8
+// and 64 were slower in round 5, 12.31-12.36 and 13.07-13.13 ms).
 inline int64_t shared_cap(int64_t full) {
   const char* h = getenv("KGX_SHARE_DEN");  // read per launch: measurement sweeps change it in-process
-  const int v = h ? atoi(h) : 16;
-  const int den = v >= 2 ? v : 16;
+  const int v = h ? atoi(h) : 32;
+  const int den = v >= 2 ? v : 32;
   const int64_t c = full * (den - 1) / den;
   return c > 0 ? c : 1;
 }

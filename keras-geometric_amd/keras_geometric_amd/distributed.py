@@ -446,8 +446,6 @@ class ShardedGraph:
     self_loops: bool = True  # the shard graph carries utils/main.py:8-16's self loops (GCN, GATv2)
     link_probe: list | None = None  # a list: time every exchange step's landing (bench.py N > 1; link_report)
     _probe_stream: object = None
-    first_pack_done: object = None  # event: the side stream after the first exchange step's packing
-    _stream2: object = None  # the second main stream of KGX_HALO_DUAL
     packs_done: object = None  # event: the side stream after every step's packing
 
     @property
@@ -1161,11 +1159,6 @@ class ShardedGraph:
                 handles = []
                 for j, st in enumerate(c.steps or [c]):
                     send = self._pack(x_local, st)
-                    if k == 0 and j == 0 and x_local.is_cuda:
-                        # the side stream after the first step's packing: the first transfer's
-                        # start (a pass may wait for it instead of slowing that packing)
-                        self.first_pack_done = torch.cuda.Event()
-                        self.first_pack_done.record()
                     ev = None
                     if self.link_probe is not None and start is not None and x_local.is_cuda:
                         ev = torch.cuda.Event(enable_timing=True)
@@ -1539,14 +1532,9 @@ class ShardedGCNConv(Layer):
         # 14.47).  KGX_HALO_A_LATE=0 / 1 forces either order (measurement A/B).
         # KGX_HALO_A_LATE=2 (experiment): pass A where it is, but after the packs
         # (the side stream's packing alone on the GPU, then pass A beside the transfers)
-        # KGX_HALO_A_LATE=3: pass A first, but after the FIRST step's packing only -- the first
-        # transfer then starts as early as with pass A late, and pass A runs beside the later
-        # packing / partial sums (which have until the first transfer lands) instead of after
-        # the merged pass
         forced = os.environ.get("KGX_HALO_A_LATE")
-        a_late = forced == "1" if forced in ("0", "1", "2", "3") else len(later) >= 2
+        a_late = forced == "1" if forced in ("0", "1", "2") else len(later) >= 2
         a_after_pack = forced == "2"
-        a_after_first = forced == "3"
         with torch.no_grad():
             works = sg.start_halo_exchange(x_local, halo, pp.chunks)
             handles = []
@@ -1561,21 +1549,12 @@ class ShardedGCNConv(Layer):
                         if handles[j] is not None:
                             handles[j].wait()
 
-            # KGX_HALO_DUAL=1: the own-only rows (g_a) and the light rows' passes on a second
-            # stream beside the merged and accumulating passes -- disjoint rows of `out`, so
-            # the passes' ramps and tails overlap instead of following one another
-            dual = halo_dual() and x_local.is_cuda and g_b is not None
-            if dual:
-                return self._forward_merged_dual(x_local, bias, halo, g_a, g_b, later, first_wait, lights, steps,
-                                                 handles, wait_step)
             if a_late and g_b is not None:
                 out = torch.empty((x_local.shape[0], self.kernel.shape[1]), dtype=torch.float32,
                                   device=x_local.device)
             else:
                 if a_after_pack and getattr(sg, "packs_done", None) is not None and x_local.is_cuda:
                     torch.cuda.current_stream(x_local.device).wait_event(sg.packs_done)
-                if a_after_first and getattr(sg, "first_pack_done", None) is not None and x_local.is_cuda:
-                    torch.cuda.current_stream(x_local.device).wait_event(sg.first_pack_done)
                 with kops.sharing_gpu():  # the exchange's packing and RCCL kernels run beside this pass
                     out = sg.backend.aggregate_transform(g_a, x_local, self.kernel, bias=bias)
             if g_b is not None:
@@ -1606,62 +1585,6 @@ class ShardedGCNConv(Layer):
             # every step, used or not: also orders the side stream's reads of x_local
             wait_step(len(steps) - 1)
         return out
-
-    def _forward_merged_dual(self, x_local, bias, halo, g_a, g_b, later, first_wait, lights, steps, handles,
-                             wait_step):
-        """_forward_merged with two main streams (KGX_HALO_DUAL=1): the current
-        stream runs the merged pass and the accumulating passes; a second stream
-        runs the own-only rows' pass (after the side stream's packing) and each
-        light-row pass (once the last group it needs has landed).  The row sets
-        are disjoint, so the result is the one-stream path's bit for bit."""
-        sg = self.sg
-        dev = x_local.device
-        main = torch.cuda.current_stream(dev)
-        if sg._stream2 is None:
-            sg._stream2 = torch.cuda.Stream(device=dev)
-        s2 = sg._stream2
-        out = torch.empty((x_local.shape[0], self.kernel.shape[1]), dtype=torch.float32, device=dev)
-        s2.wait_stream(main)  # x_local, out and the halo buffer's previous readers
-        waited2 = set()
-
-        def wait_step2(i):  # as wait_step, for the second stream
-            for j in range(i + 1):
-                if j not in waited2:
-                    waited2.add(j)
-                    if handles[j] is not None:
-                        handles[j].wait()
-
-        with torch.cuda.stream(s2):
-            if getattr(sg, "packs_done", None) is not None:
-                s2.wait_event(sg.packs_done)  # the packing first: it starts the transfers
-            with kops.sharing_gpu():
-                sg.backend.aggregate_transform(g_a, x_local, self.kernel, bias=bias, out=out, accumulate=False)
-            ga_done = torch.cuda.Event()
-            ga_done.record()  # rows of g_a may take later groups' accumulating passes
-            for i, gl in lights:
-                wait_step2(i)
-                with kops.sharing_gpu():
-                    sg.backend.aggregate_transform(gl, x_local, self.kernel, bias=bias, out=out, x2=halo,
-                                                   accumulate=False)
-        wait_step(first_wait)
-        with kops.sharing_gpu():
-            sg.backend.aggregate_transform(g_b, x_local, self.kernel, bias=bias, out=out, x2=halo,
-                                           accumulate=False)
-        main.wait_event(ga_done)
-        for n, (i, g, lo, hi) in enumerate(later):
-            wait_step(i)
-            with kops.sharing_gpu():
-                sg.backend.aggregate_transform(g, halo[lo: hi], self.kernel, out=out)
-        wait_step(len(steps) - 1)  # also orders the side stream's reads of x_local
-        main.wait_stream(s2)
-        x_local.record_stream(s2)
-        out.record_stream(s2)
-        return out
-
-
-def halo_dual() -> bool:
-    """KGX_HALO_DUAL=1: own-only and light-row passes on a second stream (measurement A/B)."""
-    return os.environ.get("KGX_HALO_DUAL", "0") == "1"
 
 
 def halo_light() -> int:

@@ -278,18 +278,6 @@ def test_sharded_gcn_chunked_halo_pipeline(world, chunks, push, comm, dev, monke
     assert err.max() <= 1e-5
 
 
-@pytest.mark.parametrize("world,chunks,comm", [(2, 2, "async_delayed"), (3, 3, "async"), (2, 1, "sync")])
-def test_sharded_gcn_dual_stream(world, chunks, comm, dev, monkeypatch):
-    """KGX_HALO_DUAL=1: the own-only and light-row passes on a second stream
-    beside the merged / accumulating passes (disjoint rows; the accumulating
-    passes wait for the own-only pass), with a delayed asynchronous comm so a
-    missing wait reads rows that have not landed -- same tolerance as the
-    one-stream path."""
-    monkeypatch.setenv("KGX_HALO_DUAL", "1")
-    monkeypatch.setenv("KGX_HALO_LIGHT", "7")
-    test_sharded_gcn_chunked_halo_pipeline(world, chunks, "1", comm, dev, monkeypatch)
-
-
 def _run_conv_rank(rank, hub, dev, x, out):
     try:
         comm = ThreadComm(hub, rank)

@@ -182,8 +182,7 @@ def main():
     ap.add_argument("--merged", default="1", help="KGX_HALO_MERGED values to run (0: round-2 own pass + chunk passes)")
     ap.add_argument("--merge-unit", default="step", help="KGX_HALO_MERGE values: step, chunk")
     ap.add_argument("--a-late", default="auto",
-                    help="KGX_HALO_A_LATE values (1: own-only rows after the merged pass; 3: first, after the first "
-                         "step's packing; auto: the layer's rule)")
+                    help="KGX_HALO_A_LATE values (1: own-only rows after the merged pass; auto: the layer's rule)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--share-den", default="8",
                     help="KGX_SHARE_DEN values timed on each built shard (the overlapped passes leave 1/den of "
@@ -228,7 +227,7 @@ def main():
         os.environ["KGX_HALO_PUSH"] = push
         os.environ["KGX_HALO_MERGED"] = merged
         os.environ["KGX_HALO_MERGE"] = unit
-        if a_late in ("0", "1", "2", "3"):
+        if a_late in ("0", "1", "2"):
             os.environ["KGX_HALO_A_LATE"] = a_late
         else:
             os.environ.pop("KGX_HALO_A_LATE", None)
