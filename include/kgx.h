@@ -129,6 +129,23 @@ int kgx_csr_build2(const int32_t* src, const int32_t* dst, int64_t E,
                    int64_t* info, kgx_stream_t stream);
 
 /* ---------------------------------------------------------------------------
+ * Schedule tails, on the device (the fused kernels' short-row and tiny-row
+ * launches take the degree-descending schedule's suffix of small unsplit rows):
+ * kgx_schedule_suffixes: out[0] = 1 + the last item (int4 {row, beg, end,
+ * slot}) that is split or has more than short_max edges, out[1] the same for
+ * tiny_max (0: none).  kgx_tiny_pack: the records of items [start, start+n):
+ * pack[i] = {row, degree, col0, col1} (col1 = col0 for degree 1, 0 / 0 for
+ * degree 0; indices clamped to n_col - 1), tw[i] = {w0, w1} (0 where absent;
+ * tw NULL: unweighted); out[0] = records of degree 2, out[1] = 1 + the last
+ * of them.  Both take a 16-byte device workspace and synchronise `stream`.
+ * ------------------------------------------------------------------------- */
+int kgx_schedule_suffixes(const int32_t* items, int64_t n_items, int short_max, int tiny_max,
+                          void* workspace, int64_t* out, kgx_stream_t stream);
+int kgx_tiny_pack(const int32_t* items, int64_t start, int64_t n, const int32_t* col, const float* w,
+                  int64_t n_col, int32_t* pack, float* tw, void* workspace, int64_t* out,
+                  kgx_stream_t stream);
+
+/* ---------------------------------------------------------------------------
  * GCN normalisation for a CSR whose sources index a different table than its
  * rows (a destination-range shard: rows = owned nodes, sources = owned + halo
  * nodes).  Same arithmetic as KGX_CSR_GCN_NORM (utils/main.py:20-33):

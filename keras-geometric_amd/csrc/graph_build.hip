@@ -31,8 +31,8 @@ struct CsrStatus {
 
 __global__ void csr_prep_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
                                 int64_t E, int64_t n_src, int64_t n_dst, int flags,
-                                uint32_t* __restrict__ keys, int32_t* __restrict__ vals,
-                                int32_t* __restrict__ srcn, CsrStatus* __restrict__ st) {
+                                uint32_t* __restrict__ keys, uint64_t* __restrict__ vals,
+                                CsrStatus* __restrict__ st) {
   const bool segment_only = flags & KGX_CSR_SEGMENT_ONLY;
   const bool loops = flags & KGX_CSR_SELF_LOOPS;
   const int64_t total = E + (loops ? n_dst : 0);
@@ -54,13 +54,11 @@ __global__ void csr_prep_kernel(const int32_t* __restrict__ src, const int32_t* 
         if (s < 0) s += n_src;
       }
       keys[e] = keep ? uint32_t(d) : uint32_t(n_dst);
-      vals[e] = int32_t(e);
-      srcn[e] = int32_t(s);
+      vals[e] = (uint64_t(uint32_t(s)) << 32) | uint32_t(e);  // {input edge id, wrapped source}
     } else {
       const int64_t i = e - E;
       keys[e] = uint32_t(i);
-      vals[e] = int32_t(e);
-      srcn[e] = int32_t(i);
+      vals[e] = (uint64_t(uint32_t(i)) << 32) | uint32_t(e);
     }
   }
   if (bad) atomicAdd(&st->bad, bad);
@@ -82,38 +80,36 @@ __global__ void csr_rowptr_kernel(const uint32_t* __restrict__ keys, int64_t tot
   }
 }
 
-// col[e] = srcn[eid[e]] (the source of every CSR slot) and, with NORM, the GCN
-// edge norm w[e] = dinv[dst(e)] * dinv[col[e]] (utils/main.py:29-32,
-// take(dinv, target) * take(dinv, source)) in the same pass.  The srcn and
-// dinv[col] reads are random: each thread takes kColIlp slots per iteration
-// (coalesced across the block) and issues all their loads before the first
-// use, so a wave has that many random reads in flight instead of one.
-constexpr int kColIlp = 8;
+// The sorted {input edge id, source} pairs -> eid[e] and col[e] (the source of
+// every CSR slot), and with NORM the GCN edge norm w[e] = dinv[dst(e)] *
+// dinv[col[e]] (utils/main.py:29-32, take(dinv, target) * take(dinv, source))
+// in the same pass.  The source travels through the sort with the edge id, so
+// only dinv[col] is a random read (a 4-byte read from the n-entry dinv table);
+// each thread takes kColIlp slots per iteration (coalesced across the block)
+// and issues their loads before the first use.
+constexpr int kColIlp = 4;
 
 template <bool NORM>
-__global__ void csr_col_kernel(const int32_t* __restrict__ eid, const int32_t* __restrict__ srcn,
-                               const uint32_t* __restrict__ keys_sorted, const int32_t* __restrict__ rowptr,
-                               int64_t n_dst, const float* __restrict__ dinv, int32_t* __restrict__ col,
-                               float* __restrict__ w) {
+__global__ void csr_col_kernel(const uint64_t* __restrict__ vals_sorted, const uint32_t* __restrict__ keys_sorted,
+                               const int32_t* __restrict__ rowptr, int64_t n_dst, const float* __restrict__ dinv,
+                               int32_t* __restrict__ eid, int32_t* __restrict__ col, float* __restrict__ w) {
   const int64_t kept = rowptr[n_dst];
   if (kept <= 0) return;
   const int64_t chunk = int64_t(blockDim.x) * kColIlp;
   for (int64_t base = int64_t(blockIdx.x) * chunk; base < kept; base += int64_t(gridDim.x) * chunk) {
-    int32_t ev[kColIlp], c[kColIlp];
+    uint64_t v[kColIlp];
 #pragma unroll
     for (int j = 0; j < kColIlp; ++j) {
       const int64_t e = base + int64_t(j) * blockDim.x + threadIdx.x;
-      ev[j] = eid[e < kept ? e : kept - 1];
+      v[j] = vals_sorted[e < kept ? e : kept - 1];
     }
-#pragma unroll
-    for (int j = 0; j < kColIlp; ++j) c[j] = srcn[ev[j]];
     if constexpr (NORM) {
       float dd[kColIlp], ds[kColIlp];
 #pragma unroll
       for (int j = 0; j < kColIlp; ++j) {
         const int64_t e = base + int64_t(j) * blockDim.x + threadIdx.x;
         dd[j] = dinv[keys_sorted[e < kept ? e : kept - 1]];
-        ds[j] = dinv[c[j]];
+        ds[j] = dinv[int32_t(v[j] >> 32)];
       }
 #pragma unroll
       for (int j = 0; j < kColIlp; ++j) {
@@ -124,7 +120,10 @@ __global__ void csr_col_kernel(const int32_t* __restrict__ eid, const int32_t* _
 #pragma unroll
     for (int j = 0; j < kColIlp; ++j) {
       const int64_t e = base + int64_t(j) * blockDim.x + threadIdx.x;
-      if (e < kept) col[e] = c[j];
+      if (e < kept) {
+        eid[e] = int32_t(uint32_t(v[j]));
+        col[e] = int32_t(v[j] >> 32);
+      }
     }
   }
 }
@@ -183,11 +182,19 @@ size_t sort_temp_bytes(int64_t n, int end_bit) {
   return bytes;
 }
 
+size_t sort_temp_bytes64(int64_t n, int end_bit) {
+  size_t bytes = 0;
+  uint32_t* k = nullptr;
+  uint64_t* v = nullptr;
+  (void)rocprim::radix_sort_pairs(nullptr, bytes, k, k, v, v, (unsigned)n, 0, end_bit, 0, false);
+  return bytes;
+}
+
 struct CsrLayout {
   uint32_t* keys;
   uint32_t* keys_sorted;
-  int32_t* vals;
-  int32_t* srcn;
+  uint64_t* vals;         // {input edge id, source} per edge
+  uint64_t* vals_sorted;
   CsrStatus* st;
   void* sort_tmp;
   size_t sort_bytes;
@@ -199,11 +206,11 @@ CsrLayout csr_layout(void* ws, int64_t total, int64_t n_dst) {
   CsrLayout L;
   L.keys = c.take<uint32_t>(total);
   L.keys_sorted = c.take<uint32_t>(total);
-  L.vals = c.take<int32_t>(total);
-  L.srcn = c.take<int32_t>(total);
+  L.vals = c.take<uint64_t>(total);
+  L.vals_sorted = c.take<uint64_t>(total);
   L.st = c.take<CsrStatus>(1);
   const int end_bit = ceil_log2_u64(uint64_t(n_dst) + 1);
-  L.sort_bytes = sort_temp_bytes(total, end_bit > 0 ? end_bit : 1);
+  L.sort_bytes = sort_temp_bytes64(total, end_bit > 0 ? end_bit : 1);
   L.sort_tmp = c.take<char>(L.sort_bytes);
   L.total = c.used();
   return L;
@@ -519,11 +526,11 @@ extern "C" int kgx_csr_build2(const int32_t* src, const int32_t* dst, int64_t E,
   KGX_CHECK_HIP(hipMemsetAsync(L.st, 0, sizeof(CsrStatus), stream));
   if (total > 0) {
     hipLaunchKernelGGL(csr_prep_kernel, dim3(grid_for(total, 8192)), dim3(kBlock), 0, stream, src, dst, E,
-                       n_src, n_dst, flags, L.keys, L.vals, L.srcn, L.st);
+                       n_src, n_dst, flags, L.keys, L.vals, L.st);
     KGX_CHECK_LAUNCH();
     const int end_bit = ceil_log2_u64(uint64_t(n_dst) + 1);
     size_t sb = L.sort_bytes;
-    KGX_CHECK_HIP(rocprim::radix_sort_pairs(L.sort_tmp, sb, L.keys, L.keys_sorted, L.vals, eid,
+    KGX_CHECK_HIP(rocprim::radix_sort_pairs(L.sort_tmp, sb, L.keys, L.keys_sorted, L.vals, L.vals_sorted,
                                             (unsigned)total, 0, end_bit > 0 ? end_bit : 1, stream,
                                             false));
   }
@@ -538,11 +545,11 @@ extern "C" int kgx_csr_build2(const int32_t* src, const int32_t* dst, int64_t E,
   if (total > 0) {
     const dim3 grid(grid_for(total / kColIlp + 1, 8192));
     if (norm)
-      hipLaunchKernelGGL(csr_col_kernel<true>, grid, dim3(kBlock), 0, stream, eid, L.srcn, L.keys_sorted, rowptr,
-                         n_dst, dinv, col, w);
+      hipLaunchKernelGGL(csr_col_kernel<true>, grid, dim3(kBlock), 0, stream, L.vals_sorted, L.keys_sorted, rowptr,
+                         n_dst, dinv, eid, col, w);
     else
-      hipLaunchKernelGGL(csr_col_kernel<false>, grid, dim3(kBlock), 0, stream, eid, L.srcn, L.keys_sorted, rowptr,
-                         n_dst, dinv, col, w);
+      hipLaunchKernelGGL(csr_col_kernel<false>, grid, dim3(kBlock), 0, stream, L.vals_sorted, L.keys_sorted, rowptr,
+                         n_dst, dinv, eid, col, w);
     KGX_CHECK_LAUNCH();
   }
   CsrStatus hs;
@@ -769,4 +776,114 @@ extern "C" int kgx_cu_split_supported(int device) {
   KGX_CHECK_HIP(hipGetDeviceCount(&n));
   KGX_REQUIRE(device >= 0 && device < n, KGX_ERR_ARG, "kgx_cu_split_supported: no device %d", device);
   return cu_split_device_ok(device) ? 1 : 0;
+}
+
+// ---------------------------------------------------------------------------
+// Schedule tails (graph.short_suffix_start / tiny.tiny_suffix_start) and the
+// tiny-row records (tiny.tiny_pack) on the device: one pass each instead of a
+// dozen torch ops with their host syncs (NS graph build: ~1.8 ms of 10).
+// ---------------------------------------------------------------------------
+namespace kgx {
+namespace {
+
+// out[0] = 1 + the last item that is split (slot >= 0) or longer than short_max,
+// out[1] = the same for tiny_max (0: none) -- the suffix of short / tiny rows starts there
+__global__ void sched_suffix_kernel(const int4* __restrict__ items, int64_t n, int short_max, int tiny_max,
+                                    unsigned long long* __restrict__ out) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  unsigned long long ls = 0, lt = 0;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int4 v = items[i];
+    const int len = v.z - v.y;
+    if (v.w >= 0 || len > short_max) ls = (unsigned long long)(i + 1);
+    if (v.w >= 0 || len > tiny_max) lt = (unsigned long long)(i + 1);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long a = __shfl_xor(ls, o, 64), b = __shfl_xor(lt, o, 64);
+    ls = a > ls ? a : ls;
+    lt = b > lt ? b : lt;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (ls) atomicMax(&out[0], ls);
+    if (lt) atomicMax(&out[1], lt);
+  }
+}
+
+// record i of the tail items [start, start + n): {row, degree, col0, col1} and {w0, w1}
+// (tiny.py's layout: col1 = col0 for degree 1, both 0 for degree 0, weights 0 where absent);
+// st[0] counts the degree-2 records, st[1] = 1 + the last degree-2 record
+__global__ void tiny_pack_kernel(const int4* __restrict__ items, int64_t start, int64_t n,
+                                 const int32_t* __restrict__ col, const float* __restrict__ w, int64_t n_col,
+                                 int4* __restrict__ pack, float2* __restrict__ tw, unsigned long long* __restrict__ st) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  unsigned long long cnt = 0, last2 = 0;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int4 v = items[start + i];
+    const int deg = v.z - v.y;
+    const int64_t last = n_col - 1;
+    const int64_t i0 = v.y < last ? v.y : last;
+    const int64_t i1b = int64_t(v.y) + (deg > 1 ? 1 : 0);
+    const int64_t i1 = i1b < last ? i1b : last;
+    const int32_t c0 = deg > 0 ? col[i0] : 0, c1 = deg > 0 ? col[i1] : 0;
+    pack[i] = make_int4(v.x, deg, c0, c1);
+    if (tw) tw[i] = make_float2(deg > 0 ? w[i0] : 0.0f, deg > 1 ? w[i1] : 0.0f);
+    if (deg == 2) {
+      ++cnt;
+      last2 = (unsigned long long)(i + 1);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    cnt += __shfl_xor(cnt, o, 64);
+    const unsigned long long b = __shfl_xor(last2, o, 64);
+    last2 = b > last2 ? b : last2;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (cnt) atomicAdd(&st[0], cnt);
+    if (last2) atomicMax(&st[1], last2);
+  }
+}
+
+}  // namespace
+}  // namespace kgx
+
+extern "C" int kgx_schedule_suffixes(const int32_t* items, int64_t n_items, int short_max, int tiny_max,
+                                     void* workspace, int64_t* out, kgx_stream_t stream_) {
+  KGX_REQUIRE(n_items >= 0 && out && workspace && (n_items == 0 || items), KGX_ERR_ARG,
+              "kgx_schedule_suffixes: bad arguments");
+  hipStream_t s = as_stream(stream_);
+  auto* st = static_cast<unsigned long long*>(workspace);
+  KGX_CHECK_HIP(hipMemsetAsync(st, 0, 2 * sizeof(unsigned long long), s));
+  if (n_items > 0) {
+    hipLaunchKernelGGL(sched_suffix_kernel, dim3(grid_for(n_items, 4096)), dim3(kBlock), 0, s,
+                       reinterpret_cast<const int4*>(items), n_items, short_max, tiny_max, st);
+    KGX_CHECK_LAUNCH();
+  }
+  unsigned long long h[2];
+  KGX_CHECK_HIP(hipMemcpyAsync(h, st, sizeof(h), hipMemcpyDeviceToHost, s));
+  KGX_CHECK_HIP(hipStreamSynchronize(s));
+  out[0] = int64_t(h[0]);
+  out[1] = int64_t(h[1]);
+  return KGX_OK;
+}
+
+extern "C" int kgx_tiny_pack(const int32_t* items, int64_t start, int64_t n, const int32_t* col, const float* w,
+                             int64_t n_col, int32_t* pack, float* tw, void* workspace, int64_t* out,
+                             kgx_stream_t stream_) {
+  KGX_REQUIRE(start >= 0 && n >= 0 && n_col > 0 && items && col && pack && workspace && out && (!tw || w),
+              KGX_ERR_ARG, "kgx_tiny_pack: bad arguments");
+  hipStream_t s = as_stream(stream_);
+  auto* st = static_cast<unsigned long long*>(workspace);
+  KGX_CHECK_HIP(hipMemsetAsync(st, 0, 2 * sizeof(unsigned long long), s));
+  if (n > 0) {
+    hipLaunchKernelGGL(tiny_pack_kernel, dim3(grid_for(n, 4096)), dim3(kBlock), 0, s,
+                       reinterpret_cast<const int4*>(items), start, n, col, tw ? w : nullptr, n_col,
+                       reinterpret_cast<int4*>(pack), reinterpret_cast<float2*>(tw), st);
+    KGX_CHECK_LAUNCH();
+  }
+  unsigned long long h[2];
+  KGX_CHECK_HIP(hipMemcpyAsync(h, st, sizeof(h), hipMemcpyDeviceToHost, s));
+  KGX_CHECK_HIP(hipStreamSynchronize(s));
+  out[0] = int64_t(h[0]);
+  out[1] = int64_t(h[1]);
+  return KGX_OK;
 }

@@ -50,6 +50,10 @@ _SIGNATURES = {
     ],
     "kgx_gcn_dinv": [_i32p, _i64, _f32p, ctypes.c_void_p],
     "kgx_cu_split_layout_ok": [_int, _int, ctypes.c_char_p],
+    "kgx_schedule_suffixes": [_i32p, _i64, _int, _int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64),
+                              ctypes.c_void_p],
+    "kgx_tiny_pack": [_i32p, _i64, _i64, _i32p, _f32p, _i64, _i32p, _f32p, ctypes.c_void_p,
+                      ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p],
     "kgx_gemm_tn_workspace_bytes": [_i64, _i64, _i64, ctypes.POINTER(ctypes.c_size_t)],
     "kgx_gemm_tn": [_i64, _f32p, _i64, _i64, _f32p, _i64, _i64, _f32p, _i64, _f32p, ctypes.c_void_p,
                     ctypes.c_size_t, ctypes.c_void_p],

@@ -240,6 +240,19 @@ def _refresh_tiny(g: CSRGraph) -> None:
 SHORT_ROW_MAX = 7  # KGX_SHORT_ROW_MAX (include/kgx.h)
 
 
+def schedule_suffixes(items: torch.Tensor, short_max: int, tiny_max: int) -> tuple[int, int]:
+    """(first item of the suffix of unsplit rows of degree <= short_max, the
+    same for tiny_max) of a device item list, in one kgx_schedule_suffixes pass."""
+    n = int(items.shape[0])
+    if n == 0:
+        return 0, 0
+    ws = torch.empty(16, dtype=torch.uint8, device=items.device)
+    out = (ctypes.c_int64 * 2)()
+    nat.check(nat.lib().kgx_schedule_suffixes(nat.ptr(items.contiguous()), n, int(short_max), int(tiny_max),
+                                              nat.ptr(ws), out, nat.stream(items.device)), "kgx_schedule_suffixes")
+    return int(out[0]), int(out[1])
+
+
 def short_suffix_start(items: torch.Tensor) -> int:
     """First item of the degree-descending schedule's suffix of unsplit rows of
     degree <= SHORT_ROW_MAX (split rows' chunks are a prefix; rows come in
@@ -248,6 +261,8 @@ def short_suffix_start(items: torch.Tensor) -> int:
     if n == 0 or os.environ.get("KGX_SHORT_ROWS", "1") in ("0", "false", "False"):
         return n
     smax = int(os.environ.get("KGX_SHORT_MAX", SHORT_ROW_MAX))  # experiment knob (the kernel takes any degree)
+    if items.is_cuda:
+        return schedule_suffixes(items, smax, smax)[0]
     short = ((items[:, 2] - items[:, 1]) <= smax) & (items[:, 3] < 0)
     # the suffix starts after the last item that is NOT short
     not_short = torch.nonzero(~short)

@@ -5,7 +5,9 @@ degree <= 2 at the end of the degree-descending schedule (on R-MAT about
 two thirds of all rows; the self loop alone is half) from one record each
 instead of an item plus index and weight loads: {row, degree, col0, col1}
 (col1 = col0 for degree 1, 0 and 0 for degree 0) and {w0, w1}.  Built once
-per graph with torch ops on the graph's device and cached on the graph.
+per graph on the device (kgx_tiny_pack; the torch restatement below builds
+the same records from host tensors and defines the layout the host tests
+check) and cached on the graph.
 Reference semantics are unchanged: the kernel folds exactly the row's CSR
 edges in order (gcn_conv.py:233-272, aggregators.py:56-167).
 """
@@ -22,10 +24,15 @@ _MIN_ROWS = 4096   # below this the tail stays on the short-row kernel
 
 
 def tiny_suffix_start(items: torch.Tensor) -> int:
-    """Index of the first item of the suffix of unsplit rows of degree <= 2."""
+    """Index of the first item of the suffix of unsplit rows of degree <= 2
+    (device items: one kgx_schedule_suffixes pass)."""
     n = items.shape[0]
     if n == 0:
         return 0
+    if items.is_cuda:
+        from .graph import schedule_suffixes
+
+        return schedule_suffixes(items, TINY_MAX, TINY_MAX)[1]
     lens = items[:, 2] - items[:, 1]
     big = (lens > TINY_MAX) | (items[:, 3] >= 0)
     nz = torch.nonzero(big)
@@ -41,6 +48,28 @@ def records(pack: torch.Tensor, tw: Optional[torch.Tensor], n: int, n2: int):
     """The packed tail as {row, degree, col0, col1} [n, 4] and {w0, w1} [n, 2]
     (or None) per row: what tests and tools compare."""
     return pack[:n].long(), (tw[:n] if tw is not None else None)
+
+
+def _tiny_pack_device(g, its: torch.Tensor, start: int, n: int):
+    """The records of items [start, start + n) in one kgx_tiny_pack pass (the
+    layout of the host restatement in tiny_pack below, bit for bit)."""
+    import ctypes
+
+    from . import _native as nat
+
+    dev = its.device
+    pack = torch.empty((n, 4), dtype=torch.int32, device=dev)
+    w = getattr(g, "w", None)
+    tw = torch.empty((n, 2), dtype=torch.float32, device=dev) if w is not None else None
+    ws = torch.empty(16, dtype=torch.uint8, device=dev)
+    out = (ctypes.c_int64 * 2)()
+    nat.check(nat.lib().kgx_tiny_pack(nat.ptr(its.contiguous()), start, n, nat.ptr(g.col), nat.ptr(w),
+                                      int(g.col.numel()), nat.ptr(pack), nat.ptr(tw), nat.ptr(ws), out,
+                                      nat.stream(dev)), "kgx_tiny_pack")
+    n2, last2 = int(out[0]), int(out[1])
+    if n2 and last2 != n2:  # not degree-descending: every record takes the two-edge kernel
+        n2 = n
+    return pack, tw, start, n2
 
 
 def tiny_pack(g, refresh: bool = False) -> tuple[Optional[torch.Tensor], Optional[torch.Tensor], int, int]:
@@ -65,7 +94,9 @@ def tiny_pack(g, refresh: bool = False) -> tuple[Optional[torch.Tensor], Optiona
         start = tiny_suffix_start(its)
         n_long = getattr(g, "n_long", -1)
         start = max(start, n_long if 0 <= n_long <= n_items else 0)
-        if n_items - start >= _MIN_ROWS:
+        if n_items - start >= _MIN_ROWS and its.is_cuda and g.col.numel() > 0:
+            res = _tiny_pack_device(g, its, start, n_items - start)
+        elif n_items - start >= _MIN_ROWS:
             t = its[start:]
             beg = t[:, 1].long()
             deg = (t[:, 2] - t[:, 1]).long()

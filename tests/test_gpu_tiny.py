@@ -146,3 +146,26 @@ def test_fused_fork_bit_identical(dev, fork, monkeypatch):
     torch.testing.assert_close(y1, y0, rtol=0, atol=0)
     torch.testing.assert_close(s1, y0.sum(1), rtol=0, atol=0)
     fused_ref.check(y1, g, fused_ref.reference(g, x, W, "sum", True, b), f"fork {fork}")
+
+
+@pytest.mark.parametrize("weighted", [True, False])
+def test_device_records_equal_host_restatement(weighted, dev):
+    """kgx_tiny_pack / kgx_schedule_suffixes (the device build of the tail
+    records and suffix starts) == tiny.py's torch restatement on the same
+    schedule moved to the host, bit for bit."""
+    from types import SimpleNamespace
+
+    from keras_geometric_amd import graph as G
+    from keras_geometric_amd import tiny as T
+
+    g, _ = _graph(dev, n=20_000, e=60_000, self_loops=True, gcn_norm=weighted)
+    pack, tw, start, n2 = T.tiny_pack(g, refresh=True)
+    assert pack is not None and pack.is_cuda
+    h = SimpleNamespace(items=g.items.cpu(), n_items=g.n_items, n_long=g.n_long, col=g.col.cpu(),
+                        w=g.w.cpu() if g.w is not None else None)
+    hp, htw, hstart, hn2 = T.tiny_pack(h)
+    assert (start, n2) == (hstart, hn2)
+    assert torch.equal(pack.cpu(), hp)
+    assert (tw is None) == (htw is None) and (tw is None or torch.equal(tw.cpu(), htw))
+    assert G.short_suffix_start(g.items) == G.short_suffix_start(g.items.cpu())
+    assert T.tiny_suffix_start(g.items) == T.tiny_suffix_start(g.items.cpu())
