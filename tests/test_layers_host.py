@@ -70,7 +70,23 @@ def test_cache_key_tracks_version():
     k1 = G.cache_key(t, 1)
     t[0, 0] = 1
     assert G.cache_key(t, 1) != k1
-    assert G.cache_key(np.zeros((2, 4)), 1) is None
+    assert G.cache_key([[0, 1], [1, 2]], 1) is None  # a list becomes a new array on every call
+
+
+def test_host_array_key():
+    """A numpy edge_index is keyed like the reference's id()-keyed cast cache
+    (message_passing.py:256-268), plus its address, shape, strides, dtype and a
+    sampled fingerprint: the same array keys the same, an in-place change in
+    the sampled positions or a different array does not."""
+    a = np.arange(20_000, dtype=np.int64).reshape(2, -1)
+    k = G.cache_key(a, 1)
+    assert k is not None and k == G.cache_key(a, 1)
+    assert G.cache_key(a, 2) != k
+    a[:] = a[:, ::-1].copy()
+    assert G.cache_key(a, 1) != k
+    b = a.copy()
+    assert G.cache_key(b, 1) != G.cache_key(a, 1)  # another array (id and address)
+    assert G.host_array_key(torch.zeros(2, 3)) is None
 
 
 def test_fused_shape_routing(monkeypatch):
