@@ -936,21 +936,19 @@ class _AggregateTransformFn(torch.autograd.Function):
         x, W, P = ctx.saved_tensors
         grad_out = grad_out.contiguous()
         g_x = g_W = g_b = None
-        side = None
-        if ctx.needs_input_grad[1]:  # dW = P^T dOut and db = colsum(dOut) in one pass (kgx_gemm_tn)
-            if ctx.needs_input_grad[0] and grad_out.is_cuda and _tn_overlap():
-                # on a side stream, beside the dx pass below: the dx op is gather-bound with its
-                # matrix cores mostly idle, kgx_gemm_tn streams P and dOut once through them
-                side = _side_stream(grad_out.device)
-                cur = torch.cuda.current_stream(grad_out.device)
-                side.wait_stream(cur)
-                with torch.cuda.stream(side):
-                    g_W, g_b = gemm_tn(P, grad_out, with_db=ctx.needs_input_grad[2])
-                P.record_stream(side)
-                grad_out.record_stream(side)
-            else:
-                g_W, g_b = gemm_tn(P, grad_out, with_db=ctx.needs_input_grad[2])
-        elif ctx.needs_input_grad[2]:
+        # dW / db (kgx_gemm_tn) beside the dx pass: the side stream waits for an event recorded
+        # here, before dx is launched, and is forked after it, so dx's blocks are dispatched first;
+        # W^T is copied before the event (queued after it, the small copy waited for the whole
+        # dW pass: its waves found no registers free beside kgx_gemm_tn's, profiles/r06/train/)
+        overlap = ctx.needs_input_grad[1] and ctx.needs_input_grad[0] and grad_out.is_cuda and _tn_overlap()
+        W_t = W.t().contiguous() if ctx.needs_input_grad[0] else None  # before the fork: see above
+        start = None
+        if overlap:
+            start = torch.cuda.Event()
+            start.record()
+        if not overlap and ctx.needs_input_grad[1]:  # dW = P^T dOut and db = colsum(dOut) in one pass
+            g_W, g_b = gemm_tn(P, grad_out, with_db=ctx.needs_input_grad[2])
+        elif not ctx.needs_input_grad[1] and ctx.needs_input_grad[2]:
             g_b = grad_out.sum(0)
         if ctx.needs_input_grad[0]:
             f_out, f_in = W.shape[1], W.shape[0]
@@ -961,19 +959,24 @@ class _AggregateTransformFn(torch.autograd.Function):
                     count = torch.clamp(ctx.g.deg, max=1 << 24).float()
                     d = (grad_out / torch.clamp(count, min=1e-8).unsqueeze(1)).contiguous()
                 t = G.transpose(ctx.g)
-                g_x = _aggregate_transform_raw(t, d, W.t().contiguous(), nat.SUM, ctx.weighted, None, False, 1.0,
-                                               ctx.exact)
+                g_x = _aggregate_transform_raw(t, d, W_t, nat.SUM, ctx.weighted, None, False, 1.0, ctx.exact)
             else:
-                dP = grad_out @ W.t()
+                dP = grad_out @ W_t
                 g_x = _reduce_backward(ctx.g, ctx.red, ctx.weighted, False, x, dP, ctx.exact, ctx.x_rows)
                 if ctx.pre_gin:
                     g_x = g_x + dP * ctx.gin_scale
-        if side is not None:  # join: dW / db are ready before anything later on this stream
+        if overlap:
             cur = torch.cuda.current_stream(grad_out.device)
-            cur.wait_stream(side)
-            for t in (g_W, g_b):
-                if t is not None:
-                    t.record_stream(cur)
+            side = _side_stream(grad_out.device)
+            side.wait_event(start)
+            with torch.cuda.stream(side):
+                g_W, g_b = gemm_tn(P, grad_out, with_db=ctx.needs_input_grad[2])
+            P.record_stream(side)
+            grad_out.record_stream(side)
+            cur.wait_stream(side)  # join: dW / db are ready before anything later on this stream
+            for t_ in (g_W, g_b):
+                if t_ is not None:
+                    t_.record_stream(cur)
         return g_x, g_W, g_b, None, None, None, None, None, None
 
 
