@@ -330,9 +330,11 @@ __global__ __launch_bounds__(kTnL, 1) void gemm_tn_lds_kernel(TnArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = kgx_f32x4_t{0.f, 0.f, 0.f, 0.f};
   float dbs[4] = {0.f, 0.f, 0.f, 0.f};
-  int bad = 0;
 
-  // one step's values -> the split planes of LDS buffer b
+  // one step's values -> the split planes of LDS buffer b.  No per-value check: a value the split
+  // does not represent exactly (inf, NaN, or |x| >= 0x1.ffp127, whose bf16 hi is inf) leaves an
+  // inf - inf or inf * 0 NaN, or an inf, in the planes, so every accumulator its row or column
+  // meets ends non-finite, and the block takes the slow path (checked once, after the loop)
   auto put = [&](const LoadSet& v, int b) {
     char* base = lds + b * kBufBytes;
 #pragma unroll
@@ -341,8 +343,6 @@ __global__ __launch_bounds__(kTnL, 1) void gemm_tn_lds_kernel(TnArgs a) {
 #pragma unroll
       for (int o = 0; o < 2; ++o) {  // P, then D
         const kgx_f32x4v_t x = o ? v.d[j] : v.p[j];
-        float sa = fabsf(x[0]) + fabsf(x[1]) + fabsf(x[2]) + fabsf(x[3]);
-        bad |= sa < 0x1.ffp127f ? 0 : 1;
         uint32_t h0, m0, l0, h1, m1, l1;
         split3_pair_rn(x[0], x[1], h0, m0, l0);
         split3_pair_rn(x[2], x[3], h1, m1, l1);
@@ -415,7 +415,16 @@ __global__ __launch_bounds__(kTnL, 1) void gemm_tn_lds_kernel(TnArgs a) {
   }
 
   float* part = a.part + (int64_t(blockIdx.x) * gridDim.y + tile) * kPart;
-  if (__syncthreads_or(bad)) {
+  float chk = 0.0f;  // non-finite iff some accumulator or column sum is (0 * inf and inf - inf: NaN)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) chk += 0.0f * acc[i][j][r];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) chk += 0.0f * dbs[e];
+  if (__syncthreads_or(chk != 0.0f)) {
     for (int o = t; o < kTile * kTile; o += kTnL) {
       const int64_t k = tk0 + o / kTile, m = tm0 + o % kTile;
       float sum = 0.0f;

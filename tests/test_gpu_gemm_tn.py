@@ -80,6 +80,25 @@ def test_gemm_tn_nonfinite(dev):
     assert torch.equal(torch.isinf(db), torch.isinf(rb))
 
 
+def test_gemm_tn_huge_finite(dev):
+    """A finite value whose bf16 rounding overflows (|x| >= 0x1.ffp127) is not split exactly: its
+    block takes the plain f32 path and the result stays finite and f32-accurate."""
+    gen = torch.Generator(device=dev).manual_seed(5)
+    N, K, M = 5000, 128, 128
+    P = torch.randn(N, K, device=dev, generator=gen)
+    D = torch.randn(N, M, device=dev, generator=gen)
+    P[250, 7] = 3.4e38  # bf16 RNE: inf
+    D[250] *= 1e-3
+    D[2600, 100] = -3.39e38  # bf16 RNE: the largest finite bf16
+    P[2600] *= 1e-3
+    dW, db = kops.gemm_tn(P, D, with_db=True)
+    ref = P.double().t() @ D.double()
+    mag = P.double().abs().t() @ D.double().abs()
+    assert bool(torch.isfinite(dW).all()) and bool(torch.isfinite(db).all())
+    assert bool(((dW.double() - ref).abs() <= 1e-5 * mag).all())
+    assert bool(((db.double() - D.double().sum(0)).abs() <= 1e-5 * D.double().abs().sum(0)).all())
+
+
 def test_gemm_tn_zero_rows(dev):
     P = torch.empty(0, 128, device=dev)
     D = torch.empty(0, 64, device=dev)
