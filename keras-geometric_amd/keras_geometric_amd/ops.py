@@ -993,9 +993,11 @@ def _side_stream(dev: torch.device) -> torch.cuda.Stream:
 
 
 def _tn_overlap() -> bool:
-    """KGX_TN_OVERLAP (default 1): the fused layers' dW / db pass (kgx_gemm_tn) runs on a side
-    stream beside the dx pass of the same backward; 0 runs it first on the current stream."""
-    return os.environ.get("KGX_TN_OVERLAP", "1") not in ("0", "", "false", "False")
+    """KGX_TN_OVERLAP (default 0): 1 runs the fused layers' dW / db pass (kgx_gemm_tn) on a side
+    stream beside the dx pass of the same backward.  Off by default: both passes stream HBM, and
+    side by side the dx pass's main kernel went 8.2 -> 13.9 ms for the 2.3 ms of dW it hid (NS
+    training step 21.7 ms serial against 21.8-24.4 overlapped, profiles/r06/train/overlap.md)."""
+    return os.environ.get("KGX_TN_OVERLAP", "0") not in ("0", "", "false", "False")
 
 
 def aggregate_transform(
