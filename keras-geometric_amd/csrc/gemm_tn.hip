@@ -467,6 +467,222 @@ __global__ __launch_bounds__(kTnL, 1) void gemm_tn_lds_kernel(TnArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// The warp-specialised form (default): the LDS form's two phases on separate
+// waves.  Waves 4-7 (producers, one per SIMD) load P and D three steps ahead,
+// split and write the planes of step s + 1; waves 0-3 (consumers, one per
+// SIMD) run step s's MFMAs -- 16 tiles of 16 x 16, a 64 x 64 block of dW per
+// wave -- so a SIMD issues the producer's VALU and LDS writes in its
+// consumer's MFMA gaps instead of after them, and each operand plane is read
+// from LDS by two consumers instead of two / four waves (96 KB of
+// transposed reads per step instead of 147).  One barrier per step hands a
+// buffer over, as in the LDS form; each role runs its own loop with the same
+// barrier count, so the producer's load waits stay partial.
+// ---------------------------------------------------------------------------
+constexpr int kPj = 4;  // float4 loads of P (and of D) per producer thread per step
+
+struct ProdSet {
+  kgx_f32x4v_t p[kPj], d[kPj];
+};
+
+__device__ __forceinline__ void prod_load(ProdSet& v, const TnArgs& a, int64_t s, int64_t s_end,
+                                          const uint32_t (&po)[kPj], const uint32_t (&dof)[kPj]) {
+  const int64_t n_end = s_end * kStep < a.N ? s_end * kStep : a.N;
+  const auto rp = step_rsrc(a.P, a.ldp, s, n_end);
+  const auto rd = step_rsrc(a.D, a.ldd, s, n_end);
+#pragma unroll
+  for (int j = 0; j < kPj; ++j) {
+    v.p[j] = __builtin_bit_cast(kgx_f32x4v_t, __builtin_amdgcn_raw_buffer_load_b128(rp, po[j], 0, 0));
+    v.d[j] = __builtin_bit_cast(kgx_f32x4v_t, __builtin_amdgcn_raw_buffer_load_b128(rd, dof[j], 0, 0));
+  }
+}
+
+__global__ __launch_bounds__(kTnL, 1) void gemm_tn_ws_kernel(TnArgs a) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * kBufBytes];  // two buffers of six planes: 96 KB
+  __shared__ float sdb[4][kTile];
+
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const bool producer = wave >= 4;
+  const int tile = blockIdx.y;
+  const int64_t tk0 = int64_t(tile / a.tiles_m) * kTile, tm0 = int64_t(tile % a.tiles_m) * kTile;
+  const int64_t s_lo = a.steps * blockIdx.x / gridDim.x, s_hi = a.steps * (blockIdx.x + 1) / gridDim.x;
+  const bool with_db = a.with_db && tk0 == 0;
+  const int64_t n_pad = (s_hi - s_lo + kSets - 1) / kSets * kSets;
+
+  auto barrier = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  kgx_f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = kgx_f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float dbs[4] = {0.f, 0.f, 0.f, 0.f};
+  // producer thread p: float4 q = p + 256 j of the step's [32][32] float4 grid -> node q >> 5, columns 4 (q & 31) ..
+  const int p = t & 255;
+  const int c4 = p & 31;
+
+  if (producer) {
+    int nrow[kPj];
+    uint32_t po[kPj], dof[kPj];
+#pragma unroll
+    for (int j = 0; j < kPj; ++j) {
+      nrow[j] = (p + 256 * j) >> 5;
+      const int64_t k = tk0 + 4 * c4, m = tm0 + 4 * c4;
+      po[j] = k < a.K ? uint32_t((nrow[j] * a.ldp + k) * 4) : 0x80000000u;
+      dof[j] = m < a.M ? uint32_t((nrow[j] * a.ldd + m) * 4) : 0x80000000u;
+    }
+    // one step's values -> the split planes of LDS buffer b (no per-value check: see the LDS form)
+    auto put = [&](const ProdSet& v, int b) {
+      char* base = lds + b * kBufBytes;
+#pragma unroll
+      for (int j = 0; j < kPj; ++j) {
+        const int off = swz(nrow[j], c4 >> 1) + 8 * (c4 & 1);
+#pragma unroll
+        for (int o = 0; o < 2; ++o) {  // P, then D
+          const kgx_f32x4v_t x = o ? v.d[j] : v.p[j];
+          uint32_t h0, m0, l0, h1, m1, l1;
+          split3_pair_rn(x[0], x[1], h0, m0, l0);
+          split3_pair_rn(x[2], x[3], h1, m1, l1);
+          char* pl = base + 3 * o * kPlaneBytes + off;
+          *reinterpret_cast<uint2*>(pl) = make_uint2(h0, h1);
+          *reinterpret_cast<uint2*>(pl + kPlaneBytes) = make_uint2(m0, m1);
+          *reinterpret_cast<uint2*>(pl + 2 * kPlaneBytes) = make_uint2(l0, l1);
+        }
+        if (with_db) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) dbs[e] = __fadd_rn(dbs[e], v.d[j][e]);
+        }
+      }
+    };
+    // steps padded to a multiple of four with steps that read 0; set (s - s_lo) % 4 holds step s
+    ProdSet v[kSets];
+    prod_load(v[0], a, s_lo, s_hi, po, dof);
+    prod_load(v[1], a, s_lo + 1, s_hi, po, dof);
+    prod_load(v[2], a, s_lo + 2, s_hi, po, dof);
+    put(v[0], 0);
+    barrier();
+    for (int64_t u0 = 0; u0 < n_pad; u0 += kSets) {
+#pragma unroll
+      for (int u = 0; u < kSets; ++u) {
+        prod_load(v[(u + 3) % kSets], a, s_lo + u0 + u + 3, s_hi, po, dof);
+        put(v[(u + 1) % kSets], (u + 1) & 1);  // the next step's planes
+        barrier();
+      }
+    }
+  } else {
+    // operand reads (ds_read_b64_tr_b16), as in the LDS form; wave w owns dW rows
+    // [64 (w >> 1), +64) and columns [64 (w & 1), +64)
+    const int gq = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+    const int kw0 = 64 * (wave >> 1), mw0 = 64 * (wave & 1);
+    auto rd_off = [&](int cb, int h) { return swz(8 * gq + 4 * h + qq, (cb >> 3) + (pp >> 1)) + 8 * (pp & 1); };
+    int offA[4][2], offB[4][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        offA[i][h] = rd_off(kw0 + 16 * i, h);
+        offB[i][h] = rd_off(mw0 + 16 * i, h);
+      }
+    auto mma = [&](int b) {
+      const char* base = lds + b * kBufBytes;
+      auto rd = [&](int plane, int off) {
+        return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_bf16x4_t*)(const_cast<char*>(base) + plane * kPlaneBytes + off));
+      };
+      auto operand = [&](int plane, const int (&off)[2]) {
+        const kgx_bf16x4_t lo = rd(plane, off[0]), hi = rd(plane, off[1]);
+        return kgx_bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      };
+      Planes B[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        B[j].hi = operand(3, offB[j]);
+        B[j].mid = operand(4, offB[j]);
+        B[j].lo = operand(5, offB[j]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        Planes A;
+        A.hi = operand(0, offA[i]);
+        A.mid = operand(1, offA[i]);
+        A.lo = operand(2, offA[i]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma6(A, B[j], acc[i][j]);
+      }
+    };
+    barrier();  // the producers' first planes
+    for (int64_t u0 = 0; u0 < n_pad; u0 += kSets) {
+#pragma unroll
+      for (int u = 0; u < kSets; ++u) {
+        mma(u & 1);
+        barrier();
+      }
+    }
+  }
+
+  float* part = a.part + (int64_t(blockIdx.x) * gridDim.y + tile) * kPart;
+  float chk = 0.0f;  // non-finite iff some accumulator or column sum is (0 * inf and inf - inf: NaN)
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) chk += 0.0f * acc[i][j][r];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) chk += 0.0f * dbs[e];
+  if (__syncthreads_or(chk != 0.0f)) {
+    for (int o = t; o < kTile * kTile; o += kTnL) {
+      const int64_t k = tk0 + o / kTile, m = tm0 + o % kTile;
+      float sum = 0.0f;
+      if (k < a.K && m < a.M)
+        for (int64_t n = s_lo * kStep; n < s_hi * kStep && n < a.N; ++n)
+          sum = __fadd_rn(sum, __fmul_rn(a.P[n * a.ldp + k], a.D[n * a.ldd + m]));
+      part[o] = sum;
+    }
+    if (with_db)
+      for (int o = t; o < kTile; o += kTnL) {
+        const int64_t m = tm0 + o;
+        float sum = 0.0f;
+        if (m < a.M)
+          for (int64_t n = s_lo * kStep; n < s_hi * kStep && n < a.N; ++n) sum = __fadd_rn(sum, a.D[n * a.ldd + m]);
+        part[kTile * kTile + o] = sum;
+      }
+    return;
+  }
+  if (!producer) {
+    // accumulator (i, j), element r: dW row kw0 + 16 i + 4 (lane >> 4) + r, column mw0 + 16 j + (lane & 15)
+    const int kw0 = 64 * (wave >> 1), mw0 = 64 * (wave & 1), gq = lane >> 4, cl = lane & 15;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) part[(kw0 + 16 * i + 4 * gq + r) * kTile + mw0 + 16 * j + cl] = acc[i][j][r];
+  }
+  if (with_db) {  // columns 4 c4 .. + 3: lanes l and l + 32 of a producer wave, then the 4 producer waves in order
+    if (producer) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dbs[e] = __fadd_rn(dbs[e], __shfl_xor(dbs[e], 32, 64));
+      if (lane < 32)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sdb[wave - 4][4 * c4 + e] = dbs[e];
+    }
+    __syncthreads();
+    if (t < kTile) {
+      float sum = 0.0f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) sum = __fadd_rn(sum, sdb[w][t]);
+      part[kTile * kTile + t] = sum;
+    }
+  }
+}
+
 // dW[k, m] = sum over blocks b (in order) of part[b][tile(k, m)][k % 128][m % 128]; db likewise
 __global__ void gemm_tn_finish_kernel(const float* __restrict__ part, int nb, int tiles, int tiles_m, int64_t K,
                                       int64_t M, float* __restrict__ dW, int64_t ld_dw, float* __restrict__ db) {
@@ -523,8 +739,12 @@ extern "C" int kgx_gemm_tn(int64_t N, const float* P, int64_t ldp, int64_t K, co
   const int nb = gemm_tn_blocks(N);
   if (N > 0) {
     TnArgs a{P, D, static_cast<float*>(workspace), N, ldp, ldd, K, M, (N + kStep - 1) / kStep, tiles_m, db ? 1 : 0};
-    const char* e = getenv("KGX_TN_LDS");  // measurement A/B: 0 = the per-wave split form
-    if ((!e || atoi(e) != 0) && K % 4 == 0 && M % 4 == 0) {
+    // measurement A/B: KGX_TN_LDS 0 = the per-wave split form, 1 = the LDS form, 2 (default) = warp-specialised
+    const char* e = getenv("KGX_TN_LDS");
+    const int form = e ? atoi(e) : 2;
+    if (form == 2 && K % 4 == 0 && M % 4 == 0) {
+      hipLaunchKernelGGL(gemm_tn_ws_kernel, dim3(nb, tiles), dim3(kTnL), 0, s, a);
+    } else if (form != 0 && K % 4 == 0 && M % 4 == 0) {
       hipLaunchKernelGGL(gemm_tn_lds_kernel, dim3(nb, tiles), dim3(kTnL), 0, s, a);
     } else {
       hipLaunchKernelGGL(gemm_tn_kernel, dim3(nb, tiles), dim3(kTn), 0, s, a);
