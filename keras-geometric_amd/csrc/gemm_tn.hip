@@ -8,6 +8,11 @@
 // split-K batched fp32 GEMM, then D.sum(0) as a second pass) read D twice and
 // ran the fp32 GEMM at ~2 TB/s (NS: 5.2 ms of a 24.5 ms training step).
 //
+// Three forms (kgx_gemm_tn picks by KGX_TN_LDS): gemm_tn_ws_kernel (default,
+// below: producer waves split into LDS, consumer waves run the MFMAs),
+// gemm_tn_lds_kernel (the same two phases on every wave in turn) and
+// gemm_tn_kernel (every wave splits its own operands, described first).
+//
 // Layout: the reduction runs over the node dimension n, which is the stored
 // row index of both operands, so the MFMA's K dimension is n.  For
 // v_mfma_f32_16x16x32_bf16, lane l supplies A[l % 16][8 (l / 16) + t] and
