@@ -416,8 +416,6 @@ def main() -> None:
 
     kops.EVENT_SINK = []
     split0 = kops.CU_SPLIT_LAUNCHES
-    if world > 1:
-        sg.link_probe = []  # every exchange step's pack-to-landing time (ShardedGraph.link_report)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -500,8 +498,16 @@ def main() -> None:
             "aggregation_ms": kern_ms, "launches_per_step": launches, "algorithmic_bytes": balg,
             "roofline_achieved_GBps": achieved, "roofline_frac": achieved / HBM_PEAK_GBS, **shard_info}
     if world > 1:
+        # every exchange step's pack-to-landing time (ShardedGraph.link_report), in a few extra
+        # steps after the timed ones: the probe's timing events and stream waits cost ~3 % of a
+        # step (tools/shard_sim.py --link-probe, profiles/r06/probe/), so they stay out of `value`
+        n_probe = min(args.steps, 5)
+        sg.link_probe = []
+        for _ in range(n_probe):
+            step()
         torch.cuda.synchronize()
-        links = sg.link_report(args.steps)
+        links = sg.link_report(n_probe)
+        mine["link_probe_steps"] = n_probe
         mine["links"] = links
         mine["link_measured_ms_sum"] = sum(r["measured_ms"] for r in links)
         mine["link_modelled_ms_sum_at_400GBps"] = sum(r["modelled_ms_at_400GBps"] for r in links)

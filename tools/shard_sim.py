@@ -200,6 +200,9 @@ def main():
                          "with --link-gbps 0 the step is the rank's compute alone; with a link rate the "
                          "modelled transfer time stands for RCCL's receive (default: a loopback device copy "
                          "per exchange, after the modelled link time)")
+    ap.add_argument("--link-probe", action="store_true",
+                    help="time every exchange step's pack-to-landing in the timed steps as bench.py does at "
+                         "N > 1 (ShardedGraph.link_probe / link_report) and add it to the JSON line")
     args = ap.parse_args()
     layer_kind, n_cfg, e_cfg, F, scaling = CONFIGS[args.config]
     n_cfg = args.nodes or n_cfg
@@ -302,12 +305,16 @@ def main():
                                       "env": {k: v for k, v in os.environ.items() if k.startswith("KGX_")}}),
                           flush=True)
                 kops.EVENT_SINK = []
+                if args.link_probe:
+                    sg.link_probe = []
                 t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 t0.record()
                 for _ in range(args.steps):
                     layer(x)
                 t1.record()
                 torch.cuda.synchronize()
+                links = sg.link_report(args.steps) if args.link_probe else None
+                sg.link_probe = None
             ev = kops.EVENT_SINK
             kops.EVENT_SINK = None
             per = len(ev) // args.steps
@@ -327,6 +334,7 @@ def main():
                                    else "loopback-copy") + ("" if args.link_gbps <= 0 or not comm.free_exchange
                                                             else ", no local copy"), "step_ms": round(t0.elapsed_time(t1) / args.steps, 3),
                 "launch_ms": [round(v, 3) for v in launch_ms],
+                **({"links": links} if links is not None else {}),
                 "own_edges": g_own.kept, "chunk_edges": [g.kept for g in g_chunks],
                 "halo_rows_pull_only": sg.n_halo, "halo_rows": pp.n_rows if pp else sg.n_halo,
                 "received_MB": recv_rows * F * 4 / 1e6,
