@@ -363,13 +363,31 @@ def halo_first_frac() -> float | None:
     return f
 
 
-def chunk_slice(count: int, k: int, K: int, first: float | None = None) -> tuple[int, int]:
+def halo_chunk_weights(K: int) -> tuple | None:
+    """KGX_HALO_WEIGHTS (measurement): K comma-separated relative sizes of the
+    push-pull plan's slice chunks (e.g. "1,4,1": small first and last chunks).
+    Applied only when it names exactly K positive weights; overrides
+    KGX_HALO_FIRST.  Unset: None."""
+    v = os.environ.get("KGX_HALO_WEIGHTS")
+    if not v or K <= 1:
+        return None
+    w = tuple(float(t) for t in v.split(","))
+    if len(w) != K or any(t <= 0 for t in w):
+        return None
+    return w
+
+
+def chunk_slice(count: int, k: int, K: int, first: float | tuple | None = None) -> tuple[int, int]:
     """[a, b) of chunk k of a list of `count` rows cut K ways: evenly
-    (floor(count k / K)), or with chunk 0 holding floor(count * first) rows and
-    chunks 1..K-1 splitting the rest evenly.  Requester and owner compute it
+    (floor(count k / K)); with chunk 0 holding floor(count * first) rows and
+    chunks 1..K-1 splitting the rest evenly; or, `first` a tuple of K weights,
+    at the weights' cumulative fractions.  Requester and owner compute it
     from the same count, so both sides agree on every chunk."""
     if first is None or K == 1:
         return count * k // K, count * (k + 1) // K
+    if isinstance(first, tuple):
+        tot = sum(first)
+        return int(count * (sum(first[:k]) / tot)), (count if k == K - 1 else int(count * (sum(first[:k + 1]) / tot)))
     f = int(count * first)
     if k == 0:
         return 0, f
@@ -607,6 +625,8 @@ class ShardedGraph:
         if self._pp_by_k is None:
             self._pp_by_k = {}
         first = halo_first_frac() if K > 1 else None
+        if not groups and halo_chunk_weights(K) is not None:
+            first = halo_chunk_weights(K)
         key = ("group" if groups else ("pull" if pull_only else "halo"), K, weighted, first)
         if key in self._pp_by_k:
             self._pp = self._pp_by_k[key]
