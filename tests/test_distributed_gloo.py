@@ -903,6 +903,20 @@ def test_chunk_slice_bounds():
                 if first is not None and K > 1:
                     assert cuts[0][1] == int(count * first)
     assert kd.chunk_slice(10, 1, 4) == (2, 5)
+    for count in (0, 1, 7, 100, 12345):  # KGX_HALO_WEIGHTS: K relative sizes
+        for w in ((1.0, 4.0, 1.0), (2.0, 1.0), (1.0, 3.0, 3.0, 1.0)):
+            cuts = [kd.chunk_slice(count, k, len(w), w) for k in range(len(w))]
+            assert cuts[0][0] == 0 and cuts[-1][1] == count
+            assert all(a <= b for a, b in cuts) and all(cuts[k][1] == cuts[k + 1][0] for k in range(len(w) - 1))
+    assert [kd.chunk_slice(1000, k, 3, (1.0, 4.0, 1.0)) for k in range(3)] == [(0, 166), (166, 833), (833, 1000)]
+
+
+def test_halo_chunk_weights_env(monkeypatch):
+    monkeypatch.setenv("KGX_HALO_WEIGHTS", "1,4,1")
+    assert kd.halo_chunk_weights(3) == (1.0, 4.0, 1.0)
+    assert kd.halo_chunk_weights(2) is None  # names K weights or is ignored
+    monkeypatch.setenv("KGX_HALO_WEIGHTS", "1,0,1")
+    assert kd.halo_chunk_weights(3) is None
 
 
 def _train_gin_sage_worker(rank, world, port, q):
