@@ -667,6 +667,16 @@ inline int cu_split_per32() {
   return v > 0 && v < 32 ? v : 0;
 }
 
+// KGX_F256_MID_TAIL (per mille, read per launch; default 200): the share of the degree 3..7
+// rows a split launch runs on the tail's CUs after the degree <= 2 tail instead of on the
+// head's.  C4 (interleaved, three rounds, profiles/r06/c4_balance/): 0 20.01-20.07 ms, 150
+// 19.69-19.70, 200 19.52-19.61, 250 19.49-19.65, 300 19.99-20.17 (the tail leg then longer)
+inline int mid_tail_permille() {
+  const char* e = getenv("KGX_F256_MID_TAIL");
+  const int v = e ? atoi(e) : 200;
+  return v < 0 ? 0 : (v > 1000 ? 1000 : v);
+}
+
 template <int RED, bool WT, bool TWO>
 int launch256(const F256Args& a, hipStream_t s) {
   const int64_t work = a.items ? a.n_work : a.n_rows;
@@ -697,10 +707,13 @@ int launch256(const F256Args& a, hipStream_t s) {
     hipLaunchKernelGGL(k, dim3(grid256(k, (n_long + kRows - 1) / kRows, cus_h)), dim3(kThreads), 0, sh, b);
     KGX_CHECK_LAUNCH();
   }
-  if (work > n_long) {
+  // split: the last mid_tail / 1000 of the degree 3..7 rows (the lowest degrees) go to the
+  // tail's CUs after the degree <= 2 tail, balancing the two legs
+  const int64_t n_cut = (sh != st && work > n_long) ? work - (work - n_long) * mid_tail_permille() / 1000 : work;
+  if (n_cut > n_long) {
     F256Args b = a;
     b.items = a.items + n_long;
-    b.n_work = work - n_long;
+    b.n_work = n_cut - n_long;
     auto k = spmm_gemm256_kernel<RED, WT, kMidPF, TWO>;
     hipLaunchKernelGGL(k, dim3(grid256(k, (b.n_work + kRows - 1) / kRows, cus_h)), dim3(kThreads), 0, sh, b);
     KGX_CHECK_LAUNCH();
@@ -712,6 +725,14 @@ int launch256(const F256Args& a, hipStream_t s) {
                  : (fast ? spmm_gemm256_tiny2_kernel<RED, WT, false, true, TWO>
                          : spmm_gemm256_tiny2_kernel<RED, WT, false, false, TWO>);
     hipLaunchKernelGGL(k, dim3(grid256(k, (a.n_tiny + kRows - 1) / kRows, cus_t)), dim3(kThreads), 0, st, a);
+    KGX_CHECK_LAUNCH();
+  }
+  if (work > n_cut) {
+    F256Args b = a;
+    b.items = a.items + n_cut;
+    b.n_work = work - n_cut;
+    auto k = spmm_gemm256_kernel<RED, WT, kMidPF, TWO>;
+    hipLaunchKernelGGL(k, dim3(grid256(k, (b.n_work + kRows - 1) / kRows, cus_t)), dim3(kThreads), 0, st, b);
     KGX_CHECK_LAUNCH();
   }
   if (join.cs) {  // the fix-up reads the long launch's partials: join first

@@ -274,13 +274,14 @@ def test_fused256_two_tables_bit_identical(dev, weighted, gin):
         assert torch.equal(a1, a2)
 
 
-@pytest.mark.parametrize("per32", ["3", "8", "16"])
-def test_fused256_cu_split_bit_identical(dev, monkeypatch, per32):
+@pytest.mark.parametrize("per32,mid_tail", [("3", "0"), ("8", "0"), ("16", "0"), ("8", "250"), ("8", "1000")])
+def test_fused256_cu_split_bit_identical(dev, monkeypatch, per32, mid_tail):
     """KGX_F256_CU_SPLIT: the degree <= 2 tail on a CU-masked stream beside the
     long-row and degree 3..7 launches on the other CUs (forked from and joined
     back into the caller's stream) gives the one-stream bits -- FAST tail (GIN,
     F_out 256), weighted non-FAST tail (F_out 128, accumulate), two tables, hub
-    fix-up after the join -- and joins before the caller reads the output."""
+    fix-up after the join -- and joins before the caller reads the output;
+    KGX_F256_MID_TAIL moves the last of the degree 3..7 rows to the tail's CUs."""
     N, H, E = 30000, 8000, 90000
     rng = np.random.default_rng(23)
     s, d = rmat_edges(5, scale_for(N + H), N + H, 0, E)
@@ -306,7 +307,9 @@ def test_fused256_cu_split_bit_identical(dev, monkeypatch, per32):
     monkeypatch.setenv("KGX_F256_CU_SPLIT", "0")
     ref = run()
     monkeypatch.setenv("KGX_F256_CU_SPLIT", per32)
+    monkeypatch.setenv("KGX_F256_MID_TAIL", mid_tail)
     for _ in range(2):
         got = run()
         for a_, b_ in zip(got, ref):
             assert torch.equal(a_, b_)
+
