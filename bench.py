@@ -503,10 +503,14 @@ def main() -> None:
         # step (tools/shard_sim.py --link-probe, profiles/r06/probe/), so they stay out of `value`
         n_probe = min(args.steps, 5)
         sg.link_probe = []
-        for _ in range(n_probe):
-            step()
-        torch.cuda.synchronize()
-        links = sg.link_report(n_probe)
+        try:  # a diagnostic: it must never cost the measured line
+            for _ in range(n_probe):
+                step()
+            torch.cuda.synchronize()
+            links = sg.link_report(n_probe)
+        except Exception as exc:  # noqa: BLE001 -- every rank runs the same code, so all fail alike
+            links = []
+            mine["link_probe_error"] = f"{type(exc).__name__}: {exc}"[:300]
         mine["link_probe_steps"] = n_probe
         mine["links"] = links
         mine["link_measured_ms_sum"] = sum(r["measured_ms"] for r in links)
