@@ -192,6 +192,24 @@ class sharing_gpu:
         _SHARE.on = self._old
 
 
+_NOSPLIT = threading.local()
+
+
+class _unsplit:
+    """CU-split launches off inside (per host thread): the training backward's
+    transposed pass.  There the split measured slower -- NS training step 21.40-21.62
+    ms split against 20.69-20.79 one-stream, the dx pass 9.12-9.18 against 8.79-8.82
+    (profiles/r06/train/split_ab/) -- while the inference forward gains from it.
+    KGX_BWD_CU_SPLIT=1 keeps the split (measurement)."""
+
+    def __enter__(self):
+        self._old = getattr(_NOSPLIT, "on", False)
+        _NOSPLIT.on = os.environ.get("KGX_BWD_CU_SPLIT") != "1"
+
+    def __exit__(self, *exc):
+        _NOSPLIT.on = self._old
+
+
 def _tiny_abi(items, n_items, n_long, tpack, tw, n_short_end, n_tiny2):
     """(n_short_end, tpack, tw, n_tiny2) arguments of kgx_spmm_gemm_ex2."""
     if items is None or tpack is None or not (n_long <= n_short_end <= n_items):
@@ -300,6 +318,8 @@ def _split_allowed(dev: torch.device | None = None) -> bool:
     validated one, and for a tensor on another device than the current one (the
     library would run it unsplit)."""
     if _share_gpu() and os.environ.get("KGX_CU_SPLIT_SHARED") != "1":
+        return False
+    if getattr(_NOSPLIT, "on", False):
         return False
     if dev is not None and dev.type == "cuda" and dev.index is not None and dev.index != torch.cuda.current_device():
         return False
@@ -951,20 +971,21 @@ class _AggregateTransformFn(torch.autograd.Function):
         elif not ctx.needs_input_grad[1] and ctx.needs_input_grad[2]:
             g_b = grad_out.sum(0)
         if ctx.needs_input_grad[0]:
-            f_out, f_in = W.shape[1], W.shape[0]
-            if ctx.red in (nat.SUM, nat.MEAN) and not ctx.pre_gin and fused_transform_supported(f_out, f_in):
-                # dx = A^T (dOut W^T) = (A^T dOut) W^T: the same fused kernel on the transposed graph
-                d = grad_out
-                if ctx.red == nat.MEAN:
-                    count = torch.clamp(ctx.g.deg, max=1 << 24).float()
-                    d = (grad_out / torch.clamp(count, min=1e-8).unsqueeze(1)).contiguous()
-                t = G.transpose(ctx.g)
-                g_x = _aggregate_transform_raw(t, d, W_t, nat.SUM, ctx.weighted, None, False, 1.0, ctx.exact)
-            else:
-                dP = grad_out @ W_t
-                g_x = _reduce_backward(ctx.g, ctx.red, ctx.weighted, False, x, dP, ctx.exact, ctx.x_rows)
-                if ctx.pre_gin:
-                    g_x = g_x + dP * ctx.gin_scale
+            with _unsplit():  # the transposed pass one-stream (see _unsplit)
+                f_out, f_in = W.shape[1], W.shape[0]
+                if ctx.red in (nat.SUM, nat.MEAN) and not ctx.pre_gin and fused_transform_supported(f_out, f_in):
+                    # dx = A^T (dOut W^T) = (A^T dOut) W^T: the same fused kernel on the transposed graph
+                    d = grad_out
+                    if ctx.red == nat.MEAN:
+                        count = torch.clamp(ctx.g.deg, max=1 << 24).float()
+                        d = (grad_out / torch.clamp(count, min=1e-8).unsqueeze(1)).contiguous()
+                    t = G.transpose(ctx.g)
+                    g_x = _aggregate_transform_raw(t, d, W_t, nat.SUM, ctx.weighted, None, False, 1.0, ctx.exact)
+                else:
+                    dP = grad_out @ W_t
+                    g_x = _reduce_backward(ctx.g, ctx.red, ctx.weighted, False, x, dP, ctx.exact, ctx.x_rows)
+                    if ctx.pre_gin:
+                        g_x = g_x + dP * ctx.gin_scale
         if overlap:
             cur = torch.cuda.current_stream(grad_out.device)
             side = _side_stream(grad_out.device)

@@ -63,6 +63,23 @@ def test_split_off_while_sharing(monkeypatch):
     assert ops._split_allowed()
 
 
+def test_split_off_in_the_backward_pass(monkeypatch):
+    """The training backward's transposed pass runs one-stream (ops._unsplit), unless
+    KGX_BWD_CU_SPLIT=1; the flag is restored on exit, nested or not."""
+    monkeypatch.delenv("KGX_CU_SPLIT_SHARED", raising=False)
+    monkeypatch.delenv("KGX_BWD_CU_SPLIT", raising=False)
+    assert ops._split_allowed()
+    with ops._unsplit():
+        assert not ops._split_allowed()
+        with ops._unsplit():
+            assert not ops._split_allowed()
+        assert not ops._split_allowed()
+    assert ops._split_allowed()
+    monkeypatch.setenv("KGX_BWD_CU_SPLIT", "1")
+    with ops._unsplit():
+        assert ops._split_allowed()
+
+
 def test_sharing_flag_is_per_thread():
     """Threaded ranks (one process) enter and leave their passes' sharing_gpu
     contexts in any interleaving: the flag is per host thread, so no thread's
