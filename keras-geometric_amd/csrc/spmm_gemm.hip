@@ -919,6 +919,14 @@ int launch(const FusedArgs& a, hipStream_t s) {
       const int64_t cap = a.share_gpu ? shared_cap(full) : full;
       hipLaunchKernelGGL(k, dim3(unsigned(need < cap ? need : cap)), dim3(kThreads), 0, cs->head, a);
       KGX_CHECK_LAUNCH();
+      if (a.items && a.n_split > 0) {
+        // the hub fix-up reads only the main kernel's partials and writes only split rows:
+        // on the head's CUs right after it, hidden behind the longer tail leg
+        const int64_t blocks = (a.n_split + 7) / 8;
+        auto fk = spmm_gemm_fixup_kernel<RED, NARROW>;
+        hipLaunchKernelGGL(fk, dim3(unsigned(blocks < 4096 ? blocks : 4096)), dim3(256), 0, cs->head, a);
+        KGX_CHECK_LAUNCH();
+      }
       if (has_short && launch_short<RED, W, TWO, NARROW>(a, cs->tail, cs->n_tail) != KGX_OK) return KGX_ERR_HIP;
       if (a.tpack && a.n_tiny > 0 && launch_tiny<RED, W, TWO, NARROW>(a, cs->tail, cs->n_tail) != KGX_OK)
         return KGX_ERR_HIP;
@@ -927,12 +935,6 @@ int launch(const FusedArgs& a, hipStream_t s) {
       KGX_CHECK_HIP(hipEventRecord(cs->jt, cs->tail));
       KGX_CHECK_HIP(hipStreamWaitEvent(s, cs->jh, 0));
       KGX_CHECK_HIP(hipStreamWaitEvent(s, cs->jt, 0));
-      if (a.items && a.n_split > 0) {
-        const int64_t blocks = (a.n_split + 7) / 8;
-        auto fk = spmm_gemm_fixup_kernel<RED, NARROW>;
-        hipLaunchKernelGGL(fk, dim3(unsigned(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s, a);
-        KGX_CHECK_LAUNCH();
-      }
       return KGX_OK;
     }
   }
