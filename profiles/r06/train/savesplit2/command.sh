@@ -1,5 +1,5 @@
 # Round 6: with the backward's dx pass one-stream, the training forward (P kept) CU-split
-# (KGX_SAVE_CU_SPLIT=1, measurement) against one-stream (default).
+# (KGX_SAVE_CU_SPLIT=1, a temporary ops.py switch, not in the tree) against one-stream (default).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
