@@ -1,4 +1,5 @@
 # Round 6: kgx_gemm_tn LDS form with and without the wave stagger (KGX_TN_STAGGER), register form.
+# (KGX_TN_STAGGER was a temporary kernel variant, measured slower and removed; DESIGN.md §4 kgx_gemm_tn)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp

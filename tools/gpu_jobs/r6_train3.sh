@@ -1,4 +1,5 @@
 # Round 6: the NS training step, serial dW (the default now), with the forward-with-P launch
+# (KGX_SAVE_CU_SPLIT was a temporary ops.py switch, not in the tree; result in DESIGN.md, verdict item 7)
 # CU-split (KGX_SAVE_CU_SPLIT=1) or not, and a kernel trace of the default.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
