@@ -77,6 +77,16 @@ const char* kgx_last_error(void);
  * ------------------------------------------------------------------------- */
 int kgx_cu_split_layout_ok(int cus, int xccs, const char* arch);
 int kgx_cu_split_supported(int device);
+/* Census of the CU-masked streams a split launch uses (a diagnostic the tests run):
+ * n_blocks short blocks on the head stream and n_blocks on the tail stream of
+ * cu_split(per32) each record where they ran, (XCC id << 8) | (SE id << 5) |
+ * (SH id << 4) | CU id from the hardware registers, into head_ids[n_blocks] and
+ * tail_ids[n_blocks]; n_cus[0] / n_cus[1] = the head / tail CU counts the split
+ * believes its masks hold.  Synchronises the caller's stream.  KGX_ERR_UNSUPPORTED
+ * when the device has no validated split layout.  Checks that the masks are
+ * disjoint and cover what they claim (tests/test_gpu_cu_census.py). */
+int kgx_cu_split_census(int per32, int64_t n_blocks, int32_t* head_ids, int32_t* tail_ids, int* n_cus,
+                        kgx_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Graph preparation: COO int32 [2,E] (generation order, unsorted) -> CSR by

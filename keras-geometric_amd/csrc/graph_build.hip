@@ -792,6 +792,47 @@ extern "C" int kgx_cu_split_supported(int device) {
   return cu_split_device_ok(device) ? 1 : 0;
 }
 
+namespace kgx {
+namespace {
+// where block b ran: (XCC << 8) | (SE << 5) | (SH << 4) | CU, from HW_REG_HW_ID (gfx9 layout:
+// CU_ID [11:8], SH_ID [12], SE_ID [15:13]) and HW_REG_XCC_ID; each block stays ~20 us so the
+// dispatcher spreads the grid over every CU its stream's mask allows
+__global__ void cu_census_kernel(int32_t* __restrict__ ids, int64_t n) {
+  unsigned hw, xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  const int64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < 2000) __builtin_amdgcn_s_sleep(8);  // 100 MHz ticks: ~20 us
+  if (threadIdx.x == 0 && int64_t(blockIdx.x) < n)
+    ids[blockIdx.x] = int32_t(((xcc & 0xf) << 8) | (((hw >> 13) & 7) << 5) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 0xf));
+}
+}  // namespace
+}  // namespace kgx
+
+extern "C" int kgx_cu_split_census(int per32, int64_t n_blocks, int32_t* head_ids, int32_t* tail_ids, int* n_cus,
+                                   kgx_stream_t stream_) {
+  KGX_REQUIRE(per32 > 0 && per32 < 32 && n_blocks > 0 && n_blocks <= (1 << 20) && head_ids && tail_ids && n_cus,
+              KGX_ERR_ARG, "kgx_cu_split_census: bad arguments");
+  hipStream_t s = as_stream(stream_);
+  CuSplit* cs = cu_split(per32, s);
+  KGX_REQUIRE(cs != nullptr, KGX_ERR_UNSUPPORTED, "kgx_cu_split_census: no CU split on this device / stream");
+  KGX_CHECK_HIP(hipEventRecord(cs->fork, s));
+  KGX_CHECK_HIP(hipStreamWaitEvent(cs->head, cs->fork, 0));
+  KGX_CHECK_HIP(hipStreamWaitEvent(cs->tail, cs->fork, 0));
+  hipLaunchKernelGGL(cu_census_kernel, dim3(unsigned(n_blocks)), dim3(64), 0, cs->head, head_ids, n_blocks);
+  KGX_CHECK_LAUNCH();
+  hipLaunchKernelGGL(cu_census_kernel, dim3(unsigned(n_blocks)), dim3(64), 0, cs->tail, tail_ids, n_blocks);
+  KGX_CHECK_LAUNCH();
+  KGX_CHECK_HIP(hipEventRecord(cs->jh, cs->head));
+  KGX_CHECK_HIP(hipEventRecord(cs->jt, cs->tail));
+  KGX_CHECK_HIP(hipStreamWaitEvent(s, cs->jh, 0));
+  KGX_CHECK_HIP(hipStreamWaitEvent(s, cs->jt, 0));
+  KGX_CHECK_HIP(hipStreamSynchronize(s));
+  n_cus[0] = cs->n_head;
+  n_cus[1] = cs->n_tail;
+  return KGX_OK;
+}
+
 // ---------------------------------------------------------------------------
 // Schedule tails (graph.short_suffix_start / tiny.tiny_suffix_start) and the
 // tiny-row records (tiny.tiny_pack) on the device: one pass each instead of a

@@ -58,6 +58,7 @@ _SIGNATURES = {
     "kgx_gemm_tn": [_i64, _f32p, _i64, _i64, _f32p, _i64, _i64, _f32p, _i64, _f32p, ctypes.c_void_p,
                     ctypes.c_size_t, ctypes.c_void_p],
     "kgx_cu_split_supported": [_int],
+    "kgx_cu_split_census": [_int, _i64, _i32p, _i32p, ctypes.POINTER(ctypes.c_int), ctypes.c_void_p],
     "kgx_gcn_dinv_table": [_i32p, _i64, _f32p, _i64, _f32p, ctypes.c_void_p],
     "kgx_gcn_edge_norm": [_i32p, _i32p, _i64, _f32p, _f32p, _f32p, ctypes.c_void_p],
     "kgx_schedule_workspace_bytes": [_i64, ctypes.POINTER(ctypes.c_size_t)],
