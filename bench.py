@@ -99,6 +99,22 @@ def pmc_traffic(config: str, kernels) -> tuple[float | None, str | None]:
     return None, None
 
 
+def pmc_step_traffic(name: str) -> tuple[float | None, str | None]:
+    """HBM bytes per training step (profiles/r*/pmc_<name>.json, tools/pmc_step.py),
+    used only when every kernel of the step was profiled from the sources being run."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("pmc_summary", ROOT / "tools" / "pmc_summary.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    for path in sorted(ROOT.glob(f"profiles/r*/pmc_{name}.json"), reverse=True):
+        d = json.loads(path.read_text())
+        ks = d.get("kernels", {})
+        if ks and all(v.get("source_hash") == mod.kernel_source_hash(k) for k, v in ks.items()):
+            return d["traffic_bytes_per_step"], str(path.relative_to(ROOT))
+    return None, None
+
+
 def log(msg: str) -> None:
     r = int(os.environ.get("RANK", "0"))
     if r == 0 or int(os.environ.get("WORLD_SIZE", "1")) > 1:  # N > 1: every rank reports its own progress
@@ -448,7 +464,8 @@ def main() -> None:
         b_dx = b_alg_spmm(n_rows, e_agg, f_out, weighted=True, f_out=f_in)
         b_dw = 4 * n_rows * (f_in + f_out) + 4 * f_out * (f_in + 1)
         balg = b_fwd + b_dx + b_dw
-        kernel = ("spmm_gemm_kernel", "spmm_gemm_short_kernel", "spmm_gemm_tiny_kernel", "spmm_gemm_fixup_kernel")
+        kernel = ("spmm_gemm_kernel", "spmm_gemm_short_kernel", "spmm_gemm_tiny_kernel", "spmm_gemm_fixup_kernel",
+                  "gemm_tn_ws_kernel", "gemm_tn_finish_kernel")
         ev_ms = [s.elapsed_time(e) for s, e in events]
         per = len(ev_ms) // args.steps if args.steps else 0
         fwd_ms = sum(ev_ms[i] for i in range(0, len(ev_ms), per)) / args.steps if per else None
@@ -533,6 +550,8 @@ def main() -> None:
     traffic, traffic_src = (None, None)
     if world == 1 and train_parts is None:
         traffic, traffic_src = pmc_traffic(args.config, kernel)
+    elif world == 1 and kind == "gcn":
+        traffic, traffic_src = pmc_step_traffic(f"{args.config}_train")
     if world == 1 and not args.train:
         if not args.no_cold:
             # cold layer: CSR + (GCN) norm + schedule + forward from a fresh edge_index,
